@@ -1,0 +1,223 @@
+"""Headline benchmark: quorum commit decisions/s at 64k groups x 5 peers
+(BASELINE.json) and the HBM-roofline fraction of the
+dominant kernel.
+
+One step = one fused replication tick over a fresh, HBM-resident copy of the
+seeded config-#3 state: for each of the G groups the leader gathers an
+AppendEntries per follower (a3), each follower handles it (a4: term check,
+prevLog match, ConflictIndex scan, entry merge/truncate/append, follower
+commit), and the leader folds the P-1 replies in peer order with the
+majority/current-term commit rule (a2 + a1); then GetState words are exported
+(and, with N > 1, all-gathered over RCCL for the shard router, §8e).
+decisions/s = groups x steps / time. Every timed step runs on its own pristine
+copy of the state (a tick mutates the state; re-running it on mutated state
+would be a different, lighter workload).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
+torch.distributed.run (one process per GPU). Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "quorum commit decisions/sec @64k groups×5 peers; % HBM roofline"
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(G_total, P, L, seed, budget_s, rank):
+    """The CPU oracle (C restatement of the Go control flow, incl. the
+    per-message entries copy of raft_append_entry.go:50-54 and a1's downward
+    loop) timed on a bounded sample of the same workload on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle  # test infrastructure: the checker / CPU baseline only
+
+    from multiraft_amd import synth_tick_state
+    Gs = min(8192, G_total)
+    st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gs)
+    threads = max(1, min(16, os.cpu_count() or 1))
+
+    def run(nt, budget):
+        done, spent = 0, 0.0
+        while spent < budget:
+            o = Oracle(Gs, P, L, st)  # fresh copy, untimed
+            t = time.perf_counter()
+            o.replicate_tick(lp, nthreads=nt)
+            spent += time.perf_counter() - t
+            done += Gs
+        return done / spent, done, spent
+
+    v1, d1, s1 = run(1, min(3.0, budget_s / 4))
+    vt, dt, stt = run(threads, budget_s)
+    log(rank, f"cpu baseline: {vt:.4g} decisions/s on {threads} threads, {v1:.4g} on 1 thread")
+    return {"value": vt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle/mraft_oracle.c replicate_tick over groups 0..{Gs - 1} of the same "
+                       f"seeded config-#3 workload ({P} peers, L={L}), fresh state per pass, "
+                       f"{d1 // Gs + dt // Gs} passes; {threads} threads: {dt} decisions in {stt:.2f} s; "
+                       f"1 thread: {v1:.4g} decisions/s; excludes gob persist()/labrpc encoding "
+                       f"the Go reference also pays per handler"),
+            "single_thread_value": v1}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
+    ap.add_argument("--peers", type=int, default=5)
+    ap.add_argument("--log", type=int, default=4096, help="log capacity L")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
+    from multiraft_amd.engine import export_group_status_into, state_sizes
+
+    G, P, L, K, W = args.groups, args.peers, args.log, args.steps, args.warmup
+    G_total = G * world
+    seed = synth_seed(3)
+    t = time.perf_counter()
+    st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=rank * G, g_end=(rank + 1) * G,
+                                 nthreads=min(16, os.cpu_count() or 1))
+    log(rank, f"generated {G}x{P}x{L} state in {time.perf_counter() - t:.1f}s")
+
+    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    del st
+    clone_bytes = sum(v.numel() * 4 for v in master.values())
+    free, _ = torch.cuda.mem_get_info(dev)
+    pool = max(1, min(K + 1, int(free * 0.9 // clone_bytes)))
+    restore = pool < K + 1
+    clones = [{k: v.clone() for k, v in master.items()} for _ in range(pool)]
+    torch.cuda.synchronize()
+    log(rank, f"{pool} state copies of {clone_bytes / 2**30:.2f} GiB each"
+              f"{' (restore inside timed steps)' if restore else ''}")
+
+    eng = Engine(G, P, L, device=local, alloc=False)
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+    lp_d = torch.from_numpy(lp).to(dev)
+    gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
+    commit_d = torch.zeros(G, dtype=torch.int32, device=dev)
+    tl_d = torch.zeros(G, dtype=torch.int32, device=dev)
+    if world > 1:
+        all_c = torch.zeros(G_total, dtype=torch.int32, device=dev)
+        all_t = torch.zeros(G_total, dtype=torch.int32, device=dev)
+
+    # Algorithmic words of one tick on the pristine state.
+    eng.bind(master)
+    rd, wr, active = eng.replicate_tick_count(lp_d, where=DEVICE)
+    algo_bytes = 4 * (rd + wr)
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+
+    def step(i, timed):
+        if restore:  # not enough HBM for a copy per step: restore inside the step
+            c = clones[i % pool]
+            for k in c:
+                c[k].copy_(master[k], non_blocking=True)
+        else:
+            c = clones[i] if timed else clones[K]
+        eng.bind(c)
+        if timed:
+            ev[i][0].record(stream)
+        eng.replicate_tick(lp_d, gf_d, where=DEVICE)
+        if timed:
+            ev[i][1].record(stream)
+        export_group_status_into(eng, lp_d, commit_d, tl_d)
+        if world > 1:
+            dist.all_gather_into_tensor(all_c, commit_d)
+            dist.all_gather_into_tensor(all_t, tl_d)
+
+    for i in range(W):
+        step(i, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        step(i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ker_ms = [a.elapsed_time(b) for a, b in ev]
+    flags = gf_d.cpu().numpy()
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    ker_s = float(np.mean(ker_ms)) / 1e3
+    achieved = algo_bytes / ker_s
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            pm = json.load(open(args.pmc_json))
+            if (pm.get("groups"), pm.get("peers"), pm.get("log")) == (G, P, L):
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": G_total * K / dt,
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": dt / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic: seeded config-#3 generator (include/mraft_synth.h), fresh HBM-resident copy per step",
+        "config": {"workload": "config #3 fused replication tick (a3+a4+a2+a1) + GetState export"
+                               + (" + RCCL all-gather of commit/term words" if world > 1 else ""),
+                   "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
+                   "committed_groups_last_step": int(((flags & 2) != 0).sum()),
+                   "active_groups": active, "restore_in_timed_step": restore},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK,
+                     "traffic": traffic,
+                     "kernel": "k_replicate_tick<5,false>",
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "algorithmic_bytes_per_decision": algo_bytes / max(active, 1),
+                     "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms))},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, args.cpu_seconds, rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,301 @@
+/*
+ * mraft.h — C ABI of libmraft_hip.so, the MI355X-native batched Multi-Raft
+ * decision engine.
+ *
+ * The reference (yusong-yan/MultiRaft, Go) has no FFI: its hot path sits behind
+ * the Go package API of `raft` (src/raft/raft.go:51-104,237-246) and the RPC
+ * handlers dispatched by labrpc reflection (`Raft.HandleAppendEntries`,
+ * `Raft.HandleRequestVote`; src/labrpc/labrpc.go:457-506). Every entry point
+ * below names the reference function it replaces (file:line, relative to the
+ * reference's root). A cgo binding for a Go host is shown in INTEGRATION.md.
+ *
+ * Conventions:
+ *  - Plain C types only; no exceptions cross the boundary. Every function
+ *    returns an int status (MRAFT_OK = 0, negative = API error) and sets a
+ *    thread-local message readable with mraft_last_error_string().
+ *  - Where Go would panic (raft_append_entry.go:41-43, raft_log.go:56-58) the
+ *    engine does not abort: the affected item/group is flagged in a per-item
+ *    (or per-group) error/flag array and left unmodified; the CPU oracle flags
+ *    the same items.
+ *  - All integers are int32 on the device. Go's `int` is 64-bit; values must be
+ *    in [-1, 2^31) and the engine rejects nothing silently.
+ *  - The engine owns its device state (hipMalloc) unless created with
+ *    MRAFT_CREATE_NO_ALLOC and bound to caller-owned device buffers with
+ *    mraft_bind_state(). Batch buffers belong to the caller and are read/written
+ *    only for the duration of the call. `where` says whether batch pointers are
+ *    host (MRAFT_HOST) or device (MRAFT_DEVICE) memory. With MRAFT_DEVICE the
+ *    call is asynchronous on the engine's stream; with MRAFT_HOST it is
+ *    synchronous (results are in the caller's buffers on return).
+ *  - Concurrency: calls on one handle must be serialized by the caller (one
+ *    handle per GPU, one stream per handle). Within a call, items addressed to
+ *    the same replica slot are NOT allowed (the reference serializes them under
+ *    rf.mu, raft.go:17): all but the lowest-indexed such item are rejected with
+ *    MRAFT_ITEM_DUP_SLOT in item_err and the rest are processed. Host-side
+ *    wrappers split batches into rounds of unique slots.
+ *
+ * Data model: G groups x P peers = G*P replica slots,
+ * slot = group*P + peer ("me" of a slot is its peer index). Per slot the Raft
+ * struct fields of raft.go:16-40 are stored struct-of-arrays; the log is a
+ * fixed-capacity array of L terms per slot with slot 0 holding the dummy entry
+ * (raft_log.go:3-12): entry with Index i lives at log[slot*L + (i - dummy)].
+ * Commands never cross the boundary; they stay index-aligned on the host.
+ */
+#ifndef MRAFT_H
+#define MRAFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRAFT_ABI_VERSION 1
+
+/* Node states, raft_rpc.go:8-12 (values preserved). */
+enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
+
+/* Where batch pointers live. */
+enum { MRAFT_HOST = 0, MRAFT_DEVICE = 1 };
+
+/* mraft_create flags */
+enum { MRAFT_CREATE_NO_ALLOC = 1 };
+
+/* Return status codes. */
+enum {
+  MRAFT_OK = 0,
+  MRAFT_E_INVAL = -1,   /* bad argument (null pointer, out-of-range dims)       */
+  MRAFT_E_NOMEM = -2,   /* device allocation failed                             */
+  MRAFT_E_HIP = -3,     /* HIP runtime error                                    */
+  MRAFT_E_NOSTATE = -4  /* engine has no state bound                            */
+};
+
+/* Per-item error codes (int32 item_err[]). Items with a non-zero code leave
+ * the state they would have touched unmodified and produce no reply. */
+enum {
+  MRAFT_ITEM_OK = 0,
+  MRAFT_ITEM_PREV_BEYOND_LAST = 1, /* a3 panic, raft_append_entry.go:41-43          */
+  MRAFT_ITEM_BELOW_DUMMY = 2,      /* convertIndex panic, raft_log.go:56-58         */
+  MRAFT_ITEM_LOG_FULL = 3,         /* append would exceed capacity L (engine limit) */
+  MRAFT_ITEM_NEED_SNAPSHOT = 4,    /* prev < dummy: InstallSnapshot path,
+                                      raft_append_entry.go:27-39 (not an AE)        */
+  MRAFT_ITEM_DUP_SLOT = 5,         /* second item for the same slot in one call    */
+  MRAFT_ITEM_BAD_SLOT = 6,         /* slot/peer out of range                        */
+  MRAFT_ITEM_BAD_STATE = 7         /* commitIndex < dummyIndex (outside the
+                                      reference's reachable states, raft.go:79)    */
+};
+
+/* Per-reply flags written by the fold (int32 out_flags[]). */
+enum {
+  MRAFT_F_NEED_MORE = 1,     /* tryAppendCond[peer].Signal(), raft_append_entry.go:84-86 */
+  MRAFT_F_COMMITTED = 2,     /* applyCond.Signal(): commitIndex advanced, :99-100        */
+  MRAFT_F_STEPPED_DOWN = 4,  /* adopted a higher term and became follower, :67-72        */
+  MRAFT_F_BECAME_LEADER = 8, /* vote tally reached a majority, raft_election.go:32-38   */
+  MRAFT_F_APPLIED = 16       /* the reply passed the term/state/prev gate, :73-74       */
+};
+
+/* Per-group flags written by mraft_replicate_tick (int32 group_flags[G]). */
+enum {
+  MRAFT_G_ACTIVE = 1,        /* the leader replica was a leader and sent AEs          */
+  MRAFT_G_COMMITTED = 2,     /* leader commitIndex advanced                            */
+  MRAFT_G_STEPPED_DOWN = 4,  /* leader stepped down on a higher reply term             */
+  MRAFT_G_NEED_SNAPSHOT = 8, /* some peer needs InstallSnapshot (prev < dummy)         */
+  MRAFT_G_ERROR = 16,        /* a3 would panic / bad state / log full: group skipped   */
+  MRAFT_G_FOLLOWER_COMMIT = 32, /* some follower advanced its commitIndex              */
+  MRAFT_G_LOG_FULL = 64      /* a follower rejected its AE with MRAFT_ITEM_LOG_FULL    */
+};
+
+/* Per-slot state, struct-of-arrays (raft.go:16-40). Arrays of G*P int32 unless
+ * noted. Any pointer may be NULL in mraft_store_state to skip that array. */
+typedef struct {
+  int32_t *current_term;  /* currentTerm                                    */
+  int32_t *voted_for;     /* votedFor (-1 = none)                           */
+  int32_t *state;         /* MRAFT_LEADER / CANDIDATE / FOLLOWER            */
+  int32_t *commit_index;  /* commitIndex                                    */
+  int32_t *last_applied;  /* lastApplied                                    */
+  int32_t *dummy_index;   /* logs[0].Index (snapshot base), raft_log.go:33  */
+  int32_t *last_index;    /* logs[len-1].Index, raft_log.go:44-46           */
+  int32_t *granted_votes; /* StartElection's grantedVotes closure counter   */
+  int32_t *log_term;      /* [G*P*L] log[slot*L + (Index - dummy)] = Term   */
+  int32_t *match_index;   /* [G*P*P] matchIndex[slot*P + peer]              */
+  int32_t *next_index;    /* [G*P*P] nextIndex[slot*P + peer]               */
+} mraft_soa;
+
+/* AppendEntriesArgs, raft_rpc.go:55-62. Entries are passed by reference:
+ * entry k (0 <= k < n_entries) has Index prev_log_index+1+k (as built by
+ * appendOneRound, raft_append_entry.go:50-54) and Term
+ * entry_terms[entries_offset + k]. `slot` is the receiving replica. */
+typedef struct {
+  int32_t slot;
+  int32_t term;
+  int32_t leader_id;
+  int32_t prev_log_index;
+  int32_t prev_log_term;
+  int32_t leader_commit;
+  int32_t n_entries;
+  int32_t _pad;
+  int64_t entries_offset;
+} mraft_ae_args;
+
+/* AppendEntriesReply, raft_rpc.go:64-69 (`Conflict` is never set by the
+ * reference and is always 0 here). */
+typedef struct {
+  int32_t term;
+  int32_t success;
+  int32_t conflict_index;
+  int32_t conflict;
+} mraft_ae_reply;
+
+/* One AppendEntries reply delivered back to a leader replica, together with
+ * the fields of the args it answers that processAppendEntriesReply reads
+ * (raft_append_entry.go:66-88). */
+typedef struct {
+  int32_t slot;          /* leader replica                           */
+  int32_t peer;          /* replying follower (0..P-1)               */
+  int32_t args_term;
+  int32_t args_prev_log_index;
+  int32_t args_n_entries;
+  int32_t reply_term;
+  int32_t reply_success;
+  int32_t reply_conflict_index;
+} mraft_ae_result;
+
+/* RequestVoteArgs, raft_rpc.go:71-76; `slot` is the receiving voter. */
+typedef struct {
+  int32_t slot;
+  int32_t candidate_id;
+  int32_t term;
+  int32_t last_log_index;
+  int32_t last_log_term;
+} mraft_rv_args;
+
+/* RequestVoteReply, raft_rpc.go:78-82 (`State` is never written: omitted). */
+typedef struct {
+  int32_t term;
+  int32_t vote_granted;
+} mraft_rv_reply;
+
+/* One RequestVote reply delivered back to a candidate replica with the args
+ * term it answers (raft_election.go:22-47). */
+typedef struct {
+  int32_t slot;       /* candidate replica */
+  int32_t peer;       /* voter             */
+  int32_t args_term;
+  int32_t reply_term;
+  int32_t vote_granted;
+} mraft_rv_result;
+
+typedef struct mraft_engine mraft_engine;
+
+/* ---- lifetime ---------------------------------------------------------- */
+
+/* Replaces Make (raft.go:51-87) for G groups x P peers at once: allocates the
+ * device SoA (unless MRAFT_CREATE_NO_ALLOC) and initialises every slot as Make
+ * does: Follower, term 0, votedFor -1, dummy entry {0,0}, commit = lastApplied
+ * = dummyIndex. peers in [1, 8]; log_capacity >= 1. */
+int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity,
+                 int32_t device, uint32_t flags, mraft_engine **out);
+/* Replaces Kill (utility.go:9-19): frees device state owned by the engine. */
+int mraft_destroy(mraft_engine *h);
+/* Use a caller-provided hipStream_t (NULL = the engine's own stream). */
+int mraft_set_stream(mraft_engine *h, void *hip_stream);
+void *mraft_get_stream(mraft_engine *h);
+int mraft_synchronize(mraft_engine *h);
+int mraft_dims(const mraft_engine *h, int32_t *groups, int32_t *peers,
+               int32_t *log_capacity);
+const char *mraft_last_error_string(void);
+int mraft_abi_version(void);
+
+/* ---- state transfer (readPersist / SaveState analogues, raft.go:205-235) --- */
+
+/* Copy a full state image into / out of the engine. All arrays required for
+ * load; NULL entries are skipped on store. */
+int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where);
+int mraft_store_state(mraft_engine *h, const mraft_soa *dst, int32_t where);
+/* Device pointers of the state the engine currently works on (zero-copy). */
+int mraft_state_view(mraft_engine *h, mraft_soa *out_device_ptrs);
+/* Bind caller-owned device buffers (all required) as the working state. */
+int mraft_bind_state(mraft_engine *h, const mraft_soa *device_ptrs);
+
+/* ---- hot path: replication & commit ----------- */
+
+/* a3, appendOneRound's args gather (raft_append_entry.go:20-54) for n
+ * (slot, peer) pairs: fills args (entries by reference into the leader's own
+ * log: entries_offset indexes the engine's log_term array, see
+ * mraft_state_view) and item_err (NEED_SNAPSHOT, PREV_BEYOND_LAST, or
+ * MRAFT_ITEM_BAD_STATE when the slot is not a leader — appendOneRound returns
+ * without sending, :22-25). */
+int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
+                             const int32_t *peers, int64_t n,
+                             mraft_ae_args *out_args, int32_t *item_err,
+                             int32_t where);
+
+/* a4, HandleAppendEntries (raft_append_entry.go:108-162 with matchLog,
+ * raft_log.go:92-96) for n items at distinct slots. entry_terms holds the
+ * entries' terms (n_entry_terms words; pass NULL to read entries from the
+ * engine's own log_term array, as produced by mraft_gather_append_args). */
+int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
+                                int64_t n, const int32_t *entry_terms,
+                                int64_t n_entry_terms, mraft_ae_reply *replies,
+                                int32_t *item_err, int32_t where);
+
+/* a2 + a1, processAppendEntriesReply + advanceCommitIndexForLeader
+ * (raft_append_entry.go:66-105). Items are folded per segment in array order;
+ * segment s = items [seg_begin[s], seg_begin[s+1]) all with the same leader
+ * slot (distinct across segments). seg_begin == NULL means one item per
+ * segment. out_flags[i] gets MRAFT_F_* bits for item i. */
+int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items,
+                                 int64_t n, const int64_t *seg_begin,
+                                 int64_t n_seg, int32_t *out_flags,
+                                 int32_t *item_err, int32_t where);
+
+/* Fused co-resident tick: for every group g with leader_peer[g] >= 0, the
+ * leader replica gathers AppendEntries for every other peer (a3), each
+ * follower replica handles it (a4, entries read in place from the leader's
+ * log), and the leader folds the replies in peer order (a2 + a1). Equivalent
+ * to the sequence gather -> handle -> process on the same state.
+ * group_flags (optional, [G]) gets MRAFT_G_* bits. */
+int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer,
+                         int32_t *group_flags, int32_t where);
+
+/* Algorithmic word count of one mraft_replicate_tick on the current state
+ * (DESIGN.md §4 definition; does not modify state): out_words[0] = words
+ * read, out_words[1] = words written, out_words[2] = active groups. */
+int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer,
+                               int64_t out_words[3], int32_t where);
+
+/* ---- elections ------------------------------- */
+
+/* StartElection (raft_election.go:4-15): state=Candidate, term++,
+ * votedFor=me, grantedVotes=1, args from lastEntry (raft_log.go:50-53). */
+int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n,
+                         mraft_rv_args *out_args, int32_t *item_err,
+                         int32_t where);
+
+/* HandleRequestVote (raft_election.go:54-77 with isLogUpToDate,
+ * raft_log.go:99-104) for n items at distinct voter slots. */
+int mraft_handle_request_vote(mraft_engine *h, const mraft_rv_args *args,
+                              int64_t n, mraft_rv_reply *replies,
+                              int32_t *item_err, int32_t where);
+
+/* Vote tally closure (raft_election.go:22-47), segments as in
+ * mraft_process_append_replies. On majority: Leader, matchIndex[*]=0,
+ * nextIndex[*]=lastIndex+1 (:30-38). */
+int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items,
+                               int64_t n, const int64_t *seg_begin,
+                               int64_t n_seg, int32_t *out_flags,
+                               int32_t *item_err, int32_t where);
+
+/* ---- read-out (GetState, raft.go:237-246) -------------------------------- */
+
+/* For each group g and its replica leader_peer[g] (or, with leader_peer NULL,
+ * replica 0): commit[g] = commitIndex, term_leader[g] = currentTerm<<1 |
+ * (state == Leader). These are the words the multi-GPU path all-gathers. */
+int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer,
+                              int32_t *commit, int32_t *term_leader,
+                              int32_t where);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MRAFT_H */

@@ -1,0 +1,491 @@
+// mraft_abi.hip — the extern "C" boundary of libmraft_hip.so (include/mraft.h).
+//
+// Host side of the engine: device state ownership (one HBM-resident SoA image
+// per handle), staging of host batches, duplicate-slot claims and kernel
+// launches on the handle's stream. No exception or C++ type crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mraft.h"
+#include "mraft_device.h"
+#include "mraft_internal.h"
+
+struct mraft_engine {
+  int32_t G = 0, P = 0, L = 0, device = 0;
+  bool owned = false, bound = false;
+  mraft_soa dev{};
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  unsigned long long *claim = nullptr;
+  uint32_t epoch = 0;
+  std::vector<void *> scratch_ptr;
+  std::vector<size_t> scratch_cap;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(MRAFT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));          \
+  } while (0)
+
+int64_t gp_of(const mraft_engine *h) { return (int64_t)h->G * h->P; }
+
+mraft::Dev dev_of(const mraft_engine *h) {
+  mraft::Dev d;
+  d.term = h->dev.current_term; d.voted = h->dev.voted_for; d.role = h->dev.state;
+  d.commit = h->dev.commit_index; d.applied = h->dev.last_applied; d.dummy = h->dev.dummy_index;
+  d.last = h->dev.last_index; d.votes = h->dev.granted_votes; d.log = h->dev.log_term;
+  d.match = h->dev.match_index; d.next = h->dev.next_index;
+  d.G = h->G; d.P = h->P; d.L = h->L;
+  return d;
+}
+
+// Array table: pointer-to-member + element count.
+struct ArrDesc { int32_t *mraft_soa::*ptr; int kind; };  // kind 0: G*P, 1: G*P*L, 2: G*P*P
+const ArrDesc kArrays[] = {
+    {&mraft_soa::current_term, 0}, {&mraft_soa::voted_for, 0},   {&mraft_soa::state, 0},
+    {&mraft_soa::commit_index, 0}, {&mraft_soa::last_applied, 0}, {&mraft_soa::dummy_index, 0},
+    {&mraft_soa::last_index, 0},   {&mraft_soa::granted_votes, 0}, {&mraft_soa::log_term, 1},
+    {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2}};
+
+size_t arr_bytes(const mraft_engine *h, int kind) {
+  int64_t gp = gp_of(h);
+  int64_t n = kind == 0 ? gp : kind == 1 ? gp * h->L : gp * h->P;
+  return (size_t)n * sizeof(int32_t);
+}
+
+int check(const mraft_engine *h) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (!h->bound) return fail(MRAFT_E_NOSTATE, "engine has no device state bound");
+  return MRAFT_OK;
+}
+
+// Grow-only device scratch slot `idx`.
+int scratch(mraft_engine *h, size_t idx, size_t bytes, void **out) {
+  if (h->scratch_ptr.size() <= idx) {
+    h->scratch_ptr.resize(idx + 1, nullptr);
+    h->scratch_cap.resize(idx + 1, 0);
+  }
+  if (bytes == 0) bytes = 16;
+  if (h->scratch_cap[idx] < bytes) {
+    if (h->scratch_ptr[idx]) {
+      HIP_TRY(hipStreamSynchronize(h->stream));
+      HIP_TRY(hipFree(h->scratch_ptr[idx]));
+    }
+    h->scratch_ptr[idx] = nullptr;
+    h->scratch_cap[idx] = 0;
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(MRAFT_E_NOMEM, "scratch alloc of %zu B failed", bytes);
+    h->scratch_ptr[idx] = p;
+    h->scratch_cap[idx] = bytes;
+  }
+  *out = h->scratch_ptr[idx];
+  return MRAFT_OK;
+}
+
+// Batch pointer staging: for MRAFT_HOST, input buffers are copied to device
+// scratch and output buffers are copied back by finish().
+struct Stage {
+  mraft_engine *h;
+  bool host;
+  size_t next_slot = 0;
+  struct Out { void *host; void *dev; size_t bytes; };
+  std::vector<Out> outs;
+  Stage(mraft_engine *hh, int32_t where) : h(hh), host(where == MRAFT_HOST) {}
+
+  // in: read by the kernel; out: written by the kernel; both: read and written.
+  int map(const void *p, size_t bytes, bool in, bool out, void **dptr) {
+    if (!p) { *dptr = nullptr; return MRAFT_OK; }
+    if (!host) { *dptr = const_cast<void *>(p); return MRAFT_OK; }
+    void *d = nullptr;
+    int rc = scratch(h, 8 + next_slot++, bytes, &d);
+    if (rc) return rc;
+    if (in && bytes) HIP_TRY(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, h->stream));
+    if (out) outs.push_back({const_cast<void *>(p), d, bytes});
+    *dptr = d;
+    return MRAFT_OK;
+  }
+  int finish() {
+    HIP_TRY(hipGetLastError());
+    if (!host) return MRAFT_OK;
+    for (auto &o : outs)
+      if (o.bytes) HIP_TRY(hipMemcpyAsync(o.host, o.dev, o.bytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MRAFT_OK;
+  }
+};
+
+#define TRY(expr)          \
+  do {                     \
+    int rc_ = (expr);      \
+    if (rc_) return rc_;   \
+  } while (0)
+
+int ensure_claim(mraft_engine *h) {
+  if (!h->claim) {
+    size_t b = (size_t)gp_of(h) * sizeof(unsigned long long);
+    if (hipMalloc(&h->claim, b) != hipSuccess) return fail(MRAFT_E_NOMEM, "claim alloc failed");
+    HIP_TRY(hipMemsetAsync(h->claim, 0, b, h->stream));
+  }
+  if (++h->epoch == 0) {  // wrapped: reset
+    HIP_TRY(hipMemsetAsync(h->claim, 0, (size_t)gp_of(h) * sizeof(unsigned long long), h->stream));
+    h->epoch = 1;
+  }
+  return MRAFT_OK;
+}
+
+void free_owned(mraft_engine *h) {
+  if (!h->owned) return;
+  for (const auto &a : kArrays) {
+    int32_t *p = h->dev.*(a.ptr);
+    if (p) (void)hipFree(p);
+    h->dev.*(a.ptr) = nullptr;
+  }
+  h->owned = false;
+  h->bound = false;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mraft_last_error_string(void) { return g_err.c_str(); }
+int mraft_abi_version(void) { return MRAFT_ABI_VERSION; }
+
+int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t device,
+                 uint32_t flags, mraft_engine **out) {
+  if (!out) return fail(MRAFT_E_INVAL, "out is null");
+  *out = nullptr;
+  if (groups < 1 || peers < 1 || peers > 8 || log_capacity < 1)
+    return fail(MRAFT_E_INVAL, "bad dims G=%d P=%d L=%d (need G>=1, 1<=P<=8, L>=1)", groups, peers,
+                log_capacity);
+  if ((int64_t)groups * peers > INT32_MAX)
+    return fail(MRAFT_E_INVAL, "G*P must fit in int32");
+  HIP_TRY(hipSetDevice(device));
+  mraft_engine *h = new mraft_engine();
+  h->G = groups; h->P = peers; h->L = log_capacity; h->device = device;
+  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return fail(MRAFT_E_HIP, "hipStreamCreate failed");
+  }
+  h->stream = h->own_stream;
+  if (!(flags & MRAFT_CREATE_NO_ALLOC)) {
+    h->owned = true;
+    for (const auto &a : kArrays) {
+      int32_t *p = nullptr;
+      if (hipMalloc(&p, arr_bytes(h, a.kind)) != hipSuccess) {
+        free_owned(h);
+        (void)hipStreamDestroy(h->own_stream);
+        delete h;
+        return fail(MRAFT_E_NOMEM, "device state allocation failed (G=%d P=%d L=%d)", groups, peers,
+                    log_capacity);
+      }
+      h->dev.*(a.ptr) = p;
+    }
+    h->bound = true;
+    (void)hipMemsetAsync(h->dev.log_term, 0, arr_bytes(h, 1), h->stream);
+    (void)hipMemsetAsync(h->dev.match_index, 0, arr_bytes(h, 2), h->stream);
+    (void)hipMemsetAsync(h->dev.next_index, 0, arr_bytes(h, 2), h->stream);
+    mraft::launch_init_state(dev_of(h), h->stream);
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+      free_owned(h);
+      (void)hipStreamDestroy(h->own_stream);
+      delete h;
+      return fail(MRAFT_E_HIP, "init failed: %s", hipGetErrorString(e));
+    }
+  }
+  *out = h;
+  return MRAFT_OK;
+}
+
+int mraft_destroy(mraft_engine *h) {
+  if (!h) return MRAFT_OK;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  free_owned(h);
+  for (void *p : h->scratch_ptr)
+    if (p) (void)hipFree(p);
+  if (h->claim) (void)hipFree(h->claim);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  delete h;
+  return MRAFT_OK;
+}
+
+int mraft_set_stream(mraft_engine *h, void *stream) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  h->stream = stream ? (hipStream_t)stream : h->own_stream;
+  return MRAFT_OK;
+}
+
+void *mraft_get_stream(mraft_engine *h) { return h ? (void *)h->stream : nullptr; }
+
+int mraft_synchronize(mraft_engine *h) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MRAFT_OK;
+}
+
+int mraft_dims(const mraft_engine *h, int32_t *g, int32_t *p, int32_t *l) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (g) *g = h->G;
+  if (p) *p = h->P;
+  if (l) *l = h->L;
+  return MRAFT_OK;
+}
+
+int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where) {
+  TRY(check(h));
+  if (!src) return fail(MRAFT_E_INVAL, "src is null");
+  HIP_TRY(hipSetDevice(h->device));
+  const hipMemcpyKind k = where == MRAFT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+  for (const auto &a : kArrays)
+    if (!(src->*(a.ptr))) return fail(MRAFT_E_INVAL, "load_state: every array is required");
+  for (const auto &a : kArrays)
+    HIP_TRY(hipMemcpyAsync(h->dev.*(a.ptr), src->*(a.ptr), arr_bytes(h, a.kind), k, h->stream));
+  if (where == MRAFT_HOST) HIP_TRY(hipStreamSynchronize(h->stream));
+  return MRAFT_OK;
+}
+
+int mraft_store_state(mraft_engine *h, const mraft_soa *dst, int32_t where) {
+  TRY(check(h));
+  if (!dst) return fail(MRAFT_E_INVAL, "dst is null");
+  HIP_TRY(hipSetDevice(h->device));
+  const hipMemcpyKind k = where == MRAFT_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+  for (const auto &a : kArrays)
+    if (dst->*(a.ptr))
+      HIP_TRY(hipMemcpyAsync(dst->*(a.ptr), h->dev.*(a.ptr), arr_bytes(h, a.kind), k, h->stream));
+  if (where == MRAFT_HOST) HIP_TRY(hipStreamSynchronize(h->stream));
+  return MRAFT_OK;
+}
+
+int mraft_state_view(mraft_engine *h, mraft_soa *out) {
+  TRY(check(h));
+  if (!out) return fail(MRAFT_E_INVAL, "out is null");
+  *out = h->dev;
+  return MRAFT_OK;
+}
+
+int mraft_bind_state(mraft_engine *h, const mraft_soa *d) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (!d) return fail(MRAFT_E_INVAL, "state is null");
+  for (const auto &a : kArrays)
+    if (!(d->*(a.ptr))) return fail(MRAFT_E_INVAL, "bind_state: every array is required");
+  if (h->owned) {
+    (void)hipStreamSynchronize(h->stream);
+    free_owned(h);
+  }
+  h->dev = *d;
+  h->bound = true;
+  return MRAFT_OK;
+}
+
+// ---------------------------------------------------------------- hot path
+
+int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer, int32_t *group_flags,
+                         int32_t where) {
+  TRY(check(h));
+  if (!leader_peer) return fail(MRAFT_E_INVAL, "leader_peer is null");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *lp, *gf;
+  TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
+  TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
+  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, h->stream);
+  return sg.finish();
+}
+
+int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer, int64_t out_words[3],
+                               int32_t where) {
+  TRY(check(h));
+  if (!leader_peer || !out_words) return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *lp, *cnt;
+  TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
+  TRY(scratch(h, 0, 3 * sizeof(unsigned long long), &cnt));
+  HIP_TRY(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), h->stream));
+  mraft::launch_replicate_tick_count(dev_of(h), (const int32_t *)lp, (unsigned long long *)cnt,
+                                     h->stream);
+  HIP_TRY(hipGetLastError());
+  unsigned long long hc[3];
+  HIP_TRY(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  for (int i = 0; i < 3; ++i) out_words[i] = (int64_t)hc[i];
+  return MRAFT_OK;
+}
+
+int mraft_gather_append_args(mraft_engine *h, const int32_t *slots, const int32_t *peers,
+                             int64_t n, mraft_ae_args *out_args, int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !peers || !out_args || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *s, *p, *o, *e;
+  TRY(sg.map(slots, sizeof(int32_t) * n, true, false, &s));
+  TRY(sg.map(peers, sizeof(int32_t) * n, true, false, &p));
+  TRY(sg.map(out_args, sizeof(mraft_ae_args) * n, false, true, &o));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_gather_args(dev_of(h), (const int32_t *)s, (const int32_t *)p, n,
+                            (mraft_ae_args *)o, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int64_t n,
+                                const int32_t *entry_terms, int64_t n_entry_terms,
+                                mraft_ae_reply *replies, int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *a, *en, *r, *e;
+  TRY(sg.map(args, sizeof(mraft_ae_args) * n, true, false, &a));
+  TRY(sg.map(entry_terms, sizeof(int32_t) * (size_t)(entry_terms ? n_entry_terms : 0), true, false,
+             &en));
+  TRY(sg.map(replies, sizeof(mraft_ae_reply) * n, false, true, &r));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  const int32_t *src = en ? (const int32_t *)en : h->dev.log_term;
+  const int64_t src_n = en ? n_entry_terms : gp_of(h) * h->L;
+  mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h),
+                      h->P, h->claim, h->epoch, (int32_t *)e, h->stream);
+  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (mraft_ae_reply *)r,
+                          (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, int64_t n,
+                                 const int64_t *seg_begin, int64_t n_seg, int32_t *out_flags,
+                                 int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
+  if (n == 0) return MRAFT_OK;
+  const int64_t ns = seg_begin ? n_seg : n;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *it, *sb, *fl, *e, *se;
+  TRY(sg.map(items, sizeof(mraft_ae_result) * n, true, false, &it));
+  TRY(sg.map(seg_begin, sizeof(int64_t) * (size_t)(seg_begin ? n_seg + 1 : 0), true, false, &sb));
+  TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &fl));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
+  HIP_TRY(hipMemsetAsync(fl, 0, sizeof(int32_t) * n, h->stream));
+  HIP_TRY(hipMemsetAsync(e, 0, sizeof(int32_t) * n, h->stream));
+  mraft::launch_claim(it, ns, sizeof(mraft_ae_result), offsetof(mraft_ae_result, slot),
+                      (const int64_t *)sb, gp_of(h), h->P, h->claim, h->epoch, (int32_t *)se,
+                      h->stream);
+  mraft::launch_fold(dev_of(h), (const mraft_ae_result *)it, n, (const int64_t *)sb, ns,
+                     (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n, mraft_rv_args *out_args,
+                         int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !out_args || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *s, *o, *e;
+  TRY(sg.map(slots, sizeof(int32_t) * n, true, false, &s));
+  TRY(sg.map(out_args, sizeof(mraft_rv_args) * n, false, true, &o));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_claim(s, n, sizeof(int32_t), 0, nullptr, gp_of(h), h->P, h->claim, h->epoch,
+                      (int32_t *)e, h->stream);
+  mraft::launch_start_election(dev_of(h), (const int32_t *)s, n, (mraft_rv_args *)o, (int32_t *)e,
+                               h->stream);
+  return sg.finish();
+}
+
+int mraft_handle_request_vote(mraft_engine *h, const mraft_rv_args *args, int64_t n,
+                              mraft_rv_reply *replies, int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *a, *r, *e;
+  TRY(sg.map(args, sizeof(mraft_rv_args) * n, true, false, &a));
+  TRY(sg.map(replies, sizeof(mraft_rv_reply) * n, false, true, &r));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_claim(a, n, sizeof(mraft_rv_args), offsetof(mraft_rv_args, slot), nullptr, gp_of(h),
+                      h->P, h->claim, h->epoch, (int32_t *)e, h->stream);
+  mraft::launch_handle_rv(dev_of(h), (const mraft_rv_args *)a, n, (mraft_rv_reply *)r, (int32_t *)e,
+                          h->stream);
+  return sg.finish();
+}
+
+int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items, int64_t n,
+                               const int64_t *seg_begin, int64_t n_seg, int32_t *out_flags,
+                               int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
+  if (n == 0) return MRAFT_OK;
+  const int64_t ns = seg_begin ? n_seg : n;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *it, *sb, *fl, *e, *se;
+  TRY(sg.map(items, sizeof(mraft_rv_result) * n, true, false, &it));
+  TRY(sg.map(seg_begin, sizeof(int64_t) * (size_t)(seg_begin ? n_seg + 1 : 0), true, false, &sb));
+  TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &fl));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
+  HIP_TRY(hipMemsetAsync(fl, 0, sizeof(int32_t) * n, h->stream));
+  HIP_TRY(hipMemsetAsync(e, 0, sizeof(int32_t) * n, h->stream));
+  mraft::launch_claim(it, ns, sizeof(mraft_rv_result), offsetof(mraft_rv_result, slot),
+                      (const int64_t *)sb, gp_of(h), h->P, h->claim, h->epoch, (int32_t *)se,
+                      h->stream);
+  mraft::launch_tally(dev_of(h), (const mraft_rv_result *)it, n, (const int64_t *)sb, ns,
+                      (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer, int32_t *commit,
+                              int32_t *term_leader, int32_t where) {
+  TRY(check(h));
+  if (!commit || !term_leader) return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *lp, *c, *t;
+  TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
+  TRY(sg.map(commit, sizeof(int32_t) * h->G, false, true, &c));
+  TRY(sg.map(term_leader, sizeof(int32_t) * h->G, false, true, &t));
+  mraft::launch_export(dev_of(h), (const int32_t *)lp, (int32_t *)c, (int32_t *)t, h->stream);
+  return sg.finish();
+}
+
+}  // extern "C"

@@ -1,0 +1,134 @@
+// mraft_device.h — device-side building blocks shared by the gfx950 kernels.
+//
+// Wave-cooperative primitives (64-lane wavefronts, 64-bit ballots) used by the
+// AppendEntries follower path and the leader's commit scan:
+//  * wave_conflict_scan — the ConflictIndex backward scan of
+//    raft_append_entry.go:136-142, 256 terms per iteration (4 coalesced
+//    dword loads per lane in flight), first mismatch by ballot + find-first-set;
+//  * wave_merge_compare — the entry merge of :149-155: compares the entries'
+//    terms with the follower's log 256 at a time, first mismatch by ballot;
+//  * wave_copy — truncate-and-append (raft_log.go:62-75) as a streaming copy
+//    of the leader's tail into the follower's log;
+//  * wave_commit_scan — the term gate of advanceCommitIndexForLeader
+//    (:89-105): highest index in a range whose term equals currentTerm.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mraft {
+
+constexpr int kLeader = 1, kCandidate = 2, kFollower = 3;  // raft_rpc.go:8-12
+constexpr int kWave = 64;
+constexpr int kUnroll = 4;                 // loads in flight per lane per stream
+constexpr int kChunk = kWave * kUnroll;    // terms per wave iteration
+
+struct Dev {
+  int32_t *term, *voted, *role, *commit, *applied, *dummy, *last, *votes;
+  int32_t *log, *match, *next;
+  int32_t G, P, L;
+};
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ int first_lane(unsigned long long m) { return __ffsll((long long)m) - 1; }
+
+// Largest idx in [lo, hi] with row[idx - base] != a, scanning downward; returns
+// lo - 1 when every term in the range equals a. Wave-uniform arguments.
+__device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base,
+                                                 int lo, int hi, int a) {
+  const int lane = lane_id();
+  for (int top = hi; top >= lo; top -= kChunk) {
+    int v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      int idx = top - lane - kWave * u;
+      v[u] = idx >= lo ? row[idx - base] : a;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      unsigned long long m = __ballot(v[u] != a);
+      if (m) return top - kWave * u - first_lane(m);
+    }
+  }
+  return lo - 1;
+}
+
+// Largest idx in [lo, hi] with row[idx - base] == a; lo - 1 if none.
+__device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row, int base,
+                                                 int lo, int hi, int a) {
+  const int lane = lane_id();
+  for (int top = hi; top >= lo; top -= kChunk) {
+    int v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      int idx = top - lane - kWave * u;
+      v[u] = idx >= lo ? row[idx - base] : a + 1;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      unsigned long long m = __ballot(v[u] == a);
+      if (m) return top - kWave * u - first_lane(m);
+    }
+  }
+  return lo - 1;
+}
+
+// ConflictIndex of raft_append_entry.go:136-142 for prev > dummy + 1, where
+// a = term(prev): the largest index in [dummy+2, prev-1] whose term differs
+// from a, else dummy + 1.
+__device__ __forceinline__ int wave_conflict_scan(const int32_t *__restrict__ frow, int fdummy,
+                                                  int prev, int a) {
+  int r = wave_scan_down_ne(frow, fdummy, fdummy + 2, prev - 1, a);
+  return r < fdummy + 2 ? fdummy + 1 : r;
+}
+
+// First k in [0, kc) with E[k] != F[k]; -1 if none.
+__device__ __forceinline__ int wave_merge_compare(const int32_t *__restrict__ E,
+                                                  const int32_t *__restrict__ F, int kc) {
+  const int lane = lane_id();
+  for (int base = 0; base < kc; base += kChunk) {
+    int e[kUnroll], f[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      int k = base + lane + kWave * u;
+      e[u] = k < kc ? E[k] : 0;
+      f[u] = k < kc ? F[k] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      unsigned long long m = __ballot(e[u] != f[u]);
+      if (m) return base + kWave * u + first_lane(m);
+    }
+  }
+  return -1;
+}
+
+// F[k] = E[k] for k in [0, cnt).
+__device__ __forceinline__ void wave_copy(const int32_t *__restrict__ E, int32_t *__restrict__ F,
+                                          int cnt) {
+  const int lane = lane_id();
+  for (int base = 0; base < cnt; base += kChunk) {
+    int v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      int k = base + lane + kWave * u;
+      v[u] = k < cnt ? E[k] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      int k = base + lane + kWave * u;
+      if (k < cnt) F[k] = v[u];
+    }
+  }
+}
+
+__device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace mraft

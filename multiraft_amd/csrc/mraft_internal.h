@@ -1,0 +1,41 @@
+// mraft_internal.h — launchers shared between the kernel translation units and
+// the C-ABI implementation (mraft_abi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mraft.h"
+#include "mraft_device.h"
+
+namespace mraft {
+
+void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, hipStream_t st);
+void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,
+                                 hipStream_t st);
+
+void launch_init_state(const Dev &s, hipStream_t st);
+
+// Duplicate-slot claims: item i (slot read at byte offset slot_off of a record
+// of `stride` bytes; or, with seg_begin, the slot of segment i's first item)
+// wins iff it is the lowest index addressing its slot in this call.
+void launch_claim(const void *items, int64_t n, int stride, int slot_off, const int64_t *seg_begin,
+                  int64_t gp, int peers, unsigned long long *claim, uint32_t epoch, int32_t *err,
+                  hipStream_t st);
+
+void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
+                        mraft_ae_args *out, int32_t *err, hipStream_t st);
+void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
+                      int64_t n_ent, mraft_ae_reply *rep, int32_t *err, hipStream_t st);
+void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
+                 int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err, hipStream_t st);
+void launch_start_election(const Dev &s, const int32_t *slots, int64_t n, mraft_rv_args *out,
+                           int32_t *err, hipStream_t st);
+void launch_handle_rv(const Dev &s, const mraft_rv_args *args, int64_t n, mraft_rv_reply *rep,
+                      int32_t *err, hipStream_t st);
+void launch_tally(const Dev &s, const mraft_rv_result *items, int64_t n, const int64_t *seg_begin,
+                  int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
+                  hipStream_t st);
+void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t *term_leader,
+                   hipStream_t st);
+
+}  // namespace mraft

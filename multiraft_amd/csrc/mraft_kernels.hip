@@ -1,0 +1,482 @@
+// mraft_kernels.hip — item-level gfx950 kernels behind the C ABI: the
+// per-message entry points of include/mraft.h (a node receiving batches of
+// AppendEntries / RequestVote / replies from the network), as
+// opposed to the fused co-resident tick of mraft_tick.hip.
+#include "mraft_device.h"
+#include "mraft_internal.h"
+
+namespace mraft {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int blocks_for(int64_t n, int per_block = kBlock) {
+  int64_t b = (n + per_block - 1) / per_block;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// ---------------------------------------------------------------- Make
+__global__ void k_init_state(Dev s) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < gp;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    // raft.go:53-68,79-80: Follower, term 0, votedFor -1, logs = [dummy{0,0}],
+    // commitIndex = lastApplied = dummyIndex.
+    s.term[i] = 0; s.voted[i] = -1; s.role[i] = kFollower; s.commit[i] = 0; s.applied[i] = 0;
+    s.dummy[i] = 0; s.last[i] = 0; s.votes[i] = 0;
+  }
+}
+
+// ---------------------------------------------------------------- claims
+__global__ void k_claim(const char *__restrict__ items, int64_t n, int stride, int slot_off,
+                        const int64_t *__restrict__ seg_begin, int64_t gp, int peers,
+                        unsigned long long *__restrict__ claim, uint32_t epoch,
+                        int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t rec = i;
+  if (seg_begin) {
+    if (seg_begin[i] >= seg_begin[i + 1]) { err[i] = 0; return; }
+    rec = seg_begin[i];
+  }
+  const int32_t slot = *(const int32_t *)(items + rec * stride + slot_off);
+  (void)peers;
+  if (slot < 0 || slot >= gp) { err[i] = MRAFT_ITEM_BAD_SLOT; return; }
+  err[i] = 0;
+  atomicMax(&claim[slot], ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i));
+}
+
+__global__ void k_claim_check(const char *__restrict__ items, int64_t n, int stride, int slot_off,
+                              const int64_t *__restrict__ seg_begin,
+                              const unsigned long long *__restrict__ claim, uint32_t epoch,
+                              int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n || err[i]) return;
+  int64_t rec = i;
+  if (seg_begin) {
+    if (seg_begin[i] >= seg_begin[i + 1]) return;
+    rec = seg_begin[i];
+  }
+  const int32_t slot = *(const int32_t *)(items + rec * stride + slot_off);
+  if (claim[slot] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i)))
+    err[i] = MRAFT_ITEM_DUP_SLOT;
+}
+
+// ---------------------------------------------------------------- a3
+__global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
+                              const int32_t *__restrict__ peers, int64_t n,
+                              mraft_ae_args *__restrict__ out, int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int P = s.P, L = s.L;
+  const int64_t gp = (int64_t)s.G * P;
+  mraft_ae_args a = {};
+  int e = 0;
+  const int slot = slots[i], peer = peers[i];
+  if (slot < 0 || slot >= gp || peer < 0 || peer >= P || peer == slot % P) {
+    e = MRAFT_ITEM_BAD_SLOT;
+  } else if (s.role[slot] != kLeader) {                                // raft_append_entry.go:22-25
+    e = MRAFT_ITEM_BAD_STATE;
+  } else {
+    const int dummy = s.dummy[slot], last = s.last[slot];
+    const int prev = s.next[(int64_t)slot * P + peer] - 1;             // :26
+    if (prev < dummy) e = MRAFT_ITEM_NEED_SNAPSHOT;                    // :27
+    else if (prev > last) e = MRAFT_ITEM_PREV_BEYOND_LAST;             // :41-43
+    else {
+      a.slot = (slot / P) * P + peer;
+      a.leader_id = slot % P;
+      a.term = s.term[slot];
+      a.prev_log_index = prev;
+      a.prev_log_term = s.log[(int64_t)slot * L + (prev - dummy)];     // :49
+      a.n_entries = last - prev;                                       // :50
+      a.leader_commit = s.commit[slot];                                // :51
+      a.entries_offset = (int64_t)slot * L + (prev + 1 - dummy);       // :54 (by reference)
+    }
+  }
+  out[i] = a;
+  err[i] = e;
+}
+
+// ---------------------------------------------------------------- a4
+// One wave per item: uniform prologue, wave-cooperative conflict scan / merge.
+__global__ __launch_bounds__(256) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
+                                                   int64_t n, const int32_t *__restrict__ ent,
+                                                   int64_t n_ent, mraft_ae_reply *__restrict__ rep,
+                                                   int32_t *__restrict__ err) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (i >= n) return;
+  const int lane = lane_id();
+  mraft_ae_reply r = {0, 0, 0, 0};
+  int e = err[i];
+  if (e) {
+    if (lane == 0) rep[i] = r;
+    return;
+  }
+  const mraft_ae_args a = args[i];
+  const int L = s.L;
+  if (a.n_entries < 0 || a.entries_offset < 0 ||
+      (a.n_entries > 0 && a.entries_offset + a.n_entries > n_ent)) {
+    if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_BAD_SLOT; }
+    return;
+  }
+  const int f = a.slot, prev = a.prev_log_index, nn = a.n_entries;
+  const int fterm = s.term[f];
+  if (a.term < fterm) {                                                // :112-115
+    r.term = fterm;
+    if (lane == 0) rep[i] = r;
+    return;
+  }
+  const bool adopt = a.term > fterm;                                   // :116-118
+  const int fdummy = s.dummy[f];
+  const int32_t *frow = s.log + (int64_t)f * L;
+  bool write_state = true;
+  int newlast = -1, fcommit_new = -1;
+  if (prev < fdummy) {                                                 // :123-127
+    r.term = 0; r.conflict_index = fdummy + 1;
+  } else {
+    const int flast = s.last[f];
+    if (prev > flast || frow[prev - fdummy] != a.prev_log_term) {      // matchLog, raft_log.go:92-96
+      r.term = a.term;
+      if (prev > flast) r.conflict_index = flast + 1;                  // :131-133
+      else if (prev > fdummy + 1)
+        r.conflict_index = wave_conflict_scan(frow, fdummy, prev, frow[prev - fdummy]);  // :136-142
+      else r.conflict_index = prev;
+    } else {
+      const int32_t *E = ent + a.entries_offset;
+      int32_t *F = s.log + (int64_t)f * L + (prev + 1 - fdummy);
+      const int kc = min(nn, flast - prev);
+      int k = wave_merge_compare(E, F, kc);                            // :149-155
+      if (k < 0 && kc < nn) k = kc;
+      int last_after = flast;
+      if (k >= 0) {
+        if ((int64_t)prev + nn - fdummy > (int64_t)L - 1) {
+          write_state = false;                                         // engine capacity
+          if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_LOG_FULL; }
+        } else {
+          wave_copy(E + k, F + k, nn - k);
+          newlast = prev + nn;
+          last_after = newlast;
+        }
+      }
+      if (write_state) {
+        const int fc = s.commit[f];
+        if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160
+        r.term = a.term; r.success = 1;                                // :161
+      }
+    }
+  }
+  if (!write_state) return;
+  if (lane == 0) {
+    if (adopt) { s.term[f] = a.term; s.voted[f] = -1; }
+    s.role[f] = kFollower;                                             // :120
+    if (newlast >= 0) s.last[f] = newlast;
+    if (fcommit_new >= 0) s.commit[f] = fcommit_new;
+    rep[i] = r;
+  }
+}
+
+// ---------------------------------------------------------------- a2 + a1
+template <int P>
+__device__ __forceinline__ int quorum_rt(const int (&m)[8], int me) {
+  constexpr int h = P / 2;
+  if (h == 0) return INT32_MAX;
+  int best = INT32_MIN;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    if (j == me) continue;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) c += (q != me && m[q] >= m[j]) ? 1 : 0;
+    if (c >= h && m[j] > best) best = m[j];
+  }
+  return best;
+}
+
+// Lane per segment: the segment's replies folded in order, a1 evaluated after
+// each successful reply exactly as raft_append_entry.go:78 calls it.
+template <int P>
+__global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t n,
+                       const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                       const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
+                       int32_t *__restrict__ item_err) {
+  const int64_t sg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (sg >= n_seg) return;
+  const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
+  if (b >= e) return;
+  const int L = s.L;
+  const int slot = items[b].slot;
+  int bad = seg_err[sg];
+  if (!bad) {
+    for (int64_t i = b; i < e; ++i) {
+      const mraft_ae_result it = items[i];
+      if (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == slot % P)
+        bad = MRAFT_ITEM_BAD_SLOT;
+    }
+  }
+  if (!bad && s.commit[slot] < s.dummy[slot]) bad = MRAFT_ITEM_BAD_STATE;
+  if (bad) {
+    for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
+    return;
+  }
+  const int me = slot % P;
+  const int64_t mrow = (int64_t)slot * P;
+  int m[8], nx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = j < P ? s.match[mrow + j] : 0;
+    nx[j] = j < P ? s.next[mrow + j] : 0;
+  }
+  int term = s.term[slot], role = s.role[slot], commit = s.commit[slot];
+  const int last = s.last[slot], dummy = s.dummy[slot];
+  const int c0 = commit, t0 = term, r0 = role;
+  const int32_t *lrow = s.log + (int64_t)slot * L;
+  bool touched_mn = false;
+  for (int64_t i = b; i < e; ++i) {
+    const mraft_ae_result it = items[i];
+    int fl = 0;
+    const int pr = it.peer;
+    int nxp = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) if (j == pr) nxp = nx[j];
+    if (it.reply_term > term) {                                        // :67-72
+      term = it.reply_term; role = kFollower;
+      fl |= MRAFT_F_STEPPED_DOWN;
+    } else if (it.reply_term == term && role == kLeader && it.args_term == term &&
+               it.args_prev_log_index == nxp - 1) {                    // :73-74
+      fl |= MRAFT_F_APPLIED;
+      touched_mn = true;
+      if (it.reply_success) {
+        const int mv = it.args_n_entries + it.args_prev_log_index;     // :76
+        nxp = mv + 1;                                                  // :77
+#pragma unroll
+        for (int j = 0; j < P; ++j) if (j == pr) m[j] = mv;
+        // a1 (:89-105): the count holds exactly for i <= M (quorum order
+        // statistic), so scan down from min(M, last) for the term gate.
+        const int M = quorum_rt<P>(m, me);
+        const int top = min(M, last);
+        for (int x = top; x > commit; --x) {
+          if (lrow[x - dummy] == term) { commit = x; fl |= MRAFT_F_COMMITTED; break; }
+        }
+      } else {
+        nxp = it.reply_conflict_index;                                 // :82
+      }
+#pragma unroll
+      for (int j = 0; j < P; ++j) if (j == pr) nx[j] = nxp;
+      if (nxp < last + 1) fl |= MRAFT_F_NEED_MORE;                     // :84-86
+    }
+    flags[i] = fl;
+    item_err[i] = 0;
+  }
+  if (term != t0 || role != r0) {
+    s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
+  }
+  if (commit != c0) s.commit[slot] = commit;
+  if (touched_mn) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) { s.match[mrow + j] = m[j]; s.next[mrow + j] = nx[j]; }
+  }
+}
+
+// ---------------------------------------------------------------- a6 part 1
+__global__ void k_start_election(Dev s, const int32_t *__restrict__ slots, int64_t n,
+                                 mraft_rv_args *__restrict__ out, int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  mraft_rv_args a = {};
+  if (!err[i]) {
+    const int sl = slots[i];
+    const int t = s.term[sl] + 1;                                      // raft_election.go:7
+    const int last = s.last[sl];
+    s.role[sl] = kCandidate;                                           // :6
+    s.term[sl] = t;
+    s.voted[sl] = sl % s.P;                                            // :14
+    s.votes[sl] = 1;                                                   // :17
+    a.slot = sl;
+    a.term = t;
+    a.candidate_id = sl % s.P;
+    a.last_log_index = last;                                           // :12
+    a.last_log_term = s.log[(int64_t)sl * s.L + (last - s.dummy[sl])];  // :13
+  }
+  out[i] = a;
+}
+
+// ---------------------------------------------------------------- a5
+__global__ void k_handle_rv(Dev s, const mraft_rv_args *__restrict__ args, int64_t n,
+                            mraft_rv_reply *__restrict__ rep, int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  mraft_rv_reply r = {0, 0};
+  if (!err[i]) {
+    const mraft_rv_args a = args[i];
+    const int v = a.slot;
+    int term = s.term[v], voted = s.voted[v], role = s.role[v];
+    const int t0 = term, v0 = voted, r0 = role;
+    if (a.term < term) {                                               // raft_election.go:59-62
+      r.term = term;
+    } else {
+      if (a.term > term) { role = kFollower; term = a.term; voted = -1; }  // :63-66
+      r.term = term;                                                   // :67
+      const int mylast = s.last[v];
+      const int mylt = s.log[(int64_t)v * s.L + (mylast - s.dummy[v])];
+      const bool up = a.last_log_term > mylt ||                        // raft_log.go:99-104
+                      (mylt == a.last_log_term && a.last_log_index >= mylast);
+      if ((voted == -1 || voted == a.candidate_id) && up) {            // :69-74
+        voted = a.candidate_id;
+        r.vote_granted = 1;
+      }
+      if (term != t0) s.term[v] = term;
+      if (voted != v0) s.voted[v] = voted;
+      if (role != r0) s.role[v] = role;
+    }
+  }
+  rep[i] = r;
+}
+
+// ---------------------------------------------------------------- a6 part 2
+__global__ void k_tally(Dev s, const mraft_rv_result *__restrict__ items, int64_t n,
+                        const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                        const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
+                        int32_t *__restrict__ item_err) {
+  const int64_t sg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (sg >= n_seg) return;
+  const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
+  if (b >= e) return;
+  const int P = s.P;
+  const int c = items[b].slot;
+  int bad = seg_err[sg];
+  if (!bad) {
+    for (int64_t i = b; i < e; ++i) {
+      const mraft_rv_result it = items[i];
+      if (it.slot != c || it.peer < 0 || it.peer >= P || it.peer == c % P) bad = MRAFT_ITEM_BAD_SLOT;
+    }
+  }
+  if (bad) {
+    for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
+    return;
+  }
+  int term = s.term[c], role = s.role[c], votes = s.votes[c], voted = s.voted[c];
+  const int t0 = term, r0 = role, vs0 = votes, vd0 = voted;
+  bool lead = false;
+  for (int64_t i = b; i < e; ++i) {
+    const mraft_rv_result it = items[i];
+    int fl = 0;
+    if (term == it.args_term && role == kCandidate) {                  // raft_election.go:29
+      if (it.vote_granted) {                                           // :30
+        votes += 1;                                                    // :31
+        if (votes > P / 2) {                                           // :32
+          role = kLeader;                                              // :33
+          lead = true;
+          fl |= MRAFT_F_BECAME_LEADER;
+        }
+      } else if (it.reply_term > term) {                               // :42-45
+        role = kFollower; term = it.reply_term; voted = -1;
+        fl |= MRAFT_F_STEPPED_DOWN;
+      }
+    }
+    flags[i] = fl;
+    item_err[i] = 0;
+  }
+  if (term != t0) s.term[c] = term;
+  if (role != r0) s.role[c] = role;
+  if (votes != vs0) s.votes[c] = votes;
+  if (voted != vd0) s.voted[c] = voted;
+  if (lead) {                                                          // :34-38
+    const int nx = s.last[c] + 1;
+    for (int j = 0; j < P; ++j) { s.match[(int64_t)c * P + j] = 0; s.next[(int64_t)c * P + j] = nx; }
+  }
+}
+
+// ---------------------------------------------------------------- GetState
+__global__ void k_export(Dev s, const int32_t *__restrict__ lpeer, int32_t *__restrict__ commit,
+                         int32_t *__restrict__ term_leader) {
+  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (g >= s.G) return;
+  int p = lpeer ? lpeer[g] : 0;
+  if (p < 0 || p >= s.P) p = 0;
+  const int64_t sl = (int64_t)g * s.P + p;
+  commit[g] = s.commit[sl];
+  term_leader[g] = (int32_t)(((uint32_t)s.term[sl] << 1) | (s.role[sl] == kLeader ? 1u : 0u));  // raft.go:237-246
+}
+
+}  // namespace
+
+void launch_init_state(const Dev &s, hipStream_t st) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  int blocks = blocks_for(gp);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_init_state, dim3(blocks), dim3(kBlock), 0, st, s);
+}
+
+void launch_claim(const void *items, int64_t n, int stride, int slot_off, const int64_t *seg_begin,
+                  int64_t gp, int peers, unsigned long long *claim, uint32_t epoch, int32_t *err,
+                  hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_claim, dim3(blocks_for(n)), dim3(kBlock), 0, st, (const char *)items, n,
+                     stride, slot_off, seg_begin, gp, peers, claim, epoch, err);
+  hipLaunchKernelGGL(k_claim_check, dim3(blocks_for(n)), dim3(kBlock), 0, st, (const char *)items,
+                     n, stride, slot_off, seg_begin, claim, epoch, err);
+}
+
+void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
+                        mraft_ae_args *out, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_args, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, peers, n,
+                     out, err);
+}
+
+void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
+                      int64_t n_ent, mraft_ae_reply *rep, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, args, n, ent,
+                     n_ent, rep, err);
+}
+
+void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
+                 int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
+                 hipStream_t st) {
+  (void)n;
+  if (n_seg <= 0) return;
+  const dim3 gr(blocks_for(n_seg, 64)), bl(64);
+  switch (s.P) {
+#define MRAFT_FOLD_CASE(PP)                                                                   \
+  case PP:                                                                                    \
+    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, flags, \
+                       item_err);                                                             \
+    break;
+    MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
+    MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
+#undef MRAFT_FOLD_CASE
+    default: break;
+  }
+}
+
+void launch_start_election(const Dev &s, const int32_t *slots, int64_t n, mraft_rv_args *out,
+                           int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_start_election, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, n, out,
+                     err);
+}
+
+void launch_handle_rv(const Dev &s, const mraft_rv_args *args, int64_t n, mraft_rv_reply *rep,
+                      int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_handle_rv, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, args, n, rep, err);
+}
+
+void launch_tally(const Dev &s, const mraft_rv_result *items, int64_t n, const int64_t *seg_begin,
+                  int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
+                  hipStream_t st) {
+  (void)n;
+  if (n_seg <= 0) return;
+  hipLaunchKernelGGL(k_tally, dim3(blocks_for(n_seg, 64)), dim3(64), 0, st, s, items, n, seg_begin,
+                     n_seg, seg_err, flags, item_err);
+}
+
+void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t *term_leader,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(k_export, dim3(blocks_for(s.G)), dim3(kBlock), 0, st, s, lpeer, commit,
+                     term_leader);
+}
+
+}  // namespace mraft

@@ -1,0 +1,227 @@
+"""Host-side mirror of the engine boundary (include/mraft.h) over ctypes.
+
+`Engine` wraps one libmraft_hip.so handle: G groups x P peers of Raft replica
+state resident in HBM, and the batched decision entry points that replace the
+reference's per-instance handlers (src/raft/raft_append_entry.go,
+src/raft/raft_election.go). Host batches are numpy arrays of the structured
+dtypes in `_abi` (synchronous calls); device batches are torch tensors or raw
+device addresses (asynchronous on the engine's stream).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import (AE_ARGS, AE_REPLY, AE_RESULT, RV_ARGS, RV_REPLY, RV_RESULT, DEVICE, HOST,
+                   STATE_FIELDS, ptr, soa_of)
+
+
+class MraftError(RuntimeError):
+    pass
+
+
+def _ck(rc: int, what: str):
+    if rc != _abi.OK:
+        raise MraftError(f"{what} failed ({rc}): {_abi.last_error()}")
+
+
+def state_sizes(G: int, P: int, L: int) -> dict:
+    gp = G * P
+    return {f: (gp * L if f == "log_term" else gp * P if f in ("match_index", "next_index") else gp)
+            for f in STATE_FIELDS}
+
+
+def new_state(G: int, P: int, L: int) -> dict:
+    """A host state image initialised as Make does (raft.go:51-87)."""
+    st = {f: np.zeros(n, dtype=np.int32) for f, n in state_sizes(G, P, L).items()}
+    st["voted_for"][:] = -1
+    st["state"][:] = _abi.FOLLOWER
+    return st
+
+
+def copy_state(st: dict) -> dict:
+    return {k: np.array(v, copy=True) for k, v in st.items()}
+
+
+def synth_tick_state(G: int, P: int, L: int, seed: int, g_begin: int = 0, g_end: int | None = None,
+                     nthreads: int | None = None):
+    """Seeded replication-tick workload (include/mraft_synth.h). Returns
+    (state, leader_peer, item_class) for groups [g_begin, g_end)."""
+    g_end = G if g_end is None else g_end
+    n = g_end - g_begin
+    st = {f: np.empty(sz, dtype=np.int32) for f, sz in state_sizes(n, P, L).items()}
+    lp = np.empty(n, dtype=np.int32)
+    ic = np.empty(n * P, dtype=np.int32)
+    soa = soa_of(st)
+    nt = nthreads if nthreads is not None else min(16, os.cpu_count() or 1)
+    rc = _abi.synth().mraft_synth_tick_state(seed, G, P, L, g_begin, g_end, ctypes.byref(soa),
+                                             ptr(lp), ptr(ic), nt)
+    if rc != 0:
+        raise MraftError(f"mraft_synth_tick_state failed ({rc})")
+    return st, lp, ic
+
+
+def synth_fold_batch(st: dict, G: int, P: int, L: int, leader_peer: np.ndarray, seed: int):
+    items = np.zeros(G * max(P - 1, 0), dtype=AE_RESULT)
+    seg = np.zeros(G + 1, dtype=np.int64)
+    soa = soa_of(st)
+    n = _abi.synth().mraft_synth_fold_batch(seed, G, P, L, ctypes.byref(soa), ptr(leader_peer),
+                                            ptr(items), ptr(seg))
+    return items[:n], seg
+
+
+class Engine:
+    """One engine handle per GPU (calls must be serialized by the caller)."""
+
+    def __init__(self, G: int, P: int, L: int, device: int = 0, alloc: bool = True):
+        self.G, self.P, self.L = G, P, L
+        self._lib = _abi.lib()
+        h = ctypes.c_void_p()
+        _ck(self._lib.mraft_create(G, P, L, device, 0 if alloc else _abi.CREATE_NO_ALLOC,
+                                   ctypes.byref(h)), "mraft_create")
+        self._h = h
+
+    # ---- lifetime --------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.mraft_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int | None):
+        _ck(self._lib.mraft_set_stream(self._h, stream_ptr), "mraft_set_stream")
+
+    def stream(self) -> int:
+        return self._lib.mraft_get_stream(self._h) or 0
+
+    def synchronize(self):
+        _ck(self._lib.mraft_synchronize(self._h), "mraft_synchronize")
+
+    # ---- state -----------------------------------------------------------
+    def load_state(self, st: dict, where: int = HOST):
+        soa = soa_of(st)
+        _ck(self._lib.mraft_load_state(self._h, ctypes.byref(soa), where), "mraft_load_state")
+
+    def store_state(self) -> dict:
+        out = {f: np.empty(n, dtype=np.int32) for f, n in state_sizes(self.G, self.P, self.L).items()}
+        soa = soa_of(out)
+        _ck(self._lib.mraft_store_state(self._h, ctypes.byref(soa), HOST), "mraft_store_state")
+        return out
+
+    def view(self) -> dict:
+        soa = _abi.MraftSoa()
+        _ck(self._lib.mraft_state_view(self._h, ctypes.byref(soa)), "mraft_state_view")
+        return {f: getattr(soa, f) for f in STATE_FIELDS}
+
+    def bind(self, dev_state: dict):
+        soa = soa_of(dev_state)
+        _ck(self._lib.mraft_bind_state(self._h, ctypes.byref(soa)), "mraft_bind_state")
+
+    # ---- hot path --------------------------------------------------------
+    def replicate_tick(self, leader_peer, group_flags=None, where: int = HOST):
+        if where == HOST:
+            leader_peer = np.ascontiguousarray(leader_peer, dtype=np.int32)
+            if group_flags is None:
+                group_flags = np.zeros(self.G, dtype=np.int32)
+        _ck(self._lib.mraft_replicate_tick(self._h, ptr(leader_peer), ptr(group_flags), where),
+            "mraft_replicate_tick")
+        return group_flags
+
+    def replicate_tick_count(self, leader_peer, where: int = HOST):
+        if where == HOST:
+            leader_peer = np.ascontiguousarray(leader_peer, dtype=np.int32)
+        out = (ctypes.c_int64 * 3)()
+        _ck(self._lib.mraft_replicate_tick_count(self._h, ptr(leader_peer), out, where),
+            "mraft_replicate_tick_count")
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def gather_append_args(self, slots, peers):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=AE_ARGS)
+        err = np.zeros(n, dtype=np.int32)
+        _ck(self._lib.mraft_gather_append_args(self._h, ptr(slots), ptr(peers), n, ptr(out),
+                                               ptr(err), HOST), "mraft_gather_append_args")
+        return out, err
+
+    def handle_append_entries(self, args: np.ndarray, entry_terms: np.ndarray | None):
+        args = np.ascontiguousarray(args, dtype=AE_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=AE_REPLY)
+        err = np.zeros(n, dtype=np.int32)
+        et = None if entry_terms is None else np.ascontiguousarray(entry_terms, dtype=np.int32)
+        _ck(self._lib.mraft_handle_append_entries(self._h, ptr(args), n, ptr(et),
+                                                  0 if et is None else len(et), ptr(rep),
+                                                  ptr(err), HOST), "mraft_handle_append_entries")
+        return rep, err
+
+    def process_append_replies(self, items: np.ndarray, seg_begin: np.ndarray | None = None):
+        items = np.ascontiguousarray(items, dtype=AE_RESULT)
+        n = len(items)
+        flags = np.zeros(n, dtype=np.int32)
+        err = np.zeros(n, dtype=np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        _ck(self._lib.mraft_process_append_replies(self._h, ptr(items), n, ptr(sb),
+                                                   0 if sb is None else len(sb) - 1, ptr(flags),
+                                                   ptr(err), HOST),
+            "mraft_process_append_replies")
+        return flags, err
+
+    # ---- elections -------------------------------------------------------
+    def start_election(self, slots):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=RV_ARGS)
+        err = np.zeros(n, dtype=np.int32)
+        _ck(self._lib.mraft_start_election(self._h, ptr(slots), n, ptr(out), ptr(err), HOST),
+            "mraft_start_election")
+        return out, err
+
+    def handle_request_vote(self, args: np.ndarray):
+        args = np.ascontiguousarray(args, dtype=RV_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=RV_REPLY)
+        err = np.zeros(n, dtype=np.int32)
+        _ck(self._lib.mraft_handle_request_vote(self._h, ptr(args), n, ptr(rep), ptr(err), HOST),
+            "mraft_handle_request_vote")
+        return rep, err
+
+    def process_vote_replies(self, items: np.ndarray, seg_begin: np.ndarray | None = None):
+        items = np.ascontiguousarray(items, dtype=RV_RESULT)
+        n = len(items)
+        flags = np.zeros(n, dtype=np.int32)
+        err = np.zeros(n, dtype=np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        _ck(self._lib.mraft_process_vote_replies(self._h, ptr(items), n, ptr(sb),
+                                                 0 if sb is None else len(sb) - 1, ptr(flags),
+                                                 ptr(err), HOST), "mraft_process_vote_replies")
+        return flags, err
+
+    def export_group_status(self, leader_peer=None):
+        commit = np.zeros(self.G, dtype=np.int32)
+        tl = np.zeros(self.G, dtype=np.int32)
+        lp = None if leader_peer is None else np.ascontiguousarray(leader_peer, dtype=np.int32)
+        _ck(self._lib.mraft_export_group_status(self._h, ptr(lp), ptr(commit), ptr(tl), HOST),
+            "mraft_export_group_status")
+        return commit, tl
+
+
+def export_group_status_into(eng: Engine, leader_peer, commit, term_leader, where: int = DEVICE):
+    """GetState for every group into caller buffers (device tensors by default)."""
+    _ck(eng._lib.mraft_export_group_status(eng._h, ptr(leader_peer), ptr(commit), ptr(term_leader),
+                                           where), "mraft_export_group_status")

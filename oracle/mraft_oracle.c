@@ -1,0 +1,652 @@
+/*
+ * mraft_oracle.c — CPU restatement of yusong-yan/MultiRaft's Raft decision
+ * logic (src/raft/ Go files), TEST INFRASTRUCTURE ONLY (see mraft_oracle.h).
+ *
+ * Every function follows the control flow of the Go function it cites,
+ * statement by statement, including the reference's quirks (ConflictIndex
+ * off-by-one, reply.Term = 0 on prev < dummy, follower commit against the whole
+ * log's lastIndex, no ConflictTerm, matchIndex assigned not max-ed, a1's
+ * downward O((last-commit)*P) loop). Where Go panics, the item is flagged in
+ * item_err and the state it would touch is left unmodified.
+ *
+ * Go `int` is 64-bit; the state here is int32 like the device layout. Inputs
+ * are restricted to [-1, 2^31) so results are identical in that range.
+ */
+#include "mraft_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Algorithmic word counting.                                 */
+/* ------------------------------------------------------------------------ */
+
+enum { A_TERM, A_VOTED, A_ROLE, A_COMMIT, A_APPLIED, A_DUMMY, A_LAST, A_VOTES,
+       A_LOG, A_MATCH, A_NEXT, A_COUNT };
+
+static struct {
+  int on;
+  int64_t base[A_COUNT + 1];
+  uint64_t *rd, *wr;
+} cnt;
+
+int ora_count_enable(ora_engine *e) {
+  int64_t gp = (int64_t)e->G * e->P;
+  int64_t sizes[A_COUNT] = {gp, gp, gp, gp, gp, gp, gp, gp,
+                            gp * e->L, gp * e->P, gp * e->P};
+  int64_t b = 0;
+  for (int a = 0; a < A_COUNT; ++a) { cnt.base[a] = b; b += sizes[a]; }
+  cnt.base[A_COUNT] = b;
+  free(cnt.rd); free(cnt.wr);
+  int64_t nw = (b + 63) / 64;
+  cnt.rd = (uint64_t *)calloc((size_t)nw, 8);
+  cnt.wr = (uint64_t *)calloc((size_t)nw, 8);
+  if (!cnt.rd || !cnt.wr) return MRAFT_E_NOMEM;
+  cnt.on = 1;
+  return MRAFT_OK;
+}
+
+void ora_count_disable(void) {
+  cnt.on = 0;
+  free(cnt.rd); free(cnt.wr);
+  cnt.rd = cnt.wr = NULL;
+}
+
+void ora_count_result(int64_t out[2]) {
+  out[0] = out[1] = 0;
+  if (!cnt.rd) return;
+  int64_t nw = (cnt.base[A_COUNT] + 63) / 64;
+  for (int64_t i = 0; i < nw; ++i) {
+    out[0] += __builtin_popcountll(cnt.rd[i]);
+    out[1] += __builtin_popcountll(cnt.wr[i]);
+  }
+}
+
+static inline void CR(int a, int64_t i) {
+  if (cnt.on) { int64_t w = cnt.base[a] + i; cnt.rd[w >> 6] |= 1ull << (w & 63); }
+}
+static inline void CW(int a, int64_t i) {
+  if (cnt.on) { int64_t w = cnt.base[a] + i; cnt.wr[w >> 6] |= 1ull << (w & 63); }
+}
+
+/* ------------------------------------------------------------------------ */
+/* raftLog helpers, src/raft/raft_log.go                                     */
+/* ------------------------------------------------------------------------ */
+
+#define S (e->s)
+
+/* getEntry(index).Term, raft_log.go:40-42 + convertIndex :55-60 (caller
+ * guarantees index >= dummyIndex; the panic is handled by callers). */
+static inline int32_t term_at(const ora_engine *e, int64_t slot, int32_t index) {
+  return S.log_term[slot * e->L + (index - S.dummy_index[slot])];
+}
+
+static inline int32_t imin(int32_t a, int32_t b) { return a < b ? a : b; } /* utility.go:41-46 */
+
+/* Duplicate-slot claim: lowest item index wins (include/mraft.h). */
+static int32_t *claim_slots(ora_engine *e, const int32_t *slot_of, int64_t n,
+                            size_t stride_bytes, int32_t *item_err) {
+  int64_t gp = (int64_t)e->G * e->P;
+  int32_t *first = (int32_t *)malloc(sizeof(int32_t) * (size_t)(gp ? gp : 1));
+  for (int64_t i = 0; i < gp; ++i) first[i] = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    int32_t slot = *(const int32_t *)((const char *)slot_of + i * stride_bytes);
+    if (slot < 0 || slot >= gp) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
+    if (first[slot] >= 0) { item_err[i] = MRAFT_ITEM_DUP_SLOT; continue; }
+    first[slot] = (int32_t)i;
+    item_err[i] = MRAFT_ITEM_OK;
+  }
+  return first;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a3: appendOneRound args gather, raft_append_entry.go:20-54                 */
+/* ------------------------------------------------------------------------ */
+
+static int32_t gather_one(ora_engine *e, int32_t slot, int32_t peer,
+                          mraft_ae_args *a) {
+  int32_t P = e->P;
+  if (peer < 0 || peer >= P || peer == slot % P) return MRAFT_ITEM_BAD_SLOT;
+  if (S.state[slot] != MRAFT_LEADER) return MRAFT_ITEM_BAD_STATE;      /* :22-25 */
+  int32_t prev = S.next_index[(int64_t)slot * P + peer] - 1;           /* :26 */
+  if (prev < S.dummy_index[slot]) return MRAFT_ITEM_NEED_SNAPSHOT;     /* :27 */
+  if (prev > S.last_index[slot]) return MRAFT_ITEM_PREV_BEYOND_LAST;   /* :41-43 */
+  a->slot = (slot / P) * P + peer;
+  a->leader_id = slot % P;                                             /* :46 */
+  a->term = S.current_term[slot];                                      /* :47 */
+  a->prev_log_index = prev;                                            /* :48 */
+  a->prev_log_term = term_at(e, slot, prev);                           /* :49 */
+  a->n_entries = S.last_index[slot] - prev;                            /* :50 */
+  a->leader_commit = S.commit_index[slot];                             /* :51 */
+  a->_pad = 0;
+  a->entries_offset = (int64_t)slot * e->L + (prev + 1 - S.dummy_index[slot]); /* :54 */
+  return MRAFT_ITEM_OK;
+}
+
+int ora_gather_append_args(ora_engine *e, const int32_t *slots,
+                           const int32_t *peers, int64_t n,
+                           mraft_ae_args *out, int32_t *item_err) {
+  int64_t gp = (int64_t)e->G * e->P;
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&out[i], 0, sizeof(out[i]));
+    if (slots[i] < 0 || slots[i] >= gp) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
+    item_err[i] = gather_one(e, slots[i], peers[i], &out[i]);
+  }
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a4: HandleAppendEntries, raft_append_entry.go:108-162                      */
+/* ------------------------------------------------------------------------ */
+
+/* ent = entries' terms (entry k has Index prev+1+k); ent_cnt_base = word index
+ * of entry 0 in the LOG array when entries are a view of a leader log (for
+ * counting), or -1. */
+static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
+                             const int32_t *ent, int64_t ent_cnt_base,
+                             mraft_ae_reply *r, int *follower_committed) {
+  const int32_t L = e->L;
+  const int64_t row = (int64_t)f * L;
+  const int32_t prev = a->prev_log_index, n = a->n_entries;
+  memset(r, 0, sizeof(*r)); /* reply := new(AppendEntriesReply) */
+  *follower_committed = 0;
+
+  /* Capacity pre-check (engine limit, not a Go condition): would this item
+   * reach the merge, find a mismatch and grow the log past L slots? Then it is
+   * rejected before any mutation. Reads only. */
+  if (a->term >= S.current_term[f] && prev >= S.dummy_index[f] &&
+      prev <= S.last_index[f] && term_at(e, f, prev) == a->prev_log_term) {
+    int32_t dummy = S.dummy_index[f], last = S.last_index[f];
+    for (int32_t k = 0; k < n; ++k) {
+      int32_t idx = prev + 1 + k;
+      if (idx > last || S.log_term[row + idx - dummy] != ent[k]) {
+        if ((int64_t)prev + n - dummy > (int64_t)L - 1) return MRAFT_ITEM_LOG_FULL;
+        break;
+      }
+    }
+  }
+
+  CR(A_TERM, f);
+  if (a->term < S.current_term[f]) {                                  /* :112-115 */
+    r->term = S.current_term[f]; r->success = 0;
+    return MRAFT_ITEM_OK;
+  }
+  if (a->term > S.current_term[f]) {                                  /* :116-118 */
+    S.current_term[f] = a->term; S.voted_for[f] = -1;
+    CW(A_TERM, f); CW(A_VOTED, f);
+  }
+  S.state[f] = MRAFT_FOLLOWER;                                        /* :120 */
+  CW(A_ROLE, f);
+
+  CR(A_DUMMY, f);
+  int32_t dummy = S.dummy_index[f];
+  if (prev < dummy) {                                                 /* :123-127 */
+    r->term = 0; r->success = 0; r->conflict_index = dummy + 1;
+    return MRAFT_ITEM_OK;
+  }
+  /* matchLog, raft_log.go:92-96: Index <= lastIndex && Term == getEntry(Index).Term */
+  CR(A_LAST, f);
+  int32_t last = S.last_index[f];
+  int match = 0;
+  if (prev <= last) {
+    CR(A_LOG, row + prev - dummy);
+    match = (a->prev_log_term == S.log_term[row + prev - dummy]);
+  }
+  if (!match) {                                                       /* :128-145 */
+    r->term = S.current_term[f]; r->success = 0;
+    if (prev > last) {
+      r->conflict_index = last + 1;                                   /* :131-133 */
+    } else {
+      int32_t abandoned = S.log_term[row + prev - dummy];             /* :137 */
+      int32_t index = prev;                                           /* :138 */
+      while (index > dummy + 1) {                                     /* :139-141 */
+        CR(A_LOG, row + index - dummy);
+        if (S.log_term[row + index - dummy] != abandoned) break;
+        index--;
+      }
+      r->conflict_index = index;                                      /* :142 */
+    }
+    return MRAFT_ITEM_OK;
+  }
+  /* :149-155 — merge without blind truncation (non-FIFO guard). */
+  for (int32_t k = 0; k < n; ++k) {
+    int32_t index = prev + 1 + k;                                     /* entry.Index */
+    int diff;
+    if (index - dummy >= last - dummy + 1) {                          /* convertIndex >= len */
+      diff = 1;
+    } else {
+      CR(A_LOG, row + index - dummy);
+      if (ent_cnt_base >= 0) CR(A_LOG, ent_cnt_base + k);
+      diff = (S.log_term[row + index - dummy] != ent[k]);
+    }
+    if (diff) {
+      /* trunc(entry.Index) then append(args.Entries[k:]...), raft_log.go:62-75 */
+      for (int32_t j = k; j < n; ++j) {
+        int32_t idx = prev + 1 + j;
+        if (ent_cnt_base >= 0) CR(A_LOG, ent_cnt_base + j);
+        S.log_term[row + idx - dummy] = ent[j];
+        CW(A_LOG, row + idx - dummy);
+      }
+      S.last_index[f] = prev + n;
+      CW(A_LAST, f);
+      break;
+    }
+  }
+  CR(A_COMMIT, f);
+  if (a->leader_commit > S.commit_index[f]) {                         /* :157-160 */
+    S.commit_index[f] = imin(a->leader_commit, S.last_index[f]);
+    CW(A_COMMIT, f);
+    *follower_committed = 1;
+  }
+  r->term = S.current_term[f]; r->success = 1;                        /* :161 */
+  return MRAFT_ITEM_OK;
+}
+
+int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
+                              int64_t n, const int32_t *entry_terms,
+                              int64_t n_entry_terms, mraft_ae_reply *replies,
+                              int32_t *item_err) {
+  int32_t *first = claim_slots(e, &args[0].slot, n, sizeof(mraft_ae_args), item_err);
+  const int32_t *src = entry_terms ? entry_terms : S.log_term;
+  int64_t src_n = entry_terms ? n_entry_terms : (int64_t)e->G * e->P * e->L;
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&replies[i], 0, sizeof(replies[i]));
+    if (item_err[i]) continue;
+    const mraft_ae_args *a = &args[i];
+    if (a->n_entries < 0 || a->entries_offset < 0 ||
+        (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n)) {
+      item_err[i] = MRAFT_ITEM_BAD_SLOT;
+      continue;
+    }
+    int fc;
+    item_err[i] = handle_ae_one(e, a->slot, a, src + a->entries_offset, -1,
+                                &replies[i], &fc);
+  }
+  free(first);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a1: advanceCommitIndexForLeader, raft_append_entry.go:89-105               */
+/* ------------------------------------------------------------------------ */
+
+static int advance_commit(ora_engine *e, int32_t slot) {
+  const int32_t P = e->P, me = slot % P;
+  const int32_t *match = &S.match_index[(int64_t)slot * P];
+  for (int32_t i = S.last_index[slot]; i > S.commit_index[slot]; i--) {
+    int32_t num = 0;
+    for (int32_t j = 0; j < P; ++j)
+      if (j != me && match[j] >= i) num++;
+    /* Go evaluates getEntry(i) only when the count holds (&& short-circuit);
+     * commit >= dummy is enforced by callers so i >= dummy here. */
+    if (num + 1 > P / 2 && term_at(e, slot, i) == S.current_term[slot]) {
+      S.commit_index[slot] = i;                                       /* :99 */
+      return 1;                                                       /* applyCond.Signal */
+    }
+  }
+  return 0;
+}
+
+/* h-th largest (h = P/2) of matchIndex[j != me]: the largest i whose count in
+ * a1 reaches the quorum (used only for counting). */
+static int32_t quorum_match(const ora_engine *e, int32_t slot) {
+  const int32_t P = e->P, me = slot % P, h = P / 2;
+  const int32_t *match = &S.match_index[(int64_t)slot * P];
+  if (h == 0) return INT32_MAX;
+  int32_t best = INT32_MIN;
+  for (int32_t j = 0; j < P; ++j) {
+    if (j == me) continue;
+    int32_t c = 0;
+    for (int32_t k = 0; k < P; ++k)
+      if (k != me && match[k] >= match[j]) c++;
+    if (c >= h && match[j] > best) best = match[j];
+  }
+  return best;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a2: processAppendEntriesReply, raft_append_entry.go:66-88                  */
+/* ------------------------------------------------------------------------ */
+
+static int32_t process_reply_one(ora_engine *e, int32_t slot, int32_t peer,
+                                 int32_t args_term, int32_t args_prev,
+                                 int32_t args_n, int32_t reply_term,
+                                 int32_t reply_success, int32_t reply_ci,
+                                 int32_t *mstar) {
+  const int32_t P = e->P;
+  int32_t flags = 0;
+  int64_t pi = (int64_t)slot * P + peer;
+  if (reply_term > S.current_term[slot]) {                            /* :67-72 */
+    S.current_term[slot] = reply_term;
+    S.voted_for[slot] = -1;
+    S.state[slot] = MRAFT_FOLLOWER;
+    CW(A_TERM, slot); CW(A_VOTED, slot); CW(A_ROLE, slot);
+    flags |= MRAFT_F_STEPPED_DOWN;
+  } else if (reply_term == S.current_term[slot] &&                    /* :73-74 */
+             S.state[slot] == MRAFT_LEADER &&
+             args_term == S.current_term[slot] &&
+             args_prev == S.next_index[pi] - 1) {
+    flags |= MRAFT_F_APPLIED;
+    if (reply_success) {
+      S.match_index[pi] = args_n + args_prev;                         /* :76 */
+      S.next_index[pi] = S.match_index[pi] + 1;                       /* :77 */
+      CW(A_MATCH, pi); CW(A_NEXT, pi);
+      if (mstar) {
+        int32_t m = quorum_match(e, slot);
+        if (m > *mstar) *mstar = m;
+      }
+      if (advance_commit(e, slot)) flags |= MRAFT_F_COMMITTED;        /* :78 */
+    } else {
+      S.next_index[pi] = reply_ci;                                    /* :82 */
+      CW(A_NEXT, pi);
+    }
+    if (S.next_index[pi] < S.last_index[slot] + 1)                    /* :84-86 */
+      flags |= MRAFT_F_NEED_MORE;
+  }
+  return flags;
+}
+
+int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
+                               int64_t n, const int64_t *seg_begin,
+                               int64_t n_seg, int32_t *out_flags,
+                               int32_t *item_err) {
+  const int32_t P = e->P;
+  int64_t gp = (int64_t)e->G * P;
+  int64_t ns = seg_begin ? n_seg : n;
+  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t b = seg_begin ? seg_begin[s] : s, en = seg_begin ? seg_begin[s + 1] : s + 1;
+    if (b >= en) continue;
+    int32_t slot = items[b].slot;
+    int32_t bad = 0;
+    if (slot < 0 || slot >= gp) bad = MRAFT_ITEM_BAD_SLOT;
+    else if (seen[slot]) bad = MRAFT_ITEM_DUP_SLOT;
+    else {
+      for (int64_t i = b; i < en; ++i)
+        if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
+            items[i].peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+    }
+    if (!bad && S.commit_index[slot] < S.dummy_index[slot]) bad = MRAFT_ITEM_BAD_STATE;
+    if (bad) {
+      for (int64_t i = b; i < en; ++i) item_err[i] = bad;
+      continue;
+    }
+    seen[slot] = 1;
+    for (int64_t i = b; i < en; ++i) {
+      const mraft_ae_result *it = &items[i];
+      out_flags[i] = process_reply_one(e, slot, it->peer, it->args_term,
+                                       it->args_prev_log_index, it->args_n_entries,
+                                       it->reply_term, it->reply_success,
+                                       it->reply_conflict_index, NULL);
+    }
+  }
+  free(seen);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Fused tick = for each group: a3 for every peer, a4 at every follower, a2   */
+/* (+a1) at the leader in peer order.                                         */
+/* ------------------------------------------------------------------------ */
+
+static void tick_group(ora_engine *e, const int32_t *leader_peer,
+                       int32_t *group_flags, int32_t g, int32_t *scratch) {
+  const int32_t P = e->P;
+  int32_t flags = 0;
+  int32_t lp = leader_peer[g];
+  if (lp < 0) { if (group_flags) group_flags[g] = 0; return; }
+  if (lp >= P) { if (group_flags) group_flags[g] = MRAFT_G_ERROR; return; }
+  const int32_t ld = g * P + lp;
+  CR(A_ROLE, ld);
+  if (S.state[ld] != MRAFT_LEADER) { if (group_flags) group_flags[g] = 0; return; }
+  CR(A_TERM, ld); CR(A_COMMIT, ld); CR(A_LAST, ld); CR(A_DUMMY, ld);
+  if (S.commit_index[ld] < S.dummy_index[ld]) {
+    if (group_flags) group_flags[g] = MRAFT_G_ERROR;
+    return;
+  }
+  int32_t ok[8] = {0};
+  for (int32_t p = 0; p < P; ++p) {
+    if (p == lp) continue;
+    CR(A_NEXT, (int64_t)ld * P + p);
+    int32_t prev = S.next_index[(int64_t)ld * P + p] - 1;
+    if (prev < S.dummy_index[ld]) flags |= MRAFT_G_NEED_SNAPSHOT;
+    else if (prev > S.last_index[ld]) flags |= MRAFT_G_ERROR;
+    else ok[p] = 1;
+  }
+  if (flags & MRAFT_G_ERROR) {
+    if (group_flags) group_flags[g] = MRAFT_G_ERROR | (flags & MRAFT_G_NEED_SNAPSHOT);
+    return;
+  }
+  flags |= MRAFT_G_ACTIVE;
+
+  mraft_ae_args args[8];
+  mraft_ae_reply rep[8];
+  int32_t have[8] = {0};
+  for (int32_t p = 0; p < P; ++p) {
+    if (!ok[p]) continue;
+    gather_one(e, ld, p, &args[p]);                                   /* a3 */
+    int32_t prev = args[p].prev_log_index;
+    CR(A_LOG, (int64_t)ld * e->L + prev - S.dummy_index[ld]);         /* PrevLogTerm */
+    /* Go copies the entries into the args (raft_append_entry.go:50-54). */
+    memcpy(scratch, S.log_term + args[p].entries_offset,
+           sizeof(int32_t) * (size_t)args[p].n_entries);
+    int fc = 0;
+    int32_t err = handle_ae_one(e, g * P + p, &args[p], scratch,      /* a4 */
+                                args[p].entries_offset, &rep[p], &fc);
+    if (err) { flags |= MRAFT_G_LOG_FULL; continue; }
+    have[p] = 1;
+    if (fc) flags |= MRAFT_G_FOLLOWER_COMMIT;
+  }
+  int32_t commit0 = S.commit_index[ld];
+  int32_t term0 = S.current_term[ld];
+  int32_t mstar = INT32_MIN;
+  int any_eval = 0;
+  for (int32_t p = 0; p < P; ++p) {                                   /* a2 (+a1) */
+    if (!have[p]) continue;
+    int32_t ms = INT32_MIN;
+    int32_t fl = process_reply_one(e, ld, p, args[p].term, args[p].prev_log_index,
+                                   args[p].n_entries, rep[p].term, rep[p].success,
+                                   rep[p].conflict_index, cnt.on ? &ms : NULL);
+    if ((fl & MRAFT_F_APPLIED) && rep[p].success) {
+      any_eval = 1;
+      if (ms > mstar) mstar = ms;
+    }
+    if (fl & MRAFT_F_STEPPED_DOWN) flags |= MRAFT_G_STEPPED_DOWN;
+  }
+  if (S.commit_index[ld] != commit0) {
+    flags |= MRAFT_G_COMMITTED;
+    CW(A_COMMIT, ld);
+  }
+  if (cnt.on && any_eval) {
+    /* Minimal exact commit scan: matchIndex of the followers,
+     * then log terms from min(M*, last) down to the first term == currentTerm
+     * or commit0+1. */
+    for (int32_t j = 0; j < P; ++j)
+      if (j != lp) CR(A_MATCH, (int64_t)ld * P + j);
+    int32_t top = imin(mstar, S.last_index[ld]);
+    for (int32_t i = top; i > commit0; --i) {
+      CR(A_LOG, (int64_t)ld * e->L + i - S.dummy_index[ld]);
+      if (term_at(e, ld, i) == term0) break;
+    }
+  }
+  if (group_flags) group_flags[g] = flags;
+}
+
+int ora_replicate_tick_range(ora_engine *e, const int32_t *leader_peer,
+                             int32_t *group_flags, int32_t g_begin,
+                             int32_t g_end) {
+  int32_t *scratch = (int32_t *)malloc(sizeof(int32_t) * (size_t)e->L);
+  if (!scratch) return MRAFT_E_NOMEM;
+  for (int32_t g = g_begin; g < g_end; ++g)
+    tick_group(e, leader_peer, group_flags, g, scratch);
+  free(scratch);
+  return MRAFT_OK;
+}
+
+int ora_replicate_tick(ora_engine *e, const int32_t *leader_peer,
+                       int32_t *group_flags) {
+  if (e->P > 8) return MRAFT_E_INVAL;
+  return ora_replicate_tick_range(e, leader_peer, group_flags, 0, e->G);
+}
+
+typedef struct {
+  ora_engine *e;
+  const int32_t *lp;
+  int32_t *gf;
+  int32_t b, en;
+} tick_job;
+
+static void *tick_worker(void *arg) {
+  tick_job *j = (tick_job *)arg;
+  ora_replicate_tick_range(j->e, j->lp, j->gf, j->b, j->en);
+  return NULL;
+}
+
+int ora_replicate_tick_mt(ora_engine *e, const int32_t *leader_peer,
+                          int32_t *group_flags, int32_t nthreads) {
+  if (cnt.on || nthreads <= 1) return ora_replicate_tick(e, leader_peer, group_flags);
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  tick_job jobs[256];
+  int32_t G = e->G;
+  for (int32_t t = 0; t < nthreads; ++t) {
+    jobs[t].e = e; jobs[t].lp = leader_peer; jobs[t].gf = group_flags;
+    jobs[t].b = (int32_t)((int64_t)G * t / nthreads);
+    jobs[t].en = (int32_t)((int64_t)G * (t + 1) / nthreads);
+    pthread_create(&th[t], NULL, tick_worker, &jobs[t]);
+  }
+  for (int32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a6 part 1: StartElection, raft_election.go:4-15                            */
+/* ------------------------------------------------------------------------ */
+
+int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
+                       mraft_rv_args *out, int32_t *item_err) {
+  int32_t *first = claim_slots(e, slots, n, sizeof(int32_t), item_err);
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&out[i], 0, sizeof(out[i]));
+    if (item_err[i]) continue;
+    int32_t s = slots[i];
+    S.state[s] = MRAFT_CANDIDATE;                                     /* :6 */
+    S.current_term[s] += 1;                                           /* :7 */
+    int32_t last = S.last_index[s];                                   /* lastEntry, raft_log.go:50-53 */
+    out[i].slot = s;
+    out[i].term = S.current_term[s];                                  /* :10 */
+    out[i].candidate_id = s % e->P;                                   /* :11 */
+    out[i].last_log_index = last;                                     /* :12 */
+    out[i].last_log_term = term_at(e, s, last);                       /* :13 */
+    S.voted_for[s] = s % e->P;                                        /* :14 */
+    S.granted_votes[s] = 1;                                           /* :17 */
+  }
+  free(first);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a5: HandleRequestVote, raft_election.go:54-77 + isLogUpToDate              */
+/* ------------------------------------------------------------------------ */
+
+int ora_handle_request_vote(ora_engine *e, const mraft_rv_args *args,
+                            int64_t n, mraft_rv_reply *replies,
+                            int32_t *item_err) {
+  int32_t *first = claim_slots(e, &args[0].slot, n, sizeof(mraft_rv_args), item_err);
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&replies[i], 0, sizeof(replies[i]));
+    if (item_err[i]) continue;
+    const mraft_rv_args *a = &args[i];
+    int32_t v = a->slot;
+    if (a->term < S.current_term[v]) {                                /* :59-62 */
+      replies[i].term = S.current_term[v]; replies[i].vote_granted = 0;
+      continue;
+    }
+    if (a->term > S.current_term[v]) {                                /* :63-66 */
+      S.state[v] = MRAFT_FOLLOWER;
+      S.current_term[v] = a->term; S.voted_for[v] = -1;
+    }
+    replies[i].term = S.current_term[v];                              /* :67 */
+    int32_t my_last = S.last_index[v];
+    int32_t my_last_term = term_at(e, v, my_last);
+    int up_to_date = a->last_log_term > my_last_term ||               /* raft_log.go:99-104 */
+                     (my_last_term == a->last_log_term && a->last_log_index >= my_last);
+    if ((S.voted_for[v] == -1 || S.voted_for[v] == a->candidate_id) && up_to_date) {
+      S.voted_for[v] = a->candidate_id;                               /* :71 */
+      replies[i].vote_granted = 1;
+      continue;
+    }
+    replies[i].vote_granted = 0;                                      /* :76 */
+  }
+  free(first);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* a6 part 2: vote tally closure, raft_election.go:22-47 (guard :29)                      */
+/* ------------------------------------------------------------------------ */
+
+int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
+                             int64_t n, const int64_t *seg_begin,
+                             int64_t n_seg, int32_t *out_flags,
+                             int32_t *item_err) {
+  const int32_t P = e->P;
+  int64_t gp = (int64_t)e->G * P;
+  int64_t ns = seg_begin ? n_seg : n;
+  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t b = seg_begin ? seg_begin[s] : s, en = seg_begin ? seg_begin[s + 1] : s + 1;
+    if (b >= en) continue;
+    int32_t c = items[b].slot;
+    int32_t bad = 0;
+    if (c < 0 || c >= gp) bad = MRAFT_ITEM_BAD_SLOT;
+    else if (seen[c]) bad = MRAFT_ITEM_DUP_SLOT;
+    else {
+      for (int64_t i = b; i < en; ++i)
+        if (items[i].slot != c || items[i].peer < 0 || items[i].peer >= P ||
+            items[i].peer == c % P) bad = MRAFT_ITEM_BAD_SLOT;
+    }
+    if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
+    seen[c] = 1;
+    for (int64_t i = b; i < en; ++i) {
+      const mraft_rv_result *it = &items[i];
+      int32_t fl = 0;
+      if (S.current_term[c] == it->args_term && S.state[c] == MRAFT_CANDIDATE) { /* :29 */
+        if (it->vote_granted) {                                       /* :30 */
+          S.granted_votes[c] += 1;                                    /* :31 */
+          if (S.granted_votes[c] > P / 2) {                           /* :32 */
+            S.state[c] = MRAFT_LEADER;                                /* :33 */
+            for (int32_t j = 0; j < P; ++j) {                         /* :34-38 */
+              S.match_index[(int64_t)c * P + j] = 0;
+              S.next_index[(int64_t)c * P + j] = S.last_index[c] + 1;
+            }
+            fl |= MRAFT_F_BECAME_LEADER;
+          }
+        } else if (it->reply_term > S.current_term[c]) {              /* :42-45 */
+          S.state[c] = MRAFT_FOLLOWER;
+          S.current_term[c] = it->reply_term; S.voted_for[c] = -1;
+          fl |= MRAFT_F_STEPPED_DOWN;
+        }
+      }
+      out_flags[i] = fl;
+    }
+  }
+  free(seen);
+  return MRAFT_OK;
+}
+
+/* GetState, raft.go:237-246, per group. */
+int ora_export_group_status(ora_engine *e, const int32_t *leader_peer,
+                            int32_t *commit, int32_t *term_leader) {
+  for (int32_t g = 0; g < e->G; ++g) {
+    int32_t p = leader_peer ? leader_peer[g] : 0;
+    if (p < 0 || p >= e->P) p = 0;
+    int64_t s = (int64_t)g * e->P + p;
+    commit[g] = S.commit_index[s];
+    term_leader[g] = (int32_t)(((uint32_t)S.current_term[s] << 1) | (S.state[s] == MRAFT_LEADER));
+  }
+  return MRAFT_OK;
+}

@@ -1,0 +1,239 @@
+"""Generates tests/golden/kat.json: the known-answer tests K1-K14 of SURVEY.md
+§8c, hand-derived from the reference's Go source (cited per case), plus
+tests/golden/tick_vectors.npz: seeded replication-tick input/output vectors
+produced by the pure-Python restatement (oracle/pyoracle.py).
+
+The reference (Go) cannot run in this image, so the expected values of the
+KATs are derived by hand from the cited lines; this script asserts that the
+Python restatement reproduces each hand-derived value before writing the
+fixture. Run from the repo root:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import pyoracle as po  # noqa: E402
+
+LEADER, CANDIDATE, FOLLOWER = 1, 2, 3
+
+
+def one_group(P, L, slots):
+    """slots: {peer: dict(term, voted, state, commit, dummy, terms, match, next)}"""
+    st = {k: np.zeros(n, dtype=np.int64) for k, n in {
+        "current_term": P, "voted_for": P, "state": P, "commit_index": P, "last_applied": P,
+        "dummy_index": P, "last_index": P, "granted_votes": P, "log_term": P * L,
+        "match_index": P * P, "next_index": P * P}.items()}
+    st["voted_for"][:] = -1
+    st["state"][:] = FOLLOWER
+    for p in range(P):
+        st["log_term"][p * L] = 0
+    for p, d in slots.items():
+        st["current_term"][p] = d.get("term", 0)
+        st["voted_for"][p] = d.get("voted", -1)
+        st["state"][p] = d.get("state", FOLLOWER)
+        st["commit_index"][p] = d.get("commit", 0)
+        st["last_applied"][p] = d.get("commit", 0)
+        st["dummy_index"][p] = d.get("dummy", 0)
+        terms = d.get("terms", [0])
+        st["last_index"][p] = d.get("dummy", 0) + len(terms) - 1
+        st["log_term"][p * L:p * L + len(terms)] = terms
+        st["match_index"][p * P:(p + 1) * P] = d.get("match", [0] * P)
+        st["next_index"][p * P:(p + 1) * P] = d.get("next", [0] * P)
+    return {k: v.tolist() for k, v in st.items()}
+
+
+LT = [0, 1, 1, 2, 2, 3, 3, 4, 4, 4, 4]          # K1-K4 leader log, indices 0..10
+FT = [0, 1, 1, 2, 2, 2, 3]                      # K5-K8 follower log, indices 0..6
+
+
+def commit_kat(name, P, me, match, term, commit, peer, cite, expect):
+    """a2 success from `peer` (args rebuilding match[peer]) triggers a1."""
+    nxt = [m + 1 for m in match]
+    nxt[me] = len(LT)
+    m = list(match)
+    m[me] = 0
+    prev = m[peer] - 1
+    nxt[peer] = prev + 1
+    st = one_group(P, 16, {me: dict(term=term, voted=me, state=LEADER, commit=commit, terms=LT,
+                                    match=m, next=nxt)})
+    item = dict(slot=me, peer=peer, args_term=term, args_prev_log_index=prev, args_n_entries=1,
+                reply_term=term, reply_success=1, reply_conflict_index=0)
+    return dict(name=name, cite=cite, G=1, P=P, L=16, state=st, op="process_append_replies",
+                items=[item], expect={"commit_index": {str(me): expect}})
+
+
+def ae_kat(name, follower, args, cite, expect_reply, expect_state=None, P=3):
+    st = one_group(P, 16, {1: follower})
+    a = dict(slot=1, term=args["term"], leader_id=0, prev_log_index=args["prev"],
+             prev_log_term=args.get("prev_term", 0), leader_commit=args.get("leader_commit", 0),
+             n_entries=len(args.get("entries", [])), _pad=0, entries_offset=0)
+    return dict(name=name, cite=cite, G=1, P=P, L=16, state=st, op="handle_append_entries",
+                args=[a], entry_terms=args.get("entries", []) or [0],
+                expect={"reply": expect_reply, "slot1": expect_state or {}})
+
+
+def rv_kat(name, voter, args, cite, expect_reply, expect_state):
+    st = one_group(3, 16, {1: voter})
+    a = dict(slot=1, candidate_id=args.get("cand", 2), term=args["term"],
+             last_log_index=args["last_idx"], last_log_term=args["last_term"])
+    return dict(name=name, cite=cite, G=1, P=3, L=16, state=st, op="handle_request_vote",
+                args=[a], expect={"reply": expect_reply, "slot1": expect_state})
+
+
+def build():
+    ae = "src/raft/raft_append_entry.go"
+    kats = [
+        commit_kat("K1", 5, 0, [0, 7, 5, 3, 9], 4, 2, 1, f"{ae}:89-105", 7),
+        commit_kat("K2", 5, 0, [0, 7, 5, 3, 9], 5, 2, 1, f"{ae}:98 (Figure-8 gate)", 2),
+        commit_kat("K3", 3, 1, [8, 0, 2], 4, 0, 0, f"{ae}:89-105", 8),
+        commit_kat("K4", 4, 0, [0, 9, 7, 3], 4, 2, 1, f"{ae}:98 (P=4 needs 3 of 4)", 7),
+        ae_kat("K5", dict(term=3, terms=FT), dict(term=3, prev=5, prev_term=4),
+               f"{ae}:136-142 (ConflictIndex is one below the run)",
+               dict(term=3, success=0, conflict_index=2)),
+        ae_kat("K6", dict(term=3, terms=FT), dict(term=3, prev=9, prev_term=4),
+               f"{ae}:131-133", dict(term=3, success=0, conflict_index=7)),
+        ae_kat("K7", dict(term=3, terms=[0, 2, 2, 2]), dict(term=3, prev=3, prev_term=5),
+               f"{ae}:139 (scan stops at dummy+1)", dict(term=3, success=0, conflict_index=1)),
+        ae_kat("K8", dict(term=8, dummy=10, terms=[7, 7, 8]), dict(term=8, prev=8, prev_term=7),
+               f"{ae}:123-127 (reply.Term = 0)", dict(term=0, success=0, conflict_index=11)),
+        ae_kat("K9", dict(term=2, commit=1, terms=[0, 1, 1, 2, 2, 2]),
+               dict(term=3, prev=2, prev_term=1, entries=[2, 2], leader_commit=5),
+               f"{ae}:146-160 (no truncation when all match)",
+               dict(term=3, success=1, conflict_index=0),
+               dict(last_index=5, commit_index=5, current_term=3, voted_for=-1)),
+        ae_kat("K10", dict(term=2, commit=1, terms=[0, 1, 1, 2, 2, 2]),
+               dict(term=3, prev=2, prev_term=1, entries=[3], leader_commit=5),
+               f"{ae}:149-160 (truncate + append, commit vs whole log)",
+               dict(term=3, success=1, conflict_index=0),
+               dict(last_index=3, commit_index=3, log=[0, 1, 1, 3])),
+        rv_kat("K11", dict(term=5, voted=-1, terms=[0] + [4] * 10),
+               dict(term=5, last_term=4, last_idx=9), "src/raft/raft_log.go:99-104",
+               dict(term=5, vote_granted=0), dict(voted_for=-1)),
+        rv_kat("K12", dict(term=5, voted=-1, terms=[0] + [4] * 10),
+               dict(term=5, last_term=4, last_idx=10), "src/raft/raft_election.go:69-74",
+               dict(term=5, vote_granted=1), dict(voted_for=2)),
+        rv_kat("K13", dict(term=5, voted=-1, state=CANDIDATE, terms=[0] + [4] * 10),
+               dict(term=6, last_term=3, last_idx=10), "src/raft/raft_election.go:63-67",
+               dict(term=6, vote_granted=0), dict(current_term=6, voted_for=-1, state=FOLLOWER)),
+    ]
+    # K14: tally, P = 7, candidate peer 0: leader at the 3rd granted reply.
+    st = one_group(7, 16, {0: dict(term=5, voted=0, state=CANDIDATE, terms=[0, 1, 2])})
+    st["granted_votes"][0] = 1
+    items = [dict(slot=0, peer=p, args_term=5, reply_term=5, vote_granted=1) for p in (1, 2, 3, 4)]
+    kats.append(dict(name="K14", cite="src/raft/raft_election.go:29-38", G=1, P=7, L=16, state=st,
+                     op="process_vote_replies", items=items,
+                     expect={"flags": [0, 0, 8, 0], "slot0": dict(state=LEADER, granted_votes=4),
+                             "next0": [3] * 7, "match0": [0] * 7}))
+    return kats
+
+
+def run_py(k):
+    """Evaluate a KAT with the pure-Python restatement."""
+    G, P, L = k["G"], k["P"], k["L"]
+    st = {kk: np.array(v, dtype=np.int32) for kk, v in k["state"].items()}
+    rafts = po.from_soa(st, G, P, L)
+    out = {}
+    if k["op"] == "process_append_replies":
+        flags = []
+        for it in k["items"]:
+            rf = rafts[it["slot"]]
+            args = po.AppendEntriesArgs(Term=it["args_term"], LeaderId=rf.me,
+                                        Entries=[None] * it["args_n_entries"],
+                                        PrevLogIndex=it["args_prev_log_index"], PrevLogTerm=0,
+                                        LeaderCommit=0)
+            rep = po.AppendEntriesReply(Term=it["reply_term"], Success=bool(it["reply_success"]),
+                                        ConflictIndex=it["reply_conflict_index"])
+            flags.append(rf.processAppendEntriesReply(it["peer"], args, rep))
+        out["flags"] = flags
+    elif k["op"] == "handle_append_entries":
+        a = k["args"][0]
+        rf = rafts[a["slot"]]
+        ents = [po.Entry(a["prev_log_index"] + 1 + i, t)
+                for i, t in enumerate(k["entry_terms"][:a["n_entries"]])]
+        args = po.AppendEntriesArgs(Term=a["term"], LeaderId=a["leader_id"], Entries=ents,
+                                    PrevLogIndex=a["prev_log_index"], PrevLogTerm=a["prev_log_term"],
+                                    LeaderCommit=a["leader_commit"])
+        rep = po.AppendEntriesReply()
+        rf.HandleAppendEntries(args, rep)
+        out["reply"] = dict(term=rep.Term, success=int(rep.Success), conflict_index=rep.ConflictIndex)
+    elif k["op"] == "handle_request_vote":
+        a = k["args"][0]
+        rf = rafts[a["slot"]]
+        rep = po.RequestVoteReply()
+        rf.HandleRequestVote(po.RequestVoteArgs(CandidateId=a["candidate_id"], Term=a["term"],
+                                                LastLogIndex=a["last_log_index"],
+                                                LastLogTerm=a["last_log_term"]), rep)
+        out["reply"] = dict(term=rep.Term, vote_granted=int(rep.VoteGranted))
+    elif k["op"] == "process_vote_replies":
+        flags = []
+        for it in k["items"]:
+            rf = rafts[it["slot"]]
+            flags.append(rf.tally(po.RequestVoteArgs(CandidateId=rf.me, Term=it["args_term"],
+                                                     LastLogIndex=0, LastLogTerm=0),
+                                  po.RequestVoteReply(Term=it["reply_term"],
+                                                      VoteGranted=bool(it["vote_granted"]))))
+        out["flags"] = flags
+    out["state"] = po.to_soa(rafts, st, G, P, L)
+    return out
+
+
+def check_kat(k, out):
+    """Assert that evaluation output `out` (flags/reply/state) meets k['expect']."""
+    e = k["expect"]
+    st = out["state"]
+    P, L = k["P"], k["L"]
+    if "commit_index" in e:
+        for s, v in e["commit_index"].items():
+            assert st["commit_index"][int(s)] == v, (k["name"], st["commit_index"][int(s)], v)
+    if "reply" in e:
+        for f, v in e["reply"].items():
+            assert out["reply"][f] == v, (k["name"], f, out["reply"][f], v)
+    for key, slot in (("slot1", 1), ("slot0", 0)):
+        for f, v in e.get(key, {}).items():
+            if f == "log":
+                got = list(st["log_term"][slot * L: slot * L + len(v)])
+                assert got == v, (k["name"], got, v)
+            else:
+                assert st[f][slot] == v, (k["name"], f, st[f][slot], v)
+    if "flags" in e:
+        assert list(out["flags"]) == e["flags"], (k["name"], out["flags"], e["flags"])
+    if "next0" in e:
+        assert list(st["next_index"][0:P]) == e["next0"], k["name"]
+        assert list(st["match_index"][0:P]) == e["match0"], k["name"]
+
+
+def tick_vectors():
+    """Seeded tick vectors: inputs from the synthetic generator, outputs from
+    the Python restatement (independent of the C oracle under test)."""
+    from multiraft_amd import synth_tick_state
+    out = {}
+    for i, (G, P, L) in enumerate([(24, 3, 32), (16, 5, 64), (12, 7, 48)]):
+        st, lp, _ = synth_tick_state(G, P, L, seed=0x5EED + i, nthreads=1)
+        pst, gf = po.replicate_tick(st, G, P, L, lp)
+        out[f"v{i}_dims"] = np.array([G, P, L], dtype=np.int32)
+        out[f"v{i}_leader_peer"] = lp
+        for kk, v in st.items():
+            out[f"v{i}_in_{kk}"] = v
+        for kk, v in pst.items():
+            out[f"v{i}_out_{kk}"] = v.astype(np.int32)
+        out[f"v{i}_flags"] = gf
+    return out
+
+
+if __name__ == "__main__":
+    kats = build()
+    for k in kats:
+        check_kat(k, run_py(k))
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kats, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "tick_vectors.npz"), **tick_vectors())
+    print(f"wrote {len(kats)} KATs and tick vectors")

@@ -1,0 +1,166 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so) with the same method
+names as multiraft_amd.engine.Engine. Test infrastructure only."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from multiraft_amd._abi import (AE_ARGS, AE_REPLY, AE_RESULT, RV_ARGS, RV_REPLY, RV_RESULT,
+                                MraftSoa, ptr, soa_of)
+from multiraft_amd.engine import copy_state
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+class OraEngine(ctypes.Structure):
+    _fields_ = [("G", ctypes.c_int32), ("P", ctypes.c_int32), ("L", ctypes.c_int32),
+                ("s", MraftSoa)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        l = ctypes.CDLL(_PATH)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        E = ctypes.POINTER(OraEngine)
+        sigs = {
+            "ora_count_enable": [E], "ora_count_disable": [], "ora_count_result": [vp],
+            "ora_gather_append_args": [E, vp, vp, i64, vp, vp],
+            "ora_handle_append_entries": [E, vp, i64, vp, i64, vp, vp],
+            "ora_process_append_replies": [E, vp, i64, vp, i64, vp, vp],
+            "ora_replicate_tick": [E, vp, vp],
+            "ora_replicate_tick_mt": [E, vp, vp, i32],
+            "ora_start_election": [E, vp, i64, vp, vp],
+            "ora_handle_request_vote": [E, vp, i64, vp, vp],
+            "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
+            "ora_export_group_status": [E, vp, vp, vp],
+        }
+        for n, a in sigs.items():
+            f = getattr(l, n)
+            f.argtypes = a
+            f.restype = None if n in ("ora_count_disable", "ora_count_result") else ctypes.c_int
+        _lib = l
+    return _lib
+
+
+class Oracle:
+    """CPU restatement with the Engine's interface; operates on its own copy
+    of the state."""
+
+    def __init__(self, G: int, P: int, L: int, st: dict):
+        self.G, self.P, self.L = G, P, L
+        self.st = copy_state(st)
+        self._e = OraEngine(G, P, L, soa_of(self.st))
+
+    def state(self) -> dict:
+        return self.st
+
+    def replicate_tick(self, leader_peer, nthreads: int = 1):
+        lp = np.ascontiguousarray(leader_peer, dtype=np.int32)
+        gf = np.zeros(self.G, dtype=np.int32)
+        if nthreads > 1:
+            lib().ora_replicate_tick_mt(ctypes.byref(self._e), ptr(lp), ptr(gf), nthreads)
+        else:
+            lib().ora_replicate_tick(ctypes.byref(self._e), ptr(lp), ptr(gf))
+        return gf
+
+    def replicate_tick_count(self, leader_peer):
+        """Counts on a scratch copy (the state is left untouched)."""
+        scratch = Oracle(self.G, self.P, self.L, self.st)
+        L = lib()
+        L.ora_count_enable(ctypes.byref(scratch._e))
+        try:
+            gf = scratch.replicate_tick(leader_peer)
+            out = (ctypes.c_int64 * 2)()
+            L.ora_count_result(out)
+        finally:
+            L.ora_count_disable()
+        active = int(np.count_nonzero(gf & 1))
+        return int(out[0]), int(out[1]), active
+
+    def gather_append_args(self, slots, peers):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=AE_ARGS)
+        err = np.zeros(n, dtype=np.int32)
+        lib().ora_gather_append_args(ctypes.byref(self._e), ptr(slots), ptr(peers), n, ptr(out), ptr(err))
+        return out, err
+
+    def handle_append_entries(self, args, entry_terms):
+        args = np.ascontiguousarray(args, dtype=AE_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=AE_REPLY)
+        err = np.zeros(n, dtype=np.int32)
+        et = None if entry_terms is None else np.ascontiguousarray(entry_terms, dtype=np.int32)
+        lib().ora_handle_append_entries(ctypes.byref(self._e), ptr(args), n, ptr(et),
+                                        0 if et is None else len(et), ptr(rep), ptr(err))
+        return rep, err
+
+    def process_append_replies(self, items, seg_begin=None):
+        items = np.ascontiguousarray(items, dtype=AE_RESULT)
+        n = len(items)
+        flags = np.zeros(n, dtype=np.int32)
+        err = np.zeros(n, dtype=np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        lib().ora_process_append_replies(ctypes.byref(self._e), ptr(items), n, ptr(sb),
+                                         0 if sb is None else len(sb) - 1, ptr(flags), ptr(err))
+        return flags, err
+
+    def start_election(self, slots):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=RV_ARGS)
+        err = np.zeros(n, dtype=np.int32)
+        lib().ora_start_election(ctypes.byref(self._e), ptr(slots), n, ptr(out), ptr(err))
+        return out, err
+
+    def handle_request_vote(self, args):
+        args = np.ascontiguousarray(args, dtype=RV_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=RV_REPLY)
+        err = np.zeros(n, dtype=np.int32)
+        lib().ora_handle_request_vote(ctypes.byref(self._e), ptr(args), n, ptr(rep), ptr(err))
+        return rep, err
+
+    def process_vote_replies(self, items, seg_begin=None):
+        items = np.ascontiguousarray(items, dtype=RV_RESULT)
+        n = len(items)
+        flags = np.zeros(n, dtype=np.int32)
+        err = np.zeros(n, dtype=np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        lib().ora_process_vote_replies(ctypes.byref(self._e), ptr(items), n, ptr(sb),
+                                       0 if sb is None else len(sb) - 1, ptr(flags), ptr(err))
+        return flags, err
+
+    def export_group_status(self, leader_peer=None):
+        commit = np.zeros(self.G, dtype=np.int32)
+        tl = np.zeros(self.G, dtype=np.int32)
+        lp = None if leader_peer is None else np.ascontiguousarray(leader_peer, dtype=np.int32)
+        lib().ora_export_group_status(ctypes.byref(self._e), ptr(lp), ptr(commit), ptr(tl))
+        return commit, tl
+
+
+def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = ""):
+    """Compare two state images. Log slots beyond lastIndex are dead and may
+    differ (the reference's slice has no such slots), so only live slots
+    [0, last-dummy] of every replica are compared."""
+    for k in a:
+        if k == "log_term":
+            continue
+        if not np.array_equal(a[k], b[k]):
+            bad = np.nonzero(a[k] != b[k])[0][:8]
+            raise AssertionError(f"{ctx}: {k} differs at {bad}: {a[k][bad]} vs {b[k][bad]}")
+    la = a["log_term"].reshape(G * P, L)
+    lb = b["log_term"].reshape(G * P, L)
+    live = a["last_index"] - a["dummy_index"]
+    mask = np.arange(L)[None, :] <= live[:, None]
+    if not np.array_equal(np.where(mask, la, 0), np.where(mask, lb, 0)):
+        rows = np.nonzero((np.where(mask, la, 0) != np.where(mask, lb, 0)).any(axis=1))[0][:8]
+        raise AssertionError(f"{ctx}: log_term differs in replicas {rows}")

@@ -1,0 +1,47 @@
+"""CPU checks of the boundary: the shared library loads without a GPU and
+exports every symbol include/mraft.h declares (no compute calls)."""
+import ctypes
+import os
+import re
+
+from multiraft_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    return set(re.findall(r"^\s*(?:int|int64_t|void\s*\*|const char\s*\*)\s*\*?\s*(mraft_\w+)\s*\(",
+                          txt, re.M))
+
+
+def test_header_symbols_match_binding_list():
+    assert _declared("mraft.h") == set(_abi.ABI_SYMBOLS)
+    assert _declared("mraft_synth.h") == set(_abi.SYNTH_SYMBOLS)
+
+
+def test_library_exports_every_symbol():
+    assert os.path.exists(_abi.LIB_PATH), "build libmraft_hip.so first"
+    lib = ctypes.CDLL(_abi.LIB_PATH)
+    for s in _abi.ABI_SYMBOLS:
+        assert hasattr(lib, s), s
+    syn = ctypes.CDLL(_abi.SYNTH_PATH)
+    for s in _abi.SYNTH_SYMBOLS:
+        assert hasattr(syn, s), s
+
+
+def test_abi_version_and_struct_sizes():
+    lib = _abi.lib()
+    assert lib.mraft_abi_version() == 1
+    assert _abi.AE_ARGS.itemsize == 40
+    assert _abi.AE_REPLY.itemsize == 16
+    assert _abi.RV_RESULT.itemsize == 20
+    assert ctypes.sizeof(_abi.MraftSoa) == 11 * 8
+
+
+def test_create_rejects_bad_dims_without_gpu():
+    lib = _abi.lib()
+    h = ctypes.c_void_p()
+    assert lib.mraft_create(0, 5, 16, 0, 0, ctypes.byref(h)) == _abi.E_INVAL
+    assert lib.mraft_create(4, 9, 16, 0, 0, ctypes.byref(h)) == _abi.E_INVAL
+    assert b"bad dims" in lib.mraft_last_error_string()
