@@ -119,7 +119,10 @@ def main():
               f"{' (restore inside timed steps)' if restore else ''}")
 
     eng = Engine(G, P, L, device=local, alloc=False)
-    stream = torch.cuda.current_stream(dev)
+    # A dedicated (non-null) stream shared by torch and the engine, so the
+    # events below bracket exactly the engine's kernels.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     lp_d = torch.from_numpy(lp).to(dev)
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
