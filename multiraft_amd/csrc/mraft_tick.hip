@@ -75,76 +75,125 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// One chunk of the multi-follower merge pass. VEC: lane j owns entries
-// c+4j .. c+4j+3 (one dwordx4 per stream); otherwise lane j owns c+j+64u.
-// Leader entry idx lives at log[eo + idx], follower q's at log[fo[q] + idx].
-template <int NI, bool VEC, bool COUNT>
-__device__ __forceinline__ void merge_chunk(int32_t *__restrict__ log, long long eo,
-                                            const long long (&fo)[NI], const int (&start)[NI],
-                                            const int (&cend)[NI], const int (&nend)[NI],
-                                            int (&mode)[NI], int (&cfrom)[NI],
-                                            const int (&capok)[NI], int &fullmask, int c, int hi) {
+// One chunk of the streaming pass over the leader's log. The pass serves
+// (1) every follower q's entry merge: compare entries [start_q, cend_q) with
+// the follower's log, then (from the first mismatch) copy entries up to `hi`
+// into it; and (2) the exact commit scan: the largest index in [slo, shi]
+// whose term equals T (kept in `found`, the pass ascends).
+// VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
+// otherwise lane j owns c+64(4v+u)+j. Leader entry idx is log[eo + idx],
+// follower q's is log[fo[q] + idx].
+template <int NI, int V, bool VEC, bool COUNT>
+__device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long eo,
+                                           const long long (&fo)[NI], const int (&start)[NI],
+                                           const int (&cend)[NI], int nend, int (&mode)[NI],
+                                           int (&cfrom)[NI], const int (&capok)[NI],
+                                           int &fullmask, int slo, int shi, int T, int &found,
+                                           int c, int plo, int phi) {
+  constexpr int CW = 256 * V;
   const int lane = lane_id();
-  int idx[4];
-  int e[4];
+  int idx[V][4], e[V][4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) idx[u] = VEC ? c + 4 * lane + u : c + lane + 64 * u;
-  if (VEC) {
-    int4 v = make_int4(0, 0, 0, 0);
-    if (idx[0] <= hi) v = *reinterpret_cast<const int4 *>(log + eo + idx[0]);
-    e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
-  } else {
+  for (int v = 0; v < V; ++v)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = idx[u] <= hi ? log[eo + idx[u]] : 0;
-  }
-  // Issue every follower's loads before any compare (more bytes in flight).
-  int f[NI][4];
+    for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
+  // Leader entries, then every comparing follower's terms: all loads in flight
+  // before the first compare.
 #pragma unroll
-  for (int q = 0; q < NI; ++q) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) f[q][u] = 0;
-    if (mode[q] != M_CMP || start[q] > c + 255 || cend[q] <= c) continue;
+  for (int v = 0; v < V; ++v) {
     if (VEC) {
-      if (idx[3] >= start[q] && idx[0] < cend[q]) {
-        const int4 v = *reinterpret_cast<const int4 *>(log + fo[q] + idx[0]);
-        f[q][0] = v.x; f[q][1] = v.y; f[q][2] = v.z; f[q][3] = v.w;
-      }
+      int4 x = make_int4(0, 0, 0, 0);
+      if (idx[v][3] >= plo && idx[v][0] <= phi) x = *reinterpret_cast<const int4 *>(log + eo + idx[v][0]);
+      e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (idx[u] >= start[q] && idx[u] < cend[q]) f[q][u] = log[fo[q] + idx[u]];
+      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? log[eo + idx[v][u]] : 0;
     }
+  }
+  int f[NI][V][4];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f[q][v][u] = 0;
+    if (mode[q] != M_CMP || start[q] > c + CW - 1 || cend[q] <= c) continue;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (VEC) {
+        if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
+          const int4 x = *reinterpret_cast<const int4 *>(log + fo[q] + idx[v][0]);
+          f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = log[fo[q] + idx[v][u]];
+      }
+    }
+  }
+  // Commit scan: highest index of this chunk in [slo, shi] with term T.
+  if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+    int hit = -1;
+#pragma unroll
+    for (int v = V - 1; v >= 0; --v) {
+      if (hit >= 0) break;
+      if (VEC) {
+        int lu = -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
+        const unsigned long long m = __ballot(lu >= 0);
+        if (m) {
+          const int l = 63 - __clzll((long long)m);
+          hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
+        }
+      } else {
+#pragma unroll
+        for (int u = 3; u >= 0; --u) {
+          if (hit >= 0) break;
+          const unsigned long long m =
+              __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
+          if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
+        }
+      }
+    }
+    if (hit >= 0) found = hit;
   }
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
-    if (mode[q] == M_DONE || start[q] > c + 255) continue;
+    if (mode[q] == M_DONE || start[q] > c + CW - 1) continue;
     if (mode[q] == M_CMP) {
       int im = -1;  // first mismatching entry index in this chunk
       if (cend[q] > c) {
-        if (VEC) {
-          int first = 4;
 #pragma unroll
-          for (int u = 3; u >= 0; --u)
-            if (idx[u] >= start[q] && idx[u] < cend[q] && e[u] != f[q][u]) first = u;
-          const unsigned long long m = __ballot(first < 4);
-          if (m) {
-            const int l = first_lane(m);
-            im = c + 4 * l + __shfl(first, l, 64);
-          }
-        } else {
+        for (int v = 0; v < V; ++v) {
+          if (im >= 0) break;
+          if (VEC) {
+            int first = 4;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const unsigned long long m =
-                __ballot(idx[u] >= start[q] && idx[u] < cend[q] && e[u] != f[q][u]);
-            if (m && im < 0) im = c + 64 * u + first_lane(m);
+            for (int u = 3; u >= 0; --u)
+              if (idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]) first = u;
+            const unsigned long long m = __ballot(first < 4);
+            if (m) {
+              const int l = first_lane(m);
+              im = c + 256 * v + 4 * l + __shfl(first, l, 64);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const unsigned long long m =
+                  __ballot(idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]);
+              if (m && im < 0) im = c + 64 * (4 * v + u) + first_lane(m);
+            }
           }
         }
       }
-      if (im < 0 && cend[q] <= c + 255) {
+      if (im < 0 && cend[q] <= c + CW - 1) {
         // Compared region ends in this chunk without a mismatch: either every
-        // entry matched (no truncation, the non-FIFO guard) or the follower's
-        // log ends before the entries do (mismatch "beyond the end").
-        if (cend[q] < nend[q]) im = cend[q];
+        // entry matched (no truncation: the non-FIFO guard, :146-155) or the
+        // follower's log ends before the entries do ("beyond the end").
+        if (cend[q] < nend) im = cend[q];
         else mode[q] = M_DONE;
       }
       if (im >= 0) {
@@ -159,76 +208,124 @@ __device__ __forceinline__ void merge_chunk(int32_t *__restrict__ log, long long
     }
     if (mode[q] == M_COPY) {
       if (!COUNT) {
-        if (VEC) {
-          if (idx[0] >= cfrom[q] && idx[3] <= hi) {
-            *reinterpret_cast<int4 *>(log + fo[q] + idx[0]) = make_int4(e[0], e[1], e[2], e[3]);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
+            *reinterpret_cast<int4 *>(log + fo[q] + idx[v][0]) =
+                make_int4(e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[u] >= cfrom[q] && idx[u] <= hi) log[fo[q] + idx[u]] = e[u];
+              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) log[fo[q] + idx[v][u]] = e[v][u];
           }
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (idx[u] >= cfrom[q] && idx[u] <= hi) log[fo[q] + idx[u]] = e[u];
         }
       }
-      if (c + 255 >= hi) mode[q] = M_DONE;
+      if (c + CW >= nend) mode[q] = M_DONE;
     }
   }
 }
+
+// Reply fold of one group (processAppendEntriesReply, :66-88, in peer order),
+// wave-uniform. Inputs per follower slot q come from lane q.
+template <int P>
+struct Fold {
+  static constexpr int NI = P - 1;
+  int term, stepped, any, mstar;
+  int gate[NI], rs[NI], rp[NI], rn[NI], rx[NI], ic[NI];
+
+  __device__ __forceinline__ void run(int T, int lp, int (&mm)[P], unsigned long long have_m,
+                                      unsigned long long succ_m, int rterm, int prev, int n,
+                                      int rci, int icls) {
+    term = T;
+    stepped = 0;
+    any = 0;
+    mstar = INT32_MIN;
+    int role = kLeader;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      const int pq = q < lp ? q : q + 1;
+      gate[q] = 0;
+      rs[q] = (int)((succ_m >> q) & 1);
+      rp[q] = uni(__shfl(prev, q, 64));
+      rn[q] = uni(__shfl(n, q, 64));
+      rx[q] = rp[q] + 1;                                                 // nextIndex[q] (gathered)
+      ic[q] = uni(__shfl(icls, q, 64));
+      const int rt = uni(__shfl(rterm, q, 64));
+      const int rc = uni(__shfl(rci, q, 64));
+      if (!((have_m >> q) & 1)) continue;
+      if (rt > term) {                                                   // :67-72
+        term = rt;
+        role = kFollower;
+        stepped = 1;
+      } else if (rt == term && role == kLeader && T == term) {           // :73-74 (prev gate holds)
+        gate[q] = 1;
+        if (rs[q]) {
+#pragma unroll
+          for (int j = 0; j < P; ++j)
+            if (j == pq) mm[j] = rp[q] + rn[q];                          // :76
+          rx[q] = rp[q] + rn[q] + 1;                                     // :77
+          mstar = max(mstar, quorum_match<P>(mm, lp));                   // :78 -> a1
+          any = 1;
+        } else {
+          rx[q] = rc;                                                    // :82
+        }
+      }
+    }
+  }
+};
 
 template <int P, bool COUNT>
 __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
                                                     int32_t *__restrict__ gflags,
                                                     unsigned long long *__restrict__ counts) {
   constexpr int NI = P - 1;
+  constexpr int V = 2;
   const int lane = lane_id();
   const int g = uni((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
   if (g >= s.G) return;
   const int L = s.L;
-  long long hR = 0;          // algorithmic words of the header (wave-uniform)
-  long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
-  int flags = 0, active = 0;
 
   // ------------------------------------------------------------ header
   const int lp = uni(leader_peer[g]);
-  const long long ld = (long long)g * P + lp;
-  int T = 0, c0 = 0, last = 0, ldummy = 0;
-  bool go = false;
-  if (lp >= P) {
-    flags = MRAFT_G_ERROR;
-  } else if (lp >= 0) {
-    hR = 1;
-    if (uni(s.role[ld]) == kLeader) {
-      T = uni(s.term[ld]);
-      c0 = uni(s.commit[ld]);
-      last = uni(s.last[ld]);
-      ldummy = uni(s.dummy[ld]);
-      hR = 5;
-      if (c0 < ldummy) flags = MRAFT_G_ERROR;  // outside the reachable states
-      else go = true;
-    }
+  if (lp < 0 || lp >= P) {
+    if (!COUNT && lane == 0 && gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
+    return;
   }
-  if (!go) {
+  const long long ld = (long long)g * P + lp;
+  const long long lrow = ld * L;
+  // Every load that depends only on the leader index, issued together.
+  const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
+            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]);
+  int mm[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) mm[j] = uni(s.match[ld * P + j]);
+  const int p = lane < lp ? lane : lane + 1;
+  const long long f = (long long)g * P + p;
+  int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0;
+  if (lane < NI) {
+    nxt = s.next[ld * P + p];
+    fterm = s.term[f];
+    fdummy = s.dummy[f];
+    flast = s.last[f];
+    fcommit = s.commit[f];
+  }
+  long long hR = 1;  // algorithmic words of the header (wave-uniform)
+  if (role != kLeader || c0 < ldummy) {
+    // not a leader: appendOneRound returns (:22-25); commit < dummy: outside
+    // the reachable states (include/mraft.h MRAFT_ITEM_BAD_STATE).
     if (COUNT) {
-      if (lane == 0) atomicAdd(&counts[0], (unsigned long long)hR);
+      if (lane == 0) atomicAdd(&counts[0], (unsigned long long)(role != kLeader ? 1 : 5));
     } else if (lane == 0 && gflags) {
-      gflags[g] = flags;
+      gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
     }
     return;
   }
+  hR = 5 + NI;
 
   // ------------------------------------------------------------ phase A
-  const long long lrow = ld * L;
-  int icls = IC_NONE, p = 0, prev = 0, n = 0, fdummy = 0, flast = 0, ft = 0, fterm = 0;
-  long long f = 0;
-  if (lane < NI) {
-    p = lane < lp ? lane : lane + 1;
-    prev = s.next[ld * P + p] - 1;                                       // :26
-    icls = prev < ldummy ? IC_SNAP : (prev > last ? IC_PANIC : IC_GO);   // :27, :41
-  }
-  hR += NI;
+  int icls = IC_NONE;
+  const int prev = nxt - 1;                                              // :26
+  if (lane < NI) icls = prev < ldummy ? IC_SNAP : (prev > last ? IC_PANIC : IC_GO);  // :27, :41
   const unsigned long long snap_m = __ballot(icls == IC_SNAP);
   if (__ballot(icls == IC_PANIC)) {  // a3 would panic: the whole group is skipped
     if (COUNT) {
@@ -238,17 +335,17 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
     }
     return;
   }
-  active = 1;
-  flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
+  int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
+  const int probe_last = uni(s.log[lrow + (last - ldummy)]);             // speculative a1 probe
+  int prev_term = 0, ft = 0;
+  if (icls == IC_GO) {
+    prev_term = s.log[lrow + (prev - ldummy)];                           // :49
+    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + (prev - fdummy)];
+  }
+  const int n = last - prev;                                             // :50
   int rterm = 0, rsucc = 0, rci = 0;
   bool adopt = false;
   if (icls == IC_GO) {
-    f = (long long)g * P + p;
-    const int prev_term = s.log[lrow + (prev - ldummy)];                 // :49
-    fterm = s.term[f];
-    fdummy = s.dummy[f];
-    flast = s.last[f];
-    n = last - prev;                                                     // :50
     if (T < fterm) {                                                     // :112-115
       icls = IC_STALE;
       rterm = fterm;
@@ -262,15 +359,12 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
         if (prev > flast) {                                              // :131-133
           icls = IC_BEYOND;
           rci = flast + 1;
+        } else if (ft != prev_term) {                                    // :128
+          if (prev > fdummy + 1) icls = IC_SCAN;
+          else { icls = IC_MISMATCH; rci = prev; }
         } else {
-          ft = s.log[f * L + (prev - fdummy)];
-          if (ft != prev_term) {                                         // :128
-            if (prev > fdummy + 1) icls = IC_SCAN;
-            else { icls = IC_MISMATCH; rci = prev; }
-          } else {
-            rsucc = 1;
-            icls = n > 0 ? IC_MERGE : IC_HB;
-          }
+          rsucc = 1;
+          icls = n > 0 ? IC_MERGE : IC_HB;
         }
       }
     }
@@ -292,154 +386,137 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
       }
     }
   }
-  int mk = -1;  // this lane's follower: first mismatching entry of its merge
+
+  // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
-  if (merge_m) {
-    long long fo[NI];
-    int start[NI], cend[NI], nend[NI], mode[NI], cfrom[NI], capok[NI];
-    int lo = last + 1;
-    bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
-    const long long eo = lrow - ldummy;
+  long long fo[NI];
+  int start[NI], cend[NI], mode[NI], cfrom[NI], capok[NI];
+  int mlo = last + 1, maybe_full = 0;
+  const long long eo = lrow - ldummy;
+  bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
 #pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      const int qp = q < lp ? q : q + 1;
-      const int sp = __shfl(prev, q, 64), sd = __shfl(fdummy, q, 64), sl = __shfl(flast, q, 64);
-      fo[q] = ((long long)g * P + qp) * L - sd;
-      start[q] = sp + 1;
-      nend[q] = last + 1;                      // entries are [prev+1, last]
-      cend[q] = min(last, sl) + 1;             // compared while the follower has the slot
-      cfrom[q] = 0;
-      capok[q] = (long long)last - sd <= (long long)L - 1;
-      mode[q] = ((merge_m >> q) & 1) ? M_CMP : M_DONE;
-      if (mode[q] == M_CMP) {
-        lo = min(lo, start[q]);
-        vec = vec && (((fo[q] - eo) & 3) == 0);
+  for (int q = 0; q < NI; ++q) {
+    const int qp = q < lp ? q : q + 1;
+    const int sp = uni(__shfl(prev, q, 64)), sd = uni(__shfl(fdummy, q, 64)),
+              sl = uni(__shfl(flast, q, 64));
+    fo[q] = ((long long)g * P + qp) * L - sd;
+    start[q] = sp + 1;
+    cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
+    cfrom[q] = 0;
+    capok[q] = (long long)last - sd <= (long long)L - 1;
+    mode[q] = ((merge_m >> q) & 1) ? M_CMP : M_DONE;
+    if (mode[q] == M_CMP) {
+      mlo = min(mlo, start[q]);
+      vec = vec && (((fo[q] - eo) & 3) == 0);
+      maybe_full |= !capok[q];
+    }
+  }
+
+  // Fold before the pass when no follower can be rejected for capacity (then
+  // every merge replies success whatever its mismatch point), so the exact
+  // commit scan of a Figure-8 group rides along the same streaming pass.
+  Fold<P> fd;
+  int commit = c0, top = 0, slo = 1, shi = 0;
+  const unsigned long long have0 = __ballot(icls >= IC_STALE && icls <= IC_HB);
+  const unsigned long long succ0 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+  if (!maybe_full) {
+    fd.run(T, lp, mm, have0, succ0, rterm, prev, n, rci, icls);
+    if (fd.any) {
+      top = min(fd.mstar, last);
+      if (top > c0) {
+        const int t = top == last ? probe_last : uni(s.log[lrow + (top - ldummy)]);  // :98
+        if (t == T) commit = top;
+        else { slo = c0 + 1; shi = top - 1; }
       }
     }
-    int fullmask = 0;
+  }
+  int fullmask = 0, found = -1;
+  if (merge_m || slo <= shi) {
+    const int plo = min(mlo, slo <= shi ? slo : mlo);
+    const int phi = merge_m ? last : shi;
     if (vec) {
-      const int a0 = lo - (int)((eo + lo) & 3);
-      for (int c = a0; c <= last; c += 256)
-        merge_chunk<NI, true, COUNT>(s.log, eo, fo, start, cend, nend, mode, cfrom, capok, fullmask,
-                                     c, last);
+      for (int c = plo - (int)((eo + plo) & 3); c <= phi; c += 256 * V)
+        pass_chunk<NI, V, true, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
+                                       fullmask, slo, shi, T, found, c, plo, phi);
     } else {
-      for (int c = lo; c <= last; c += 256)
-        merge_chunk<NI, false, COUNT>(s.log, eo, fo, start, cend, nend, mode, cfrom, capok,
-                                      fullmask, c, last);
+      for (int c = plo; c <= phi; c += 256 * V)
+        pass_chunk<NI, V, false, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
+                                        fullmask, slo, shi, T, found, c, plo, phi);
     }
+  }
+  int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (lane == q && icls == IC_MERGE) {
-        // k* relative to the first entry; -1 when every entry matched.
-        mk = (cfrom[q] > 0 || ((fullmask >> q) & 1)) ? cfrom[q] - start[q] : -1;
-        if ((fullmask >> q) & 1) icls = IC_FULL;
+  for (int q = 0; q < NI; ++q) {
+    if (lane == q && icls == IC_MERGE) {
+      mk = (cfrom[q] > 0 || ((fullmask >> q) & 1)) ? cfrom[q] - start[q] : -1;
+      if ((fullmask >> q) & 1) icls = IC_FULL;
+    }
+  }
+  if (!maybe_full) {
+    if (slo <= shi && found > c0) commit = found;
+  } else {
+    const unsigned long long have1 = __ballot(icls >= IC_STALE && icls <= IC_HB);
+    const unsigned long long succ1 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+    fd.run(T, lp, mm, have1, succ1, rterm, prev, n, rci, icls);
+    if (fd.any) {
+      top = min(fd.mstar, last);
+      if (top > c0) {
+        if (uni(s.log[lrow + (top - ldummy)]) == T) {
+          commit = top;
+        } else {
+          const int i = wave_scan_down_eq(s.log + lrow, ldummy, c0 + 1, top - 1, T);
+          if (i > c0) commit = i;
+        }
       }
     }
   }
 
   // ------------------------------------------------------------ phase C
   int fcadv = 0;
-  const int LC = c0;
+  long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
   if (icls >= IC_STALE && icls <= IC_HB) {
     if (icls == IC_STALE) {
-      cR += 1;
+      cR = 1;
     } else {
       if (!COUNT) {
         if (adopt) { s.term[f] = T; s.voted[f] = -1; }
         s.role[f] = kFollower;                                           // :120
       }
-      long long r = 2, w = (adopt ? 2 : 0) + 1;                          // term, dummy; role
-      if (icls != IC_BELOW) r += 1;                                      // last
-      if (icls >= IC_MISMATCH) r += 1;                                   // log[prev]
-      if (icls == IC_SCAN) r += scan_extra;
+      cR = 2;                                                            // term, dummy
+      cW = (adopt ? 2 : 0) + 1;                                          // role
+      if (icls != IC_BELOW) cR += 1;                                     // last
+      if (icls >= IC_MISMATCH) cR += 1;                                  // log[prev]
+      if (icls == IC_SCAN) cR += scan_extra;
       if (icls == IC_MERGE || icls == IC_HB) {
         int newlast = flast;
         if (icls == IC_MERGE) {
           const int kc = min(n, flast - prev);
-          r += (mk < 0) ? n : (mk < kc ? mk + 1 : mk);                  // compared follower terms
+          cR += (mk < 0) ? n : (mk < kc ? mk + 1 : mk);                 // compared follower terms
           if (mk >= 0) {
             newlast = prev + n;
             if (!COUNT) s.last[f] = newlast;
-            w += (n - mk) + 1;
+            cW += (n - mk) + 1;
           }
         }
-        const int fc = s.commit[f];                                      // :157-160
-        r += 1;
-        if (LC > fc) {
+        cR += 1;                                                         // :157-160
+        if (c0 > fcommit) {
           fcadv = 1;
-          w += 1;
-          if (!COUNT) s.commit[f] = min(LC, newlast);
+          cW += 1;
+          if (!COUNT) s.commit[f] = min(c0, newlast);
         }
       }
-      cR += r;
-      cW += w;
     }
   }
   if (__ballot(icls == IC_FULL)) flags |= MRAFT_G_LOG_FULL;
   if (__ballot(fcadv != 0)) flags |= MRAFT_G_FOLLOWER_COMMIT;
 
   // ------------------------------------------------------------ phase D
-  const bool have = icls >= IC_STALE && icls <= IC_HB;
-  int term = T, role = kLeader, stepped = 0, any = 0, mstar = INT32_MIN;
-  int mm[P];
-  int gate[NI], rs[NI], rp[NI], rn[NI], rx[NI], ic[NI];
-  const unsigned long long have_m = __ballot(have);
-  const unsigned long long succ_m = __ballot(have && rsucc);
-  if (succ_m) {
-#pragma unroll
-    for (int j = 0; j < P; ++j) mm[j] = (j == lp) ? 0 : uni(s.match[ld * P + j]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < P; ++j) mm[j] = 0;
-  }
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {                                         // a2, peer order
-    const int pq = q < lp ? q : q + 1;
-    gate[q] = 0;
-    rs[q] = (int)((succ_m >> q) & 1);
-    rp[q] = uni(__shfl(prev, q, 64));
-    rn[q] = uni(__shfl(n, q, 64));
-    rx[q] = rp[q] + 1;                                                   // nextIndex[q] (gathered)
-    ic[q] = uni(__shfl(icls, q, 64));
-    if (!((have_m >> q) & 1)) continue;
-    const int rt = uni(__shfl(rterm, q, 64));
-    if (rt > term) {                                                     // :67-72
-      term = rt;
-      role = kFollower;
-      stepped = 1;
-    } else if (rt == term && role == kLeader && T == term) {             // :73-74 (prev gate holds)
-      gate[q] = 1;
-      if (rs[q]) {
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-          if (j == pq) mm[j] = rp[q] + rn[q];                            // :76
-        rx[q] = rp[q] + rn[q] + 1;                                       // :77
-        mstar = max(mstar, quorum_match<P>(mm, lp));                     // :78 -> a1
-        any = 1;
-      } else {
-        rx[q] = uni(__shfl(rci, q, 64));                                 // :82
-      }
-    }
-  }
-  int commit = c0, top = 0;
-  if (any) {
-    top = min(mstar, last);
-    if (top > c0) {
-      if (uni(s.log[lrow + (top - ldummy)]) == T) {                      // :98, one probe
-        commit = top;
-      } else {                                                           // Figure-8: exact scan
-        const int i = wave_scan_down_eq(s.log + lrow, ldummy, c0 + 1, top - 1, T);
-        if (i > c0) commit = i;
-      }
-    }
-  }
   if (commit != c0) flags |= MRAFT_G_COMMITTED;
-  if (stepped) flags |= MRAFT_G_STEPPED_DOWN;
-
+  if (fd.stepped) flags |= MRAFT_G_STEPPED_DOWN;
   if (!COUNT) {
     if (lane == 0) {
-      if (stepped) {
-        s.term[ld] = term;
+      if (fd.stepped) {
+        s.term[ld] = fd.term;
         s.voted[ld] = -1;
         s.role[ld] = kFollower;
       }
@@ -449,24 +526,24 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       const int pq = q < lp ? q : q + 1;
-      if (lane == q && gate[q]) {
-        s.next[ld * P + pq] = rx[q];
-        if (rs[q]) s.match[ld * P + pq] = rp[q] + rn[q];
+      if (lane == q && fd.gate[q]) {
+        s.next[ld * P + pq] = fd.rx[q];
+        if (fd.rs[q]) s.match[ld * P + pq] = fd.rp[q] + fd.rn[q];
       }
     }
   } else {
     // Leader-side words, wave-uniform.
-    long long gR = hR + (any ? NI : 0), gW = (stepped ? 3 : 0) + (commit != c0 ? 1 : 0);
+    long long gR = hR + (fd.any ? NI : 0), gW = (fd.stepped ? 3 : 0) + (commit != c0 ? 1 : 0);
 #pragma unroll
-    for (int q = 0; q < NI; ++q) gW += gate[q] ? (rs[q] ? 2 : 1) : 0;
+    for (int q = 0; q < NI; ++q) gW += fd.gate[q] ? (fd.rs[q] ? 2 : 1) : 0;
     // Leader log words: union of {prev_q} (PrevLogTerm), [prev_q+1, last]
     // (entries consumed by merges) and the commit scan [stop, top].
     long long A = (long long)last + 1;
 #pragma unroll
     for (int q = 0; q < NI; ++q)
-      if (ic[q] == IC_MERGE) A = min(A, (long long)rp[q] + 1);
+      if (fd.ic[q] == IC_MERGE) A = min(A, (long long)fd.rp[q] + 1);
     long long a1lo = 1, a1hi = 0;
-    if (any && top > c0) {
+    if (fd.any && top > c0) {
       a1hi = top;
       a1lo = (commit != c0) ? commit : c0 + 1;
     }
@@ -474,11 +551,11 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
     u -= interval_len(max(A, a1lo), min((long long)last, a1hi));
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
-      if (ic[q] < IC_STALE) continue;  // a3 read log[prev] for every gathered item
+      if (fd.ic[q] < IC_STALE) continue;  // a3 read log[prev] for every gathered item
       bool dup = false;
 #pragma unroll
-      for (int q2 = 0; q2 < q; ++q2) dup |= (ic[q2] >= IC_STALE && rp[q2] == rp[q]);
-      const long long x = rp[q];
+      for (int q2 = 0; q2 < q; ++q2) dup |= (fd.ic[q2] >= IC_STALE && fd.rp[q2] == fd.rp[q]);
+      const long long x = fd.rp[q];
       const bool inside = (x >= A && x <= last) || (x >= a1lo && x <= a1hi);
       if (!dup && !inside) u += 1;
     }
@@ -488,7 +565,7 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
     if (lane == 0) {
       atomicAdd(&counts[0], R);
       atomicAdd(&counts[1], W);
-      atomicAdd(&counts[2], (unsigned long long)active);
+      atomicAdd(&counts[2], 1ull);
     }
   }
 }
