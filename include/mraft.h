@@ -263,6 +263,24 @@ int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer,
 int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer,
                                int64_t out_words[3], int32_t where);
 
+/* Start (raft.go:90-104) for n items: if slots[i] is a leader, append
+ * counts[i] >= 1 entries {Index: last+1.., Term: currentTerm} (Go appends one
+ * per call; k consecutive calls give consecutive indices) and return the
+ * first appended index, the term and is_leader = 1; otherwise -1, -1, 0
+ * (:93-95). Capacity overflow: MRAFT_ITEM_LOG_FULL, nothing appended.
+ * Commands stay on the host, index-aligned with the returned indices. */
+int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts,
+                int64_t n, int32_t *out_index, int32_t *out_term,
+                int32_t *out_is_leader, int32_t *item_err, int32_t where);
+
+/* Applier (raft.go:153-203, without the snapshot message): for every slot,
+ * out_from/out_to [G*P] = the ApplyMsg index range (lastApplied,
+ * commitIndex] (out_from > out_to when empty), then lastApplied =
+ * max(lastApplied, commitIndex) (:200). The entries' terms are in log_term;
+ * the host maps indices to its commands. */
+int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to,
+                        int32_t where);
+
 /* ---- elections ------------------------------- */
 
 /* StartElection (raft_election.go:4-15): state=Candidate, term++,

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmraft_hip.so")
+LIB_PATH = os.environ.get("MRAFT_LIB") or os.path.join(_HERE, "libmraft_hip.so")
 SYNTH_PATH = os.path.join(_HERE, "libmraft_synth.so")
 
 # ---- constants (include/mraft.h) -------------------------------------------
@@ -68,6 +68,7 @@ ABI_SYMBOLS = (
     "mraft_load_state", "mraft_store_state", "mraft_state_view", "mraft_bind_state",
     "mraft_gather_append_args", "mraft_handle_append_entries",
     "mraft_process_append_replies", "mraft_replicate_tick", "mraft_replicate_tick_count",
+    "mraft_start", "mraft_collect_apply",
     "mraft_start_election", "mraft_handle_request_vote", "mraft_process_vote_replies",
     "mraft_export_group_status",
 )
@@ -92,6 +93,8 @@ _SIGS = {
     "mraft_process_append_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),
     "mraft_replicate_tick": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_replicate_tick_count": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
+    "mraft_start": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32]),
+    "mraft_collect_apply": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_start_election": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_handle_request_vote": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_process_vote_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),

@@ -406,6 +406,42 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
   return sg.finish();
 }
 
+int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts, int64_t n,
+                int32_t *out_index, int32_t *out_term, int32_t *out_is_leader, int32_t *item_err,
+                int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !out_index || !out_term || !out_is_leader || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *s, *c, *oi, *ot, *ol, *e;
+  TRY(sg.map(slots, sizeof(int32_t) * n, true, false, &s));
+  TRY(sg.map(counts, sizeof(int32_t) * n, true, false, &c));
+  TRY(sg.map(out_index, sizeof(int32_t) * n, false, true, &oi));
+  TRY(sg.map(out_term, sizeof(int32_t) * n, false, true, &ot));
+  TRY(sg.map(out_is_leader, sizeof(int32_t) * n, false, true, &ol));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_claim(s, n, sizeof(int32_t), 0, nullptr, gp_of(h), h->P, h->claim, h->epoch,
+                      (int32_t *)e, h->stream);
+  mraft::launch_start(dev_of(h), (const int32_t *)s, (const int32_t *)c, n, (int32_t *)oi,
+                      (int32_t *)ot, (int32_t *)ol, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int32_t where) {
+  TRY(check(h));
+  if (!out_from || !out_to) return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *f, *t;
+  TRY(sg.map(out_from, sizeof(int32_t) * gp_of(h), false, true, &f));
+  TRY(sg.map(out_to, sizeof(int32_t) * gp_of(h), false, true, &t));
+  mraft::launch_collect_apply(dev_of(h), (int32_t *)f, (int32_t *)t, h->stream);
+  return sg.finish();
+}
+
 int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n, mraft_rv_args *out_args,
                          int32_t *item_err, int32_t where) {
   TRY(check(h));

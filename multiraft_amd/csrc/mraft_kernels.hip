@@ -278,6 +278,43 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
   }
 }
 
+// ---------------------------------------------------------------- Start
+__global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t *__restrict__ counts,
+                        int64_t n, int32_t *__restrict__ oi, int32_t *__restrict__ ot,
+                        int32_t *__restrict__ ol, int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int idx = -1, term = -1, isl = 0;
+  if (!err[i]) {
+    const int sl = slots[i], k = counts ? counts[i] : 1;
+    if (k < 1) {
+      err[i] = MRAFT_ITEM_BAD_SLOT;
+    } else if (s.role[sl] == kLeader) {                                // raft.go:93-95
+      const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl];
+      if ((int64_t)last + k - dummy > (int64_t)s.L - 1) {
+        err[i] = MRAFT_ITEM_LOG_FULL;
+      } else {
+        for (int j = 1; j <= k; ++j) s.log[(int64_t)sl * s.L + (last + j - dummy)] = t;  // :96-100
+        s.last[sl] = last + k;
+        idx = last + 1; term = t; isl = 1;                             // :103
+      }
+    }
+  }
+  oi[i] = idx; ot[i] = term; ol[i] = isl;
+}
+
+// ---------------------------------------------------------------- applier
+__global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__restrict__ to) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < gp;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int la = s.applied[i], ci = s.commit[i];
+    from[i] = la + 1;                                                  // raft.go:179-190
+    to[i] = ci;
+    if (ci > la) s.applied[i] = ci;                                    // :200
+  }
+}
+
 // ---------------------------------------------------------------- a6 part 1
 __global__ void k_start_election(Dev s, const int32_t *__restrict__ slots, int64_t n,
                                  mraft_rv_args *__restrict__ out, int32_t *__restrict__ err) {
@@ -449,6 +486,19 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 #undef MRAFT_FOLD_CASE
     default: break;
   }
+}
+
+void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
+                  int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_start, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, counts, n, oi, ot,
+                     ol, err);
+}
+
+void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t st) {
+  int blocks = blocks_for((int64_t)s.G * s.P);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_collect_apply, dim3(blocks), dim3(kBlock), 0, st, s, from, to);
 }
 
 void launch_start_election(const Dev &s, const int32_t *slots, int64_t n, mraft_rv_args *out,

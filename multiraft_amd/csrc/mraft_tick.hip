@@ -225,6 +225,86 @@ __device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long 
   }
 }
 
+// Copy-only tail of the pass, once no follower is still comparing: every
+// follower in M_COPY receives the leader's entries [c, nend) (its copy start
+// is already behind c), VC dwordx4 loads per lane in flight per iteration,
+// and the commit scan [slo, shi] continues on the same loads.
+template <int NI, int VC, bool VEC, bool COUNT>
+__device__ __forceinline__ void copy_loop(int32_t *__restrict__ log, long long eo,
+                                          const long long (&fo)[NI], const int (&mode)[NI], int c,
+                                          int nend, int phi, int slo, int shi, int T, int &found) {
+  constexpr int CW = 256 * VC;
+  const int lane = lane_id();
+  int cmask = 0;
+#pragma unroll
+  for (int q = 0; q < NI; ++q) cmask |= (mode[q] == M_COPY) ? (1 << q) : 0;
+  for (; c <= phi; c += CW) {
+    const bool scan = slo <= shi && c <= shi && c + CW - 1 >= slo;
+    if (!cmask && !(slo <= shi && c <= shi)) break;
+    int idx[VC][4], e[VC][4];
+#pragma unroll
+    for (int v = 0; v < VC; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
+#pragma unroll
+    for (int v = 0; v < VC; ++v) {
+      if (VEC) {
+        int4 x = make_int4(0, 0, 0, 0);
+        if (idx[v][0] <= phi) x = *reinterpret_cast<const int4 *>(log + eo + idx[v][0]);
+        e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? log[eo + idx[v][u]] : 0;
+      }
+    }
+    if (scan) {
+      int hit = -1;
+#pragma unroll
+      for (int v = VC - 1; v >= 0; --v) {
+        if (hit >= 0) break;
+        if (VEC) {
+          int lu = -1;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
+          const unsigned long long m = __ballot(lu >= 0);
+          if (m) {
+            const int l = 63 - __clzll((long long)m);
+            hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
+          }
+        } else {
+#pragma unroll
+          for (int u = 3; u >= 0; --u) {
+            if (hit >= 0) break;
+            const unsigned long long m =
+                __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
+            if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
+          }
+        }
+      }
+      if (hit >= 0) found = hit;
+    }
+    if (!COUNT) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if (!((cmask >> q) & 1)) continue;
+#pragma unroll
+        for (int v = 0; v < VC; ++v) {
+          if (VEC && idx[v][3] < nend) {
+            *reinterpret_cast<int4 *>(log + fo[q] + idx[v][0]) =
+                make_int4(e[v][0], e[v][1], e[v][2], e[v][3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (idx[v][u] < nend) log[fo[q] + idx[v][u]] = e[v][u];
+          }
+        }
+      }
+    }
+    if (c + CW >= nend) cmask = 0;
+  }
+}
+
 // Reply fold of one group (processAppendEntriesReply, :66-88, in peer order),
 // wave-uniform. Inputs per follower slot q come from lane q.
 template <int P>
@@ -274,14 +354,36 @@ struct Fold {
   }
 };
 
+#ifndef MRAFT_TICK_V
+#define MRAFT_TICK_V 1     // dwordx4 vectors per lane per stream per compare chunk
+#endif
+#ifndef MRAFT_TICK_MINW
+#define MRAFT_TICK_MINW 8  // __launch_bounds__ minimum waves per SIMD
+#endif
+#ifndef MRAFT_TICK_VC
+#define MRAFT_TICK_VC 4    // dwordx4 vectors per lane in the copy-only loop
+#endif
+#ifndef MRAFT_TICK_XCD
+#define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
+#endif
+
 template <int P, bool COUNT>
-__global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
+__global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
                                                     int32_t *__restrict__ gflags,
                                                     unsigned long long *__restrict__ counts) {
   constexpr int NI = P - 1;
-  constexpr int V = 2;
+  constexpr int V = MRAFT_TICK_V;
   const int lane = lane_id();
-  const int g = uni((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+  // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+  // §Workgroup dispatch): give each XCD a contiguous range of groups so the
+  // scalar SoA lines neighbouring groups share stay in one XCD's L2. Speed
+  // only; any placement gives the same results.
+  int gb = (int)blockIdx.x;
+  if (MRAFT_TICK_XCD) {
+    const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
+    gb = x * per + min(x, rem) + (gb >> 3);
+  }
+  const int g = uni(gb * 4 + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
   const int L = s.L;
 
@@ -434,14 +536,29 @@ __global__ __launch_bounds__(256) void k_tick_group(Dev s, const int32_t *__rest
   if (merge_m || slo <= shi) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
+    constexpr int VC = MRAFT_TICK_VC;
     if (vec) {
-      for (int c = plo - (int)((eo + plo) & 3); c <= phi; c += 256 * V)
+      int c = plo - (int)((eo + plo) & 3);
+      for (; c <= phi; c += 256 * V) {
+        bool cmp = false;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
+        if (!cmp) break;
         pass_chunk<NI, V, true, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
                                        fullmask, slo, shi, T, found, c, plo, phi);
+      }
+      copy_loop<NI, VC, true, COUNT>(s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
     } else {
-      for (int c = plo; c <= phi; c += 256 * V)
+      int c = plo;
+      for (; c <= phi; c += 256 * V) {
+        bool cmp = false;
+#pragma unroll
+        for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
+        if (!cmp) break;
         pass_chunk<NI, V, false, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
                                         fullmask, slo, shi, T, found, c, plo, phi);
+      }
+      copy_loop<NI, VC, false, COUNT>(s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
     }
   }
   int mk = -1;  // this lane's follower: first mismatching entry of its merge

@@ -182,6 +182,27 @@ class Engine:
             "mraft_process_append_replies")
         return flags, err
 
+    def start(self, slots, counts=None):
+        """Start (raft.go:90-104): returns (index, term, is_leader, err)."""
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        c = None if counts is None else np.ascontiguousarray(counts, dtype=np.int32)
+        idx = np.zeros(n, np.int32)
+        term = np.zeros(n, np.int32)
+        isl = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        _ck(self._lib.mraft_start(self._h, ptr(slots), ptr(c), n, ptr(idx), ptr(term), ptr(isl),
+                                  ptr(err), HOST), "mraft_start")
+        return idx, term, isl, err
+
+    def collect_apply(self):
+        """Applier (raft.go:153-203): per-slot ApplyMsg index ranges (from, to]."""
+        gp = self.G * self.P
+        fr = np.zeros(gp, np.int32)
+        to = np.zeros(gp, np.int32)
+        _ck(self._lib.mraft_collect_apply(self._h, ptr(fr), ptr(to), HOST), "mraft_collect_apply")
+        return fr, to
+
     # ---- elections -------------------------------------------------------
     def start_election(self, slots):
         slots = np.ascontiguousarray(slots, dtype=np.int32)

@@ -522,6 +522,42 @@ int ora_replicate_tick_mt(ora_engine *e, const int32_t *leader_peer,
 }
 
 /* ------------------------------------------------------------------------ */
+/* Start, raft.go:90-104, and the applier, raft.go:153-203                   */
+/* ------------------------------------------------------------------------ */
+
+int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
+              int64_t n, int32_t *out_index, int32_t *out_term,
+              int32_t *out_is_leader, int32_t *item_err) {
+  int32_t *first = claim_slots(e, slots, n, sizeof(int32_t), item_err);
+  for (int64_t i = 0; i < n; ++i) {
+    out_index[i] = -1; out_term[i] = -1; out_is_leader[i] = 0;
+    if (item_err[i]) continue;
+    int32_t s = slots[i], k = counts ? counts[i] : 1;
+    if (k < 1) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
+    if (S.state[s] != MRAFT_LEADER) continue;                         /* :93-95 */
+    int32_t last = S.last_index[s], dummy = S.dummy_index[s];
+    if ((int64_t)last + k - dummy > (int64_t)e->L - 1) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
+    for (int32_t j = 1; j <= k; ++j)                                  /* :96-100 */
+      S.log_term[(int64_t)s * e->L + (last + j - dummy)] = S.current_term[s];
+    S.last_index[s] = last + k;
+    out_index[i] = last + 1; out_term[i] = S.current_term[s]; out_is_leader[i] = 1;  /* :103 */
+  }
+  free(first);
+  return MRAFT_OK;
+}
+
+int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to) {
+  int64_t gp = (int64_t)e->G * e->P;
+  for (int64_t s = 0; s < gp; ++s) {
+    int32_t la = S.last_applied[s], ci = S.commit_index[s];
+    out_from[s] = la + 1;                                             /* :179-190 */
+    out_to[s] = ci;
+    if (ci > la) S.last_applied[s] = ci;                              /* :200 Max */
+  }
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* a6 part 1: StartElection, raft_election.go:4-15                            */
 /* ------------------------------------------------------------------------ */
 

@@ -60,6 +60,11 @@ int ora_replicate_tick_range(ora_engine *e, const int32_t *leader_peer,
 int ora_replicate_tick_mt(ora_engine *e, const int32_t *leader_peer,
                           int32_t *group_flags, int32_t nthreads);
 
+int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
+              int64_t n, int32_t *out_index, int32_t *out_term,
+              int32_t *out_is_leader, int32_t *item_err);
+int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to);
+
 int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
                        mraft_rv_args *out_args, int32_t *item_err);
 int ora_handle_request_vote(ora_engine *e, const mraft_rv_args *args,

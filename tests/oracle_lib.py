@@ -36,6 +36,8 @@ def lib():
             "ora_process_append_replies": [E, vp, i64, vp, i64, vp, vp],
             "ora_replicate_tick": [E, vp, vp],
             "ora_replicate_tick_mt": [E, vp, vp, i32],
+            "ora_start": [E, vp, vp, i64, vp, vp, vp, vp],
+            "ora_collect_apply": [E, vp, vp],
             "ora_start_election": [E, vp, i64, vp, vp],
             "ora_handle_request_vote": [E, vp, i64, vp, vp],
             "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
@@ -112,6 +114,23 @@ class Oracle:
         lib().ora_process_append_replies(ctypes.byref(self._e), ptr(items), n, ptr(sb),
                                          0 if sb is None else len(sb) - 1, ptr(flags), ptr(err))
         return flags, err
+
+    def start(self, slots, counts=None):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        c = None if counts is None else np.ascontiguousarray(counts, dtype=np.int32)
+        idx, term, isl, err = (np.zeros(n, np.int32) for _ in range(4))
+        lib().ora_start(ctypes.byref(self._e), ptr(slots), ptr(c), n, ptr(idx), ptr(term), ptr(isl), ptr(err))
+        return idx, term, isl, err
+
+    def collect_apply(self):
+        gp = self.G * self.P
+        fr, to = np.zeros(gp, np.int32), np.zeros(gp, np.int32)
+        lib().ora_collect_apply(ctypes.byref(self._e), ptr(fr), ptr(to))
+        return fr, to
+
+    def store_state(self):
+        return copy_state(self.st)
 
     def start_election(self, slots):
         slots = np.ascontiguousarray(slots, dtype=np.int32)

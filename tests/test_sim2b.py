@@ -1,0 +1,34 @@
+"""Config #1: the reference's 2A/2B test scenarios (src/raft/test_test.go),
+replayed by the deterministic harness in tests/sim2b.py through the engine's
+C ABI. The CPU run (oracle backend) checks the harness + oracle; the GPU run
+checks libmraft_hip.so; both must satisfy the reference tests' assertions
+(indices 1,2,3; no commit without a majority; index2 in [2,3]; convergence
+after divergent partitions; at most one leader per term; agreement on every
+committed index)."""
+import pytest
+
+from oracle_lib import Oracle
+from sim2b import SCENARIOS
+
+
+def _oracle(G, P, L, st):
+    return Oracle(G, P, L, st)
+
+
+def _gpu(G, P, L, st):
+    from multiraft_amd import Engine
+    e = Engine(G, P, L)
+    e.load_state(st)
+    return e
+
+
+@pytest.mark.parametrize("name", list(SCENARIOS))
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_scenario_oracle(name, seed):
+    SCENARIOS[name](_oracle, seed=seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SCENARIOS))
+def test_scenario_gpu(name):
+    SCENARIOS[name](_gpu)

@@ -1,0 +1,75 @@
+// mb_segcopy.hip — what HBM bandwidth does the tick's access pattern allow?
+// Copies ~1500-word segments between random 16 KB rows of a 5 GiB log array
+// (one wave per group of 4 segments, like the tick's copy phase) and compares
+// with a plain sequential dwordx4 copy of the same byte count.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+constexpr int L = 4096;
+
+template <int VC>
+__global__ __launch_bounds__(256) void segcopy(int *__restrict__ log, const int4 *__restrict__ seg, int nseg_groups) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= nseg_groups) return;
+  const int4 d = seg[w];  // src row, first dst row, start, end
+  const long long src = (long long)d.x * L;
+  for (int c = d.z & ~3; c <= d.w; c += 256 * VC) {
+    int4 v[VC];
+#pragma unroll
+    for (int u = 0; u < VC; ++u) {
+      const int i = c + 256 * u + 4 * lane;
+      v[u] = i <= d.w ? *reinterpret_cast<const int4 *>(log + src + i) : make_int4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long dst = (long long)(d.y + q) * L;
+#pragma unroll
+      for (int u = 0; u < VC; ++u) {
+        const int i = c + 256 * u + 4 * lane;
+        if (i + 3 <= d.w) *reinterpret_cast<int4 *>(log + dst + i) = v[u];
+      }
+    }
+  }
+}
+
+__global__ void seqcopy(const int4 *__restrict__ a, int4 *__restrict__ b, long n4) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+int main() {
+  const long G = 65536, P = 5, rows = G * P;
+  int *log;
+  if (hipMalloc(&log, rows * L * 4)) return 1;
+  (void)hipMemset(log, 1, rows * L * 4);
+  std::vector<int4> h(G);
+  srand(7);
+  double bytes = 0;
+  for (long g = 0; g < G; ++g) {
+    int last = 2048 + rand() % 2048, start = rand() % last;
+    h[g] = make_int4((int)(g * P), (int)(g * P + 1), start, last);
+    bytes += (double)(last - (start & ~3) + 1) * 4 * 5;  // 1 read + 4 writes
+  }
+  int4 *seg;
+  (void)hipMalloc(&seg, G * sizeof(int4));
+  (void)hipMemcpy(seg, h.data(), G * sizeof(int4), hipMemcpyHostToDevice);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  auto run = [&](const char *name, auto fn, double nbytes) {
+    fn(); (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a);
+    for (int r = 0; r < 10; ++r) fn();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms; (void)hipEventElapsedTime(&ms, a, b);
+    printf("%-28s %8.1f us  %6.2f TB/s\n", name, ms * 100, nbytes / (ms / 10 * 1e-3) / 1e12);
+  };
+  const int blocks = (int)((G + 3) / 4);
+  run("segcopy VC=1 (1 KB/it)", [&] { hipLaunchKernelGGL(segcopy<1>, dim3(blocks), dim3(256), 0, 0, log, seg, (int)G); }, bytes);
+  run("segcopy VC=2", [&] { hipLaunchKernelGGL(segcopy<2>, dim3(blocks), dim3(256), 0, 0, log, seg, (int)G); }, bytes);
+  run("segcopy VC=4", [&] { hipLaunchKernelGGL(segcopy<4>, dim3(blocks), dim3(256), 0, 0, log, seg, (int)G); }, bytes);
+  const long n4 = (long)(bytes / 2 / 16);
+  run("sequential copy same bytes", [&] { hipLaunchKernelGGL(seqcopy, dim3(8192), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+  return 0;
+}
