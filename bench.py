@@ -33,6 +33,14 @@ METRIC = "quorum commit decisions/sec @64k groups×5 peers; % HBM roofline"
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
 
 
+def kernel_src_sha() -> str:
+    import hashlib
+    h = hashlib.sha1()
+    for f in ("mraft_tick.hip", "mraft_device.h"):
+        h.update(open(os.path.join(ROOT, "multiraft_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:12]
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -178,12 +186,16 @@ def main():
 
     ker_s = float(np.mean(ker_ms)) / 1e3
     achieved = algo_bytes / ker_s
-    traffic = None
+    traffic, traffic_src = None, None
     if os.path.exists(args.pmc_json):
+        # PMC traffic of this exact kernel source and config, from the
+        # committed rocprofv3 summary (tools/profile_round.sh + pmc_summary.py).
         try:
             pm = json.load(open(args.pmc_json))
-            if (pm.get("groups"), pm.get("peers"), pm.get("log")) == (G, P, L):
+            if ((pm.get("groups"), pm.get("peers"), pm.get("log")) == (G, P, L)
+                    and pm.get("kernel_src_sha") == kernel_src_sha()):
                 traffic = pm.get("hbm_bytes_per_launch")
+                traffic_src = f"profiles/pmc_traffic.json ({pm.get('tag')})"
         except Exception:
             traffic = None
     out = {
@@ -207,7 +219,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
-                     "kernel": "k_replicate_tick<5,false>",
+                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE+WRITE_SIZE, calibrated)",
+                     "traffic_source": traffic_src,
+                     "kernel": f"k_tick_group<{P},false>",
+                     "algorithmic_read_bytes": 4 * rd, "algorithmic_write_bytes": 4 * wr,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "algorithmic_bytes_per_decision": algo_bytes / max(active, 1),
                      "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms))},

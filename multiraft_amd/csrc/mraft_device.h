@@ -75,11 +75,18 @@ __device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row
 
 // ConflictIndex of raft_append_entry.go:136-142 for prev > dummy + 1, where
 // a = term(prev): the largest index in [dummy+2, prev-1] whose term differs
-// from a, else dummy + 1.
+// from a, else dummy + 1. The first probe reads one term per lane (64 terms:
+// most runs end there), then 256-term iterations.
 __device__ __forceinline__ int wave_conflict_scan(const int32_t *__restrict__ frow, int fdummy,
                                                   int prev, int a) {
-  int r = wave_scan_down_ne(frow, fdummy, fdummy + 2, prev - 1, a);
-  return r < fdummy + 2 ? fdummy + 1 : r;
+  const int lo = fdummy + 2, hi = prev - 1;
+  const int idx = hi - lane_id();
+  const int v = idx >= lo ? frow[idx - fdummy] : a;
+  const unsigned long long m = __ballot(v != a);
+  if (m) return hi - first_lane(m);
+  if (hi - 64 < lo) return fdummy + 1;
+  const int r = wave_scan_down_ne(frow, fdummy, lo, hi - 64, a);
+  return r < lo ? fdummy + 1 : r;
 }
 
 // First k in [0, kc) with E[k] != F[k]; -1 if none.

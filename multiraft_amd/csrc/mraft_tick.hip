@@ -361,7 +361,7 @@ struct Fold {
 #define MRAFT_TICK_MINW 8  // __launch_bounds__ minimum waves per SIMD
 #endif
 #ifndef MRAFT_TICK_VC
-#define MRAFT_TICK_VC 4    // dwordx4 vectors per lane in the copy-only loop
+#define MRAFT_TICK_VC 1    // dwordx4 vectors per lane in the copy-only loop
 #endif
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping

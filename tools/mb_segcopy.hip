@@ -37,6 +37,30 @@ __global__ __launch_bounds__(256) void segcopy(int *__restrict__ log, const int4
 __global__ void seqcopy(const int4 *__restrict__ a, int4 *__restrict__ b, long n4) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
 }
+// 4 dwordx4 per thread in flight, block-contiguous 16 KB tiles.
+__global__ void seqcopy4(const int4 *__restrict__ a, int4 *__restrict__ b, long n4) {
+  for (long t = (long)blockIdx.x * 1024; t < n4; t += (long)gridDim.x * 1024) {
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { long i = t + u * 256 + threadIdx.x; v[u] = i < n4 ? a[i] : make_int4(0, 0, 0, 0); }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { long i = t + u * 256 + threadIdx.x; if (i < n4) b[i] = v[u]; }
+  }
+}
+__global__ void seqread4(const int4 *__restrict__ a, int *__restrict__ out, long n4) {
+  int acc = 0;
+  for (long t = (long)blockIdx.x * 1024; t < n4; t += (long)gridDim.x * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { long i = t + u * 256 + threadIdx.x; if (i < n4) { int4 v = a[i]; acc ^= v.x ^ v.y ^ v.z ^ v.w; } }
+  }
+  if (acc == 0x12345678) out[0] = acc;
+}
+__global__ void seqwrite4(int4 *__restrict__ b, long n4) {
+  for (long t = (long)blockIdx.x * 1024; t < n4; t += (long)gridDim.x * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { long i = t + u * 256 + threadIdx.x; if (i < n4) b[i] = make_int4(u, 1, 2, 3); }
+  }
+}
 
 int main() {
   const long G = 65536, P = 5, rows = G * P;
@@ -71,5 +95,14 @@ int main() {
   run("segcopy VC=4", [&] { hipLaunchKernelGGL(segcopy<4>, dim3(blocks), dim3(256), 0, 0, log, seg, (int)G); }, bytes);
   const long n4 = (long)(bytes / 2 / 16);
   run("sequential copy same bytes", [&] { hipLaunchKernelGGL(seqcopy, dim3(8192), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+  for (int grid : {2048, 4096, 8192, 16384}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "copy x4 grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL(seqcopy4, dim3(grid), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+    snprintf(nm, sizeof nm, "read x4 grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL(seqread4, dim3(grid), dim3(256), 0, 0, (const int4 *)log, log + 16, 2 * n4); }, (double)n4 * 32);
+    snprintf(nm, sizeof nm, "write x4 grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL(seqwrite4, dim3(grid), dim3(256), 0, 0, (int4 *)log, 2 * n4); }, (double)n4 * 32);
+  }
   return 0;
 }
