@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (CPU rehearsal)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -99,13 +101,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(ndev, 1)  # gloo rehearsals may share one GPU
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
-    from multiraft_amd.engine import export_group_status_into, state_sizes
+    from multiraft_amd.engine import export_group_status_into
+    from multiraft_amd.router import allgather_status
 
     G, P, L, K, W = args.groups, args.peers, args.log, args.steps, args.warmup
     G_total = G * world
@@ -115,18 +123,23 @@ def main():
                                  nthreads=min(16, os.cpu_count() or 1))
     log(rank, f"generated {G}x{P}x{L} state in {time.perf_counter() - t:.1f}s")
 
-    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    # Ranks allocate in turn (a CPU rehearsal may put several ranks on one GPU).
+    for r in range(world):
+        if r == rank:
+            master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+            clone_bytes = sum(v.numel() * 4 for v in master.values())
+            free, _ = torch.cuda.mem_get_info(dev)
+            pool = max(1, min(K + 1, int(free * 0.9 // clone_bytes)))
+            clones = [{k: v.clone() for k, v in master.items()} for _ in range(pool)]
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
     del st
-    clone_bytes = sum(v.numel() * 4 for v in master.values())
-    free, _ = torch.cuda.mem_get_info(dev)
-    pool = max(1, min(K + 1, int(free * 0.9 // clone_bytes)))
     restore = pool < K + 1
-    clones = [{k: v.clone() for k, v in master.items()} for _ in range(pool)]
-    torch.cuda.synchronize()
     log(rank, f"{pool} state copies of {clone_bytes / 2**30:.2f} GiB each"
               f"{' (restore inside timed steps)' if restore else ''}")
 
-    eng = Engine(G, P, L, device=local, alloc=False)
+    eng = Engine(G, P, L, device=local_dev, alloc=False)
     # A dedicated (non-null) stream shared by torch and the engine, so the
     # events below bracket exactly the engine's kernels.
     stream = torch.cuda.Stream(dev)
@@ -136,9 +149,7 @@ def main():
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
     commit_d = torch.zeros(G, dtype=torch.int32, device=dev)
     tl_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    if world > 1:
-        all_c = torch.zeros(G_total, dtype=torch.int32, device=dev)
-        all_t = torch.zeros(G_total, dtype=torch.int32, device=dev)
+    on_host = world > 1 and args.dist_backend != "nccl"
 
     # Algorithmic words of one tick on the pristine state.
     eng.bind(master)
@@ -161,9 +172,11 @@ def main():
         if timed:
             ev[i][1].record(stream)
         export_group_status_into(eng, lp_d, commit_d, tl_d)
-        if world > 1:
-            dist.all_gather_into_tensor(all_c, commit_d)
-            dist.all_gather_into_tensor(all_t, tl_d)
+        if world > 1:  # the shard router's fan-in
+            if on_host:
+                allgather_status(commit_d.cpu(), tl_d.cpu())
+            else:
+                allgather_status(commit_d, tl_d)
 
     for i in range(W):
         step(i, False)
@@ -180,7 +193,7 @@ def main():
     ker_ms = [a.elapsed_time(b) for a, b in ev]
     flags = gf_d.cpu().numpy()
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if on_host else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
