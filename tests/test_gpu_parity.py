@@ -163,3 +163,21 @@ def test_elections_gpu():
         c, tl = e.export_group_status(cands % P)
         oc, otl = o.export_group_status(cands % P)
         assert np.array_equal(c, oc) and np.array_equal(tl, otl)
+
+
+@pytest.mark.parametrize("P,L,mono", [(2, 8, False), (3, 16, False), (5, 12, False), (5, 16, True),
+                                      (7, 10, False), (8, 9, False), (4, 64, False), (5, 256, False),
+                                      (5, 1024, True)])
+def test_tick_random_adversarial_gpu(P, L, mono):
+    """Arbitrary (not reachable-shaped) states: non-monotone terms, accidental
+    matches, snapshots, panics, near-capacity logs, bad states."""
+    from random_states import random_tick_state
+    rng = np.random.default_rng(2000 + P * 100 + L)
+    G = 700
+    st, lp = random_tick_state(rng, G, P, L, monotone=mono)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        assert e.replicate_tick_count(lp) == o.replicate_tick_count(lp)
+        gf = e.replicate_tick(lp)
+        assert np.array_equal(gf, o.replicate_tick(lp))
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "adversarial tick")

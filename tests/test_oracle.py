@@ -219,3 +219,20 @@ def test_dup_slots_rejected():
     a["term"] = 1
     rep, err = o.handle_append_entries(a, np.zeros(4, np.int32))
     assert err.tolist() == [0, 5, 6]
+
+
+@pytest.mark.parametrize("P,L,mono", [(2, 8, False), (3, 16, False), (5, 12, False), (5, 16, True),
+                                      (7, 10, False), (8, 9, False), (4, 64, False)])
+def test_tick_random_adversarial_c_vs_py(P, L, mono):
+    from random_states import random_tick_state
+    rng = np.random.default_rng(1000 + P * 100 + L)
+    G = 300
+    st, lp = random_tick_state(rng, G, P, L, monotone=mono)
+    o = Oracle(G, P, L, st)
+    gf = o.replicate_tick(lp)
+    pst, pgf = po.replicate_tick(st, G, P, L, lp)
+    assert np.array_equal(gf, pgf)
+    assert_states_equal(o.state(), pst, G, P, L, "random tick")
+    # every branch is exercised
+    for bit in (1, 2, 4, 8, 16, 64):
+        assert (gf & bit).any() or bit in (8, 64), bit
