@@ -1,0 +1,99 @@
+"""Secondary benchmark, SURVEY.md §8d config #5 (election storm): 65,536
+groups x 7 peers, R = 64 election rounds per launch (timeouts ->
+StartElection, every RequestVote, every tally; mraft_election_rounds).
+One step = one launch over a fresh HBM-resident copy of the seeded state.
+Prints one JSON line. The headline benchmark is bench.py (config #3)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--groups", type=int, default=65536)
+    ap.add_argument("--peers", type=int, default=7)
+    ap.add_argument("--rounds", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, synth_election_state, synth_seed
+    G, P, R, L, K, W = a.groups, a.peers, a.rounds, 8, a.steps, a.warmup
+    dev = torch.device("cuda", 0)
+    st, mask = synth_election_state(G, P, L, seed=synth_seed(5), rounds=R)
+    nc = np.unpackbits(mask[..., None], axis=-1).sum(axis=-1)  # timed-out peers per (round, group)
+    rv_upper = int(nc.sum()) * (P - 1)
+    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    mask_d = torch.from_numpy(mask).to(dev)
+    clones = [{k: v.clone() for k, v in master.items()} for _ in range(K + 1)]
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    eng = Engine(G, P, L, alloc=False)
+    eng.set_stream(stream.cuda_stream)
+    gf = torch.zeros(G, dtype=torch.int32, device=dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for i in range(W):
+        eng.bind(clones[K])
+        eng.election_rounds(mask_d, gf, where=DEVICE)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        eng.bind(clones[i])
+        ev[i][0].record(stream)
+        eng.election_rounds(mask_d, gf, where=DEVICE)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ker = float(np.mean([x.elapsed_time(y) for x, y in ev])) / 1e3
+    # words touched per launch: 6 scalars + last term per replica read, 4 written,
+    # the round masks, and matchIndex/nextIndex rows of elected replicas.
+    flags = gf.cpu().numpy()
+    bytes_launch = G * P * (7 + 4) * 4 + mask.size + int(((flags & 128) != 0).sum()) * P * 2 * 4
+    out = {"metric": "election-storm rounds/sec @64k groups×7 peers (R=64 per launch)",
+           "value": G * R * K / dt, "unit": "group-rounds/s", "n_gpus": 1, "steps": K, "warmup": W,
+           "ms_per_step": dt / K * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "int32",
+           "data": "synthetic: seeded config-#5 generator (mraft_synth_election_state)",
+           "config": {"workload": "config #5 election storm", "groups": G, "peers": P, "rounds": R,
+                      "requestvotes_per_launch_upper_bound": rv_upper,
+                      "groups_with_new_leader": int(((flags & 128) != 0).sum())},
+           "roofline": {"bound": "hbm", "achieved": bytes_launch / ker / 1e9, "peak": 8000.0,
+                        "unit": "GB/s", "frac": bytes_launch / ker / 8e12, "traffic": None,
+                        "kernel": f"k_election_rounds<{P}>", "kernel_ms_mean": ker * 1e3,
+                        "note": "latency-bound: state stays in registers for all R rounds"},
+           "requestvotes_per_sec": rv_upper * K / dt,
+           "cpu_baseline": None}
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_lib import Oracle  # checker / CPU baseline only
+        Gs = 4096
+        sst, smask = synth_election_state(G, P, L, seed=synth_seed(5), rounds=R, g_begin=0, g_end=Gs)
+        done, spent = 0, 0.0
+        while spent < a.cpu_seconds:
+            o = Oracle(Gs, P, L, sst)
+            t = time.perf_counter()
+            o.election_rounds(smask)
+            spent += time.perf_counter() - t
+            done += Gs * R
+        out["cpu_baseline"] = {"value": done / spent, "unit": "group-rounds/s", "cores": 1,
+                               "kind": "port",
+                               "sample": f"oracle ora_election_rounds on groups 0..{Gs - 1}, {R} rounds, "
+                                         f"fresh state per pass, {spent:.1f} s, 1 thread"}
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

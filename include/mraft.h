@@ -101,7 +101,8 @@ enum {
   MRAFT_G_NEED_SNAPSHOT = 8, /* some peer needs InstallSnapshot (prev < dummy)         */
   MRAFT_G_ERROR = 16,        /* a3 would panic / bad state / log full: group skipped   */
   MRAFT_G_FOLLOWER_COMMIT = 32, /* some follower advanced its commitIndex              */
-  MRAFT_G_LOG_FULL = 64      /* a follower rejected its AE with MRAFT_ITEM_LOG_FULL    */
+  MRAFT_G_LOG_FULL = 64,     /* a follower rejected its AE with MRAFT_ITEM_LOG_FULL    */
+  MRAFT_G_ELECTED = 128      /* mraft_election_rounds: some replica became leader     */
 };
 
 /* Per-slot state, struct-of-arrays (raft.go:16-40). Arrays of G*P int32 unless
@@ -302,6 +303,18 @@ int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items,
                                int64_t n, const int64_t *seg_begin,
                                int64_t n_seg, int32_t *out_flags,
                                int32_t *item_err, int32_t where);
+
+/* Election storm: R rounds in one launch. In round
+ * r, every replica p of group g with bit p of cand_mask[r*G + g] set that is
+ * not a leader times out (raft.go:109-114) and runs StartElection
+ * (raft_election.go:4-15), in ascending peer order; then every RequestVote is
+ * delivered (HandleRequestVote, :54-77), voter by voter in candidate order;
+ * then every candidate tallies its replies in voter order (:22-47; on a
+ * majority: Leader, matchIndex[*]=0, nextIndex[*]=lastIndex+1). No message
+ * is lost. group_flags (optional, [G]) gets MRAFT_G_ELECTED /
+ * MRAFT_G_STEPPED_DOWN. P <= 8 (one mask byte per group and round). */
+int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask,
+                          int32_t rounds, int32_t *group_flags, int32_t where);
 
 /* ---- read-out (GetState, raft.go:237-246) -------------------------------- */
 

@@ -52,6 +52,14 @@ int64_t mraft_synth_fold_batch(uint64_t seed, int32_t G, int32_t P, int32_t L,
                                const mraft_soa *st, const int32_t *leader_peer,
                                mraft_ae_result *out_items, int64_t *seg_begin);
 
+/* Election storm (config #5): state for groups [g_begin, g_end) plus
+ * cand_mask[r*(g_end-g_begin) + g-g_begin] (r < rounds): 1-3 distinct peers
+ * per group and round whose election timer fires. L >= 4. */
+int mraft_synth_election_state(uint64_t seed, int32_t G, int32_t P, int32_t L,
+                               int32_t g_begin, int32_t g_end, const mraft_soa *st,
+                               uint8_t *cand_mask, int32_t rounds,
+                               int32_t nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ ABI in include/mraft.h); this package is its host-side mirror:
 """
 from ._abi import (CANDIDATE, DEVICE, FOLLOWER, HOST, LEADER, synth_seed)  # noqa: F401
 from .engine import (Engine, MraftError, copy_state, new_state, state_sizes,  # noqa: F401
-                     synth_fold_batch, synth_tick_state)
+                     synth_election_state, synth_fold_batch, synth_tick_state)
 
 __all__ = ["Engine", "MraftError", "new_state", "copy_state", "state_sizes", "synth_tick_state",
-           "synth_fold_batch", "synth_seed", "LEADER", "CANDIDATE", "FOLLOWER", "HOST", "DEVICE"]
+           "synth_fold_batch", "synth_election_state", "synth_seed", "LEADER", "CANDIDATE", "FOLLOWER", "HOST", "DEVICE"]

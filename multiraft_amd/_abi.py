@@ -24,7 +24,7 @@ OK, E_INVAL, E_NOMEM, E_HIP, E_NOSTATE = 0, -1, -2, -3, -4
  ITEM_DUP_SLOT, ITEM_BAD_SLOT, ITEM_BAD_STATE) = range(8)
 F_NEED_MORE, F_COMMITTED, F_STEPPED_DOWN, F_BECAME_LEADER, F_APPLIED = 1, 2, 4, 8, 16
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
- G_LOG_FULL) = 1, 2, 4, 8, 16, 32, 64
+ G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
 SYN_MATCH, SYN_MISMATCH, SYN_BEYOND, SYN_STALE, SYN_BELOW_DUMMY, SYN_HEARTBEAT = range(6)
 
 
@@ -68,11 +68,11 @@ ABI_SYMBOLS = (
     "mraft_load_state", "mraft_store_state", "mraft_state_view", "mraft_bind_state",
     "mraft_gather_append_args", "mraft_handle_append_entries",
     "mraft_process_append_replies", "mraft_replicate_tick", "mraft_replicate_tick_count",
-    "mraft_start", "mraft_collect_apply",
+    "mraft_start", "mraft_collect_apply", "mraft_election_rounds",
     "mraft_start_election", "mraft_handle_request_vote", "mraft_process_vote_replies",
     "mraft_export_group_status",
 )
-SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch")
+SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
 _vp, _i32, _i64, _u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
 _SIGS = {
@@ -95,6 +95,7 @@ _SIGS = {
     "mraft_replicate_tick_count": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_start": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32]),
     "mraft_collect_apply": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
+    "mraft_election_rounds": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32]),
     "mraft_start_election": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_handle_request_vote": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_process_vote_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),
@@ -105,6 +106,8 @@ _SYNTH_SIGS = {
                                               ctypes.POINTER(MraftSoa), _vp, _vp, _i32]),
     "mraft_synth_fold_batch": (ctypes.c_int64, [ctypes.c_uint64, _i32, _i32, _i32,
                                                 ctypes.POINTER(MraftSoa), _vp, _vp, _vp]),
+    "mraft_synth_election_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,
+                                                  ctypes.POINTER(MraftSoa), _vp, _i32, _i32]),
 }
 
 _lib = None

@@ -510,6 +510,19 @@ int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items, in
   return sg.finish();
 }
 
+int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask, int32_t rounds,
+                          int32_t *group_flags, int32_t where) {
+  TRY(check(h));
+  if (!cand_mask || rounds < 0) return fail(MRAFT_E_INVAL, "null mask or negative rounds");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *m, *gf;
+  TRY(sg.map(cand_mask, (size_t)rounds * h->G, true, false, &m));
+  TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
+  mraft::launch_election_rounds(dev_of(h), (const uint8_t *)m, rounds, (int32_t *)gf, h->stream);
+  return sg.finish();
+}
+
 int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer, int32_t *commit,
                               int32_t *term_leader, int32_t where) {
   TRY(check(h));

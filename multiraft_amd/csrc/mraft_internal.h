@@ -38,6 +38,8 @@ void launch_handle_rv(const Dev &s, const mraft_rv_args *args, int64_t n, mraft_
 void launch_tally(const Dev &s, const mraft_rv_result *items, int64_t n, const int64_t *seg_begin,
                   int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
                   hipStream_t st);
+void launch_election_rounds(const Dev &s, const uint8_t *cand, int R, int32_t *gflags,
+                            hipStream_t st);
 void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t *term_leader,
                    hipStream_t st);
 

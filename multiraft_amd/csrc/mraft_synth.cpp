@@ -231,3 +231,60 @@ extern "C" int64_t mraft_synth_fold_batch(uint64_t seed, int32_t G, int32_t P, i
   seg_begin[G] = n;
   return n;
 }
+
+// Election storm (config #5): replicas with terms around a per-group base,
+// votedFor in {-1, random} 50/50, short logs whose last entries differ by a
+// few indices / terms (so isLogUpToDate goes both ways), and per round 1-3
+// distinct timed-out peers per group.
+extern "C" int mraft_synth_election_state(uint64_t seed, int32_t G, int32_t P, int32_t L,
+                                          int32_t g_begin, int32_t g_end, const mraft_soa *st,
+                                          uint8_t *cand_mask, int32_t rounds, int32_t nthreads) {
+  if (!st || P < 1 || P > 8 || L < 4 || g_begin < 0 || g_end > G || g_begin > g_end || rounds < 0)
+    return MRAFT_E_INVAL;
+  const int32_t n = g_end - g_begin;
+  auto work = [=](int32_t b, int32_t e) {
+    for (int32_t g = b; g < e; ++g) {
+      Rng rng(seed ^ 0xE1EC7ull, (uint64_t)g);
+      const int64_t sb = (int64_t)(g - g_begin) * P;
+      const int32_t T0 = 8 + (int32_t)rng.below(60000);
+      const int32_t B = L / 2 + (int32_t)rng.below((uint32_t)(L / 2 - 2));
+      for (int32_t p = 0; p < P; ++p) {
+        const int64_t s = sb + p;
+        st->current_term[s] = T0 + (int32_t)rng.below(3) - 1;
+        st->voted_for[s] = rng.below(2) ? -1 : (int32_t)rng.below((uint32_t)P);
+        st->state[s] = rng.below(8) == 0 ? MRAFT_CANDIDATE : MRAFT_FOLLOWER;
+        st->granted_votes[s] = 0;
+        st->dummy_index[s] = 0;
+        int32_t last = B + (int32_t)rng.below(5) - 2;
+        last = std::max(1, std::min(L - 1, last));
+        st->last_index[s] = last;
+        st->commit_index[s] = 0;
+        st->last_applied[s] = 0;
+        const int32_t lt = std::max(1, T0 - (int32_t)rng.below(3) - 1);
+        int32_t *row = st->log_term + s * L;
+        row[0] = 0;
+        for (int32_t k = 1; k <= last; ++k) row[k] = std::max(1, lt - (last - k) / 2);
+        for (int32_t k = last + 1; k < L; ++k) row[k] = 0;
+        std::memset(st->match_index + s * P, 0, sizeof(int32_t) * (size_t)P);
+        std::memset(st->next_index + s * P, 0, sizeof(int32_t) * (size_t)P);
+      }
+      for (int32_t r = 0; r < rounds; ++r) {
+        uint32_t m = 0;
+        const int32_t c = 1 + (int32_t)rng.below(3);
+        for (int32_t k = 0; k < c; ++k) m |= 1u << rng.below((uint32_t)P);
+        cand_mask[(int64_t)r * n + (g - g_begin)] = (uint8_t)m;
+      }
+    }
+  };
+  if (nthreads <= 1 || n < 64) {
+    work(g_begin, g_end);
+    return MRAFT_OK;
+  }
+  nthreads = std::min(nthreads, 64);
+  std::vector<std::thread> th;
+  for (int32_t t = 0; t < nthreads; ++t)
+    th.emplace_back(work, g_begin + (int32_t)((int64_t)n * t / nthreads),
+                    g_begin + (int32_t)((int64_t)n * (t + 1) / nthreads));
+  for (auto &x : th) x.join();
+  return MRAFT_OK;
+}

@@ -64,6 +64,22 @@ def synth_tick_state(G: int, P: int, L: int, seed: int, g_begin: int = 0, g_end:
     return st, lp, ic
 
 
+def synth_election_state(G: int, P: int, L: int, seed: int, rounds: int, g_begin: int = 0,
+                         g_end: int | None = None, nthreads: int | None = None):
+    """Seeded election-storm workload (config #5): (state, cand_mask[rounds, n])."""
+    g_end = G if g_end is None else g_end
+    n = g_end - g_begin
+    st = {f: np.empty(sz, dtype=np.int32) for f, sz in state_sizes(n, P, L).items()}
+    mask = np.zeros((rounds, n), dtype=np.uint8)
+    soa = soa_of(st)
+    nt = nthreads if nthreads is not None else min(16, os.cpu_count() or 1)
+    rc = _abi.synth().mraft_synth_election_state(seed, G, P, L, g_begin, g_end, ctypes.byref(soa),
+                                                 ptr(mask), rounds, nt)
+    if rc != 0:
+        raise MraftError(f"mraft_synth_election_state failed ({rc})")
+    return st, mask
+
+
 def synth_fold_batch(st: dict, G: int, P: int, L: int, leader_peer: np.ndarray, seed: int):
     items = np.zeros(G * max(P - 1, 0), dtype=AE_RESULT)
     seg = np.zeros(G + 1, dtype=np.int64)
@@ -232,6 +248,19 @@ class Engine:
                                                  0 if sb is None else len(sb) - 1, ptr(flags),
                                                  ptr(err), HOST), "mraft_process_vote_replies")
         return flags, err
+
+    def election_rounds(self, cand_mask, group_flags=None, where: int = HOST):
+        """Election storm (config #5): len(cand_mask) rounds in one launch."""
+        if where == HOST:
+            cand_mask = np.ascontiguousarray(cand_mask, dtype=np.uint8)
+            if group_flags is None:
+                group_flags = np.zeros(self.G, dtype=np.int32)
+            rounds = cand_mask.shape[0]
+        else:
+            rounds = cand_mask.shape[0]
+        _ck(self._lib.mraft_election_rounds(self._h, ptr(cand_mask), rounds, ptr(group_flags), where),
+            "mraft_election_rounds")
+        return group_flags
 
     def export_group_status(self, leader_peer=None):
         commit = np.zeros(self.G, dtype=np.int32)

@@ -561,23 +561,26 @@ int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to) {
 /* a6 part 1: StartElection, raft_election.go:4-15                            */
 /* ------------------------------------------------------------------------ */
 
+static void start_election_one(ora_engine *e, int32_t s, mraft_rv_args *a) {
+  S.state[s] = MRAFT_CANDIDATE;                                       /* :6 */
+  S.current_term[s] += 1;                                             /* :7 */
+  int32_t last = S.last_index[s];                                     /* lastEntry, raft_log.go:50-53 */
+  a->slot = s;
+  a->term = S.current_term[s];                                        /* :10 */
+  a->candidate_id = s % e->P;                                         /* :11 */
+  a->last_log_index = last;                                           /* :12 */
+  a->last_log_term = term_at(e, s, last);                             /* :13 */
+  S.voted_for[s] = s % e->P;                                          /* :14 */
+  S.granted_votes[s] = 1;                                             /* :17 */
+}
+
 int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
                        mraft_rv_args *out, int32_t *item_err) {
   int32_t *first = claim_slots(e, slots, n, sizeof(int32_t), item_err);
   for (int64_t i = 0; i < n; ++i) {
     memset(&out[i], 0, sizeof(out[i]));
     if (item_err[i]) continue;
-    int32_t s = slots[i];
-    S.state[s] = MRAFT_CANDIDATE;                                     /* :6 */
-    S.current_term[s] += 1;                                           /* :7 */
-    int32_t last = S.last_index[s];                                   /* lastEntry, raft_log.go:50-53 */
-    out[i].slot = s;
-    out[i].term = S.current_term[s];                                  /* :10 */
-    out[i].candidate_id = s % e->P;                                   /* :11 */
-    out[i].last_log_index = last;                                     /* :12 */
-    out[i].last_log_term = term_at(e, s, last);                       /* :13 */
-    S.voted_for[s] = s % e->P;                                        /* :14 */
-    S.granted_votes[s] = 1;                                           /* :17 */
+    start_election_one(e, slots[i], &out[i]);
   }
   free(first);
   return MRAFT_OK;
@@ -587,6 +590,27 @@ int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
 /* a5: HandleRequestVote, raft_election.go:54-77 + isLogUpToDate              */
 /* ------------------------------------------------------------------------ */
 
+static void handle_rv_one(ora_engine *e, int32_t v, const mraft_rv_args *a, mraft_rv_reply *r) {
+  r->term = 0; r->vote_granted = 0;
+  if (a->term < S.current_term[v]) {                                  /* :59-62 */
+    r->term = S.current_term[v];
+    return;
+  }
+  if (a->term > S.current_term[v]) {                                  /* :63-66 */
+    S.state[v] = MRAFT_FOLLOWER;
+    S.current_term[v] = a->term; S.voted_for[v] = -1;
+  }
+  r->term = S.current_term[v];                                        /* :67 */
+  int32_t my_last = S.last_index[v];
+  int32_t my_last_term = term_at(e, v, my_last);
+  int up_to_date = a->last_log_term > my_last_term ||                 /* raft_log.go:99-104 */
+                   (my_last_term == a->last_log_term && a->last_log_index >= my_last);
+  if ((S.voted_for[v] == -1 || S.voted_for[v] == a->candidate_id) && up_to_date) {
+    S.voted_for[v] = a->candidate_id;                                 /* :71 */
+    r->vote_granted = 1;
+  }                                                                   /* else :76 */
+}
+
 int ora_handle_request_vote(ora_engine *e, const mraft_rv_args *args,
                             int64_t n, mraft_rv_reply *replies,
                             int32_t *item_err) {
@@ -594,35 +618,39 @@ int ora_handle_request_vote(ora_engine *e, const mraft_rv_args *args,
   for (int64_t i = 0; i < n; ++i) {
     memset(&replies[i], 0, sizeof(replies[i]));
     if (item_err[i]) continue;
-    const mraft_rv_args *a = &args[i];
-    int32_t v = a->slot;
-    if (a->term < S.current_term[v]) {                                /* :59-62 */
-      replies[i].term = S.current_term[v]; replies[i].vote_granted = 0;
-      continue;
-    }
-    if (a->term > S.current_term[v]) {                                /* :63-66 */
-      S.state[v] = MRAFT_FOLLOWER;
-      S.current_term[v] = a->term; S.voted_for[v] = -1;
-    }
-    replies[i].term = S.current_term[v];                              /* :67 */
-    int32_t my_last = S.last_index[v];
-    int32_t my_last_term = term_at(e, v, my_last);
-    int up_to_date = a->last_log_term > my_last_term ||               /* raft_log.go:99-104 */
-                     (my_last_term == a->last_log_term && a->last_log_index >= my_last);
-    if ((S.voted_for[v] == -1 || S.voted_for[v] == a->candidate_id) && up_to_date) {
-      S.voted_for[v] = a->candidate_id;                               /* :71 */
-      replies[i].vote_granted = 1;
-      continue;
-    }
-    replies[i].vote_granted = 0;                                      /* :76 */
+    handle_rv_one(e, args[i].slot, &args[i], &replies[i]);
   }
   free(first);
   return MRAFT_OK;
 }
 
 /* ------------------------------------------------------------------------ */
-/* a6 part 2: vote tally closure, raft_election.go:22-47 (guard :29)                      */
+/* a6 part 2: vote tally closure, raft_election.go:22-47 (guard :29)          */
 /* ------------------------------------------------------------------------ */
+
+static int32_t tally_one(ora_engine *e, int32_t c, int32_t args_term, int32_t reply_term,
+                         int32_t granted) {
+  const int32_t P = e->P;
+  int32_t fl = 0;
+  if (S.current_term[c] == args_term && S.state[c] == MRAFT_CANDIDATE) { /* :29 */
+    if (granted) {                                                    /* :30 */
+      S.granted_votes[c] += 1;                                        /* :31 */
+      if (S.granted_votes[c] > P / 2) {                               /* :32 */
+        S.state[c] = MRAFT_LEADER;                                    /* :33 */
+        for (int32_t j = 0; j < P; ++j) {                             /* :34-38 */
+          S.match_index[(int64_t)c * P + j] = 0;
+          S.next_index[(int64_t)c * P + j] = S.last_index[c] + 1;
+        }
+        fl |= MRAFT_F_BECAME_LEADER;
+      }
+    } else if (reply_term > S.current_term[c]) {                      /* :42-45 */
+      S.state[c] = MRAFT_FOLLOWER;
+      S.current_term[c] = reply_term; S.voted_for[c] = -1;
+      fl |= MRAFT_F_STEPPED_DOWN;
+    }
+  }
+  return fl;
+}
 
 int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
                              int64_t n, const int64_t *seg_begin,
@@ -647,30 +675,53 @@ int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
     }
     if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
     seen[c] = 1;
-    for (int64_t i = b; i < en; ++i) {
-      const mraft_rv_result *it = &items[i];
-      int32_t fl = 0;
-      if (S.current_term[c] == it->args_term && S.state[c] == MRAFT_CANDIDATE) { /* :29 */
-        if (it->vote_granted) {                                       /* :30 */
-          S.granted_votes[c] += 1;                                    /* :31 */
-          if (S.granted_votes[c] > P / 2) {                           /* :32 */
-            S.state[c] = MRAFT_LEADER;                                /* :33 */
-            for (int32_t j = 0; j < P; ++j) {                         /* :34-38 */
-              S.match_index[(int64_t)c * P + j] = 0;
-              S.next_index[(int64_t)c * P + j] = S.last_index[c] + 1;
-            }
-            fl |= MRAFT_F_BECAME_LEADER;
-          }
-        } else if (it->reply_term > S.current_term[c]) {              /* :42-45 */
-          S.state[c] = MRAFT_FOLLOWER;
-          S.current_term[c] = it->reply_term; S.voted_for[c] = -1;
-          fl |= MRAFT_F_STEPPED_DOWN;
-        }
-      }
-      out_flags[i] = fl;
-    }
+    for (int64_t i = b; i < en; ++i)
+      out_flags[i] = tally_one(e, c, items[i].args_term, items[i].reply_term, items[i].vote_granted);
   }
   free(seen);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Fused election storm (config #5): R rounds; in round r the peers set in   */
+/* cand_mask[r*G + g] that are not leaders time out (raft.go:109-114) and    */
+/* StartElection in ascending peer order; every RequestVote is delivered,    */
+/* voter by voter in candidate order; every candidate tallies its replies in */
+/* voter order.                                                              */
+/* ------------------------------------------------------------------------ */
+
+int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
+                        int32_t *group_flags) {
+  const int32_t P = e->P, G = e->G;
+  if (P > 8) return MRAFT_E_INVAL;
+  for (int32_t g = 0; g < G; ++g) {
+    int32_t fl = 0;
+    for (int32_t r = 0; r < R; ++r) {
+      const uint8_t m = cand_mask[(int64_t)r * G + g];
+      mraft_rv_args args[8];
+      mraft_rv_reply rep[8][8];
+      int32_t cand[8], nc = 0;
+      for (int32_t p = 0; p < P; ++p) {
+        int32_t s = g * P + p;
+        if (((m >> p) & 1) && S.state[s] != MRAFT_LEADER) {
+          start_election_one(e, s, &args[nc]);
+          cand[nc++] = p;
+        }
+      }
+      for (int32_t v = 0; v < P; ++v)                                 /* RequestVote deliveries */
+        for (int32_t k = 0; k < nc; ++k)
+          if (cand[k] != v) handle_rv_one(e, g * P + v, &args[k], &rep[k][v]);
+      for (int32_t k = 0; k < nc; ++k)                                /* tallies */
+        for (int32_t v = 0; v < P; ++v)
+          if (cand[k] != v) {
+            int32_t f2 = tally_one(e, g * P + cand[k], args[k].term, rep[k][v].term,
+                                   rep[k][v].vote_granted);
+            if (f2 & MRAFT_F_BECAME_LEADER) fl |= MRAFT_G_ELECTED;
+            if (f2 & MRAFT_F_STEPPED_DOWN) fl |= MRAFT_G_STEPPED_DOWN;
+          }
+    }
+    if (group_flags) group_flags[g] = fl;
+  }
   return MRAFT_OK;
 }
 

@@ -42,6 +42,7 @@ def lib():
             "ora_handle_request_vote": [E, vp, i64, vp, vp],
             "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
             "ora_export_group_status": [E, vp, vp, vp],
+            "ora_election_rounds": [E, vp, i32, vp],
         }
         for n, a in sigs.items():
             f = getattr(l, n)
@@ -157,6 +158,12 @@ class Oracle:
         lib().ora_process_vote_replies(ctypes.byref(self._e), ptr(items), n, ptr(sb),
                                        0 if sb is None else len(sb) - 1, ptr(flags), ptr(err))
         return flags, err
+
+    def election_rounds(self, cand_mask):
+        m = np.ascontiguousarray(cand_mask, dtype=np.uint8)
+        gf = np.zeros(self.G, np.int32)
+        lib().ora_election_rounds(ctypes.byref(self._e), ptr(m), m.shape[0], ptr(gf))
+        return gf
 
     def export_group_status(self, leader_peer=None):
         commit = np.zeros(self.G, dtype=np.int32)

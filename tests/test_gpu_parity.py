@@ -181,3 +181,15 @@ def test_tick_random_adversarial_gpu(P, L, mono):
         gf = e.replicate_tick(lp)
         assert np.array_equal(gf, o.replicate_tick(lp))
         assert_states_equal(e.store_state(), o.state(), G, P, L, "adversarial tick")
+
+
+@pytest.mark.parametrize("P,R", [(3, 16), (5, 8), (7, 64), (8, 5), (2, 7), (1, 3)])
+def test_election_rounds_gpu(P, R):
+    from multiraft_amd import synth_election_state
+    G, L = 2048, 8
+    st, mask = synth_election_state(G, P, L, seed=300 + P, rounds=R)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        gf = e.election_rounds(mask)
+        assert np.array_equal(gf, o.election_rounds(mask))
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "election rounds")

@@ -236,3 +236,42 @@ def test_tick_random_adversarial_c_vs_py(P, L, mono):
     # every branch is exercised
     for bit in (1, 2, 4, 8, 16, 64):
         assert (gf & bit).any() or bit in (8, 64), bit
+
+
+def _py_election_rounds(st, G, P, L, mask):
+    rafts = po.from_soa(st, G, P, L)
+    gf = np.zeros(G, np.int32)
+    for g in range(G):
+        for r in range(mask.shape[0]):
+            m = int(mask[r, g])
+            cands = [p for p in range(P) if (m >> p) & 1 and rafts[g * P + p].state != po.LEADER]
+            args = {c: rafts[g * P + c].StartElection() for c in cands}
+            reps = {}
+            for v in range(P):
+                for c in cands:
+                    if c != v:
+                        rep = po.RequestVoteReply()
+                        rafts[g * P + v].HandleRequestVote(args[c], rep)
+                        reps[(c, v)] = rep
+            for c in cands:
+                for v in range(P):
+                    if c != v:
+                        fl = rafts[g * P + c].tally(args[c], reps[(c, v)])
+                        if fl & po.F_BECAME_LEADER:
+                            gf[g] |= 128
+                        if fl & po.F_STEPPED_DOWN:
+                            gf[g] |= po.G_STEPPED_DOWN
+    return po.to_soa(rafts, st, G, P, L), gf
+
+
+@pytest.mark.parametrize("P", [3, 5, 7, 8])
+def test_election_rounds_c_vs_py(P):
+    from multiraft_amd import synth_election_state
+    G, L, R = 96, 8, 12
+    st, mask = synth_election_state(G, P, L, seed=90 + P, rounds=R, nthreads=1)
+    o = Oracle(G, P, L, st)
+    gf = o.election_rounds(mask)
+    pst, pgf = _py_election_rounds(st, G, P, L, mask)
+    assert np.array_equal(gf, pgf)
+    assert_states_equal(o.state(), pst, G, P, L, "election rounds")
+    assert (gf & 128).any() and (gf & 4).any()

@@ -10,7 +10,7 @@ for spec in "$@"; do
   IFS=: read V W VC X <<< "$spec"
   tag="v${V}w${W}c${VC}x${X}"
   mkdir -p build_$tag
-  for f in mraft_abi mraft_kernels mraft_tick; do
+  for f in mraft_abi mraft_kernels mraft_tick mraft_elect; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
       -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X \
       -c $f.hip -o build_$tag/$f.o 2>/dev/null &
