@@ -90,7 +90,9 @@ enum {
   MRAFT_F_COMMITTED = 2,     /* applyCond.Signal(): commitIndex advanced, :99-100        */
   MRAFT_F_STEPPED_DOWN = 4,  /* adopted a higher term and became follower, :67-72        */
   MRAFT_F_BECAME_LEADER = 8, /* vote tally reached a majority, raft_election.go:32-38   */
-  MRAFT_F_APPLIED = 16       /* the reply passed the term/state/prev gate, :73-74       */
+  MRAFT_F_APPLIED = 16,      /* the reply passed the term/state/prev gate, :73-74       */
+  MRAFT_F_SNAPSHOT_INSTALLED = 32 /* HandleInstallSnapshot replaced the log: hasSnapshot,
+                                     raft_snapshot.go:38-52 (deliver the bytes)          */
 };
 
 /* Per-group flags written by mraft_replicate_tick (int32 group_flags[G]). */
@@ -98,11 +100,14 @@ enum {
   MRAFT_G_ACTIVE = 1,        /* the leader replica was a leader and sent AEs          */
   MRAFT_G_COMMITTED = 2,     /* leader commitIndex advanced                            */
   MRAFT_G_STEPPED_DOWN = 4,  /* leader stepped down on a higher reply term             */
-  MRAFT_G_NEED_SNAPSHOT = 8, /* some peer needs InstallSnapshot (prev < dummy)         */
+  MRAFT_G_NEED_SNAPSHOT = 8, /* some peer had prev < dummy: InstallSnapshot sent        */
   MRAFT_G_ERROR = 16,        /* a3 would panic / bad state / log full: group skipped   */
   MRAFT_G_FOLLOWER_COMMIT = 32, /* some follower advanced its commitIndex              */
   MRAFT_G_LOG_FULL = 64,     /* a follower rejected its AE with MRAFT_ITEM_LOG_FULL    */
-  MRAFT_G_ELECTED = 128      /* mraft_election_rounds: some replica became leader     */
+  MRAFT_G_ELECTED = 128,     /* mraft_election_rounds: some replica became leader     */
+  MRAFT_G_SNAPSHOT_INSTALLED = 256, /* a follower installed the leader's snapshot       */
+  MRAFT_G_FOLLOWER_PANIC = 512 /* a follower's handler would panic (InstallSnapshot below
+                                  its own dummy, raft_log.go:56-58): message dropped    */
 };
 
 /* Per-slot state, struct-of-arrays (raft.go:16-40). Arrays of G*P int32 unless
@@ -185,6 +190,33 @@ typedef struct {
   int32_t vote_granted;
 } mraft_rv_result;
 
+/* InstallSnapshotArgs, raft_rpc.go:84-90 (the snapshot bytes stay on the
+ * host); `slot` is the receiving replica. */
+typedef struct {
+  int32_t slot;
+  int32_t term;
+  int32_t leader_id;
+  int32_t last_included_index;
+  int32_t last_included_term;
+} mraft_is_args;
+
+/* InstallSnapshotReply, raft_rpc.go:92-95 (`Success` is never set by the
+ * reference: always 0). */
+typedef struct {
+  int32_t term;
+  int32_t success;
+} mraft_is_reply;
+
+/* One InstallSnapshot reply delivered back to a leader replica with the args
+ * fields processInstallSnapshotReply reads (raft_snapshot.go:56-69). */
+typedef struct {
+  int32_t slot;
+  int32_t peer;
+  int32_t args_term;
+  int32_t args_last_included_index;
+  int32_t reply_term;
+} mraft_is_result;
+
 typedef struct mraft_engine mraft_engine;
 
 /* ---- lifetime ---------------------------------------------------------- */
@@ -250,10 +282,12 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items,
                                  int32_t *item_err, int32_t where);
 
 /* Fused co-resident tick: for every group g with leader_peer[g] >= 0, the
- * leader replica gathers AppendEntries for every other peer (a3), each
- * follower replica handles it (a4, entries read in place from the leader's
- * log), and the leader folds the replies in peer order (a2 + a1). Equivalent
- * to the sequence gather -> handle -> process on the same state.
+ * leader replica runs appendOneRound for every other peer (a3): an
+ * AppendEntries (entries read in place from the leader's log) or, when
+ * nextIndex-1 < dummyIndex, an InstallSnapshot; each follower replica handles
+ * its message (a4 / HandleInstallSnapshot) and the leader folds the replies
+ * in peer order (a2 + a1 / processInstallSnapshotReply). Equivalent to the
+ * sequence gather -> handle -> process on the same state.
  * group_flags (optional, [G]) gets MRAFT_G_* bits. */
 int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer,
                          int32_t *group_flags, int32_t where);
@@ -281,6 +315,43 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts,
  * the host maps indices to its commands. */
 int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to,
                         int32_t where);
+
+/* ---- snapshots --------------------------------------- */
+
+/* Snapshot (raft_snapshot.go:3-13) for n items: if index[i] > dummyIndex, the
+ * log keeps [index, last] with the entry at `index` as the new dummy (the log
+ * prefix is dropped; the service keeps the snapshot bytes). index > lastIndex
+ * is a Go panic: MRAFT_ITEM_PREV_BEYOND_LAST. */
+int mraft_snapshot(mraft_engine *h, const int32_t *slots, const int32_t *index,
+                   int64_t n, int32_t *item_err, int32_t where);
+
+/* a3's snapshot branch (raft_append_entry.go:27-34): for leader slots whose
+ * nextIndex[peer]-1 < dummyIndex, the InstallSnapshot args
+ * {currentTerm, me, dummyIndex, dummyTerm}; other items get
+ * MRAFT_ITEM_BAD_STATE (not a leader, :22-25) or MRAFT_ITEM_OK with
+ * args.slot = -1 (an AppendEntries is due instead). */
+int mraft_gather_install_snapshot_args(mraft_engine *h, const int32_t *slots,
+                                       const int32_t *peers, int64_t n,
+                                       mraft_is_args *out_args,
+                                       int32_t *item_err, int32_t where);
+
+/* HandleInstallSnapshot (raft_snapshot.go:15-54) for n items at distinct
+ * slots; out_flags[i] gets MRAFT_F_SNAPSHOT_INSTALLED when the log was
+ * replaced (the host then delivers the snapshot to the service, raft.go:168-177).
+ * A LastIncludedIndex in (commitIndex, lastIndex] but below the follower's own
+ * dummyIndex makes Go's sliceFrom panic: MRAFT_ITEM_BELOW_DUMMY, no change. */
+int mraft_handle_install_snapshot(mraft_engine *h, const mraft_is_args *args,
+                                  int64_t n, mraft_is_reply *replies,
+                                  int32_t *out_flags, int32_t *item_err,
+                                  int32_t where);
+
+/* processInstallSnapshotReply (raft_snapshot.go:56-69), segments as in
+ * mraft_process_append_replies. */
+int mraft_process_install_snapshot_replies(mraft_engine *h,
+                                           const mraft_is_result *items,
+                                           int64_t n, const int64_t *seg_begin,
+                                           int64_t n_seg, int32_t *out_flags,
+                                           int32_t *item_err, int32_t where);
 
 /* ---- elections ------------------------------- */
 

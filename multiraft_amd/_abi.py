@@ -23,6 +23,8 @@ OK, E_INVAL, E_NOMEM, E_HIP, E_NOSTATE = 0, -1, -2, -3, -4
 (ITEM_OK, ITEM_PREV_BEYOND_LAST, ITEM_BELOW_DUMMY, ITEM_LOG_FULL, ITEM_NEED_SNAPSHOT,
  ITEM_DUP_SLOT, ITEM_BAD_SLOT, ITEM_BAD_STATE) = range(8)
 F_NEED_MORE, F_COMMITTED, F_STEPPED_DOWN, F_BECAME_LEADER, F_APPLIED = 1, 2, 4, 8, 16
+F_SNAPSHOT_INSTALLED = 32
+G_SNAPSHOT_INSTALLED = 256
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
  G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
 SYN_MATCH, SYN_MISMATCH, SYN_BEYOND, SYN_STALE, SYN_BELOW_DUMMY, SYN_HEARTBEAT = range(6)
@@ -57,6 +59,11 @@ AE_RESULT = np.dtype([("slot", "<i4"), ("peer", "<i4"), ("args_term", "<i4"),
 RV_ARGS = np.dtype([("slot", "<i4"), ("candidate_id", "<i4"), ("term", "<i4"),
                     ("last_log_index", "<i4"), ("last_log_term", "<i4")])
 RV_REPLY = np.dtype([("term", "<i4"), ("vote_granted", "<i4")])
+IS_ARGS = np.dtype([("slot", "<i4"), ("term", "<i4"), ("leader_id", "<i4"),
+                    ("last_included_index", "<i4"), ("last_included_term", "<i4")])
+IS_REPLY = np.dtype([("term", "<i4"), ("success", "<i4")])
+IS_RESULT = np.dtype([("slot", "<i4"), ("peer", "<i4"), ("args_term", "<i4"),
+                      ("args_last_included_index", "<i4"), ("reply_term", "<i4")])
 RV_RESULT = np.dtype([("slot", "<i4"), ("peer", "<i4"), ("args_term", "<i4"),
                       ("reply_term", "<i4"), ("vote_granted", "<i4")])
 assert AE_ARGS.itemsize == 40 and AE_RESULT.itemsize == 32 and RV_ARGS.itemsize == 20
@@ -69,6 +76,8 @@ ABI_SYMBOLS = (
     "mraft_gather_append_args", "mraft_handle_append_entries",
     "mraft_process_append_replies", "mraft_replicate_tick", "mraft_replicate_tick_count",
     "mraft_start", "mraft_collect_apply", "mraft_election_rounds",
+    "mraft_snapshot", "mraft_gather_install_snapshot_args", "mraft_handle_install_snapshot",
+    "mraft_process_install_snapshot_replies",
     "mraft_start_election", "mraft_handle_request_vote", "mraft_process_vote_replies",
     "mraft_export_group_status",
 )
@@ -96,6 +105,10 @@ _SIGS = {
     "mraft_start": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32]),
     "mraft_collect_apply": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_election_rounds": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32]),
+    "mraft_snapshot": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i32]),
+    "mraft_gather_install_snapshot_args": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _i32]),
+    "mraft_handle_install_snapshot": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp, _i32]),
+    "mraft_process_install_snapshot_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),
     "mraft_start_election": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_handle_request_vote": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_process_vote_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),

@@ -442,6 +442,93 @@ int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int
   return sg.finish();
 }
 
+int mraft_snapshot(mraft_engine *h, const int32_t *slots, const int32_t *index, int64_t n,
+                   int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !index || !item_err))) return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *s, *x, *e;
+  TRY(sg.map(slots, sizeof(int32_t) * n, true, false, &s));
+  TRY(sg.map(index, sizeof(int32_t) * n, true, false, &x));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_claim(s, n, sizeof(int32_t), 0, nullptr, gp_of(h), h->P, h->claim, h->epoch,
+                      (int32_t *)e, h->stream);
+  mraft::launch_snapshot(dev_of(h), (const int32_t *)s, (const int32_t *)x, n, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_gather_install_snapshot_args(mraft_engine *h, const int32_t *slots, const int32_t *peers,
+                                       int64_t n, mraft_is_args *out_args, int32_t *item_err,
+                                       int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !peers || !out_args || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *s, *p, *o, *e;
+  TRY(sg.map(slots, sizeof(int32_t) * n, true, false, &s));
+  TRY(sg.map(peers, sizeof(int32_t) * n, true, false, &p));
+  TRY(sg.map(out_args, sizeof(mraft_is_args) * n, false, true, &o));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_gather_is(dev_of(h), (const int32_t *)s, (const int32_t *)p, n, (mraft_is_args *)o,
+                          (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_handle_install_snapshot(mraft_engine *h, const mraft_is_args *args, int64_t n,
+                                  mraft_is_reply *replies, int32_t *out_flags, int32_t *item_err,
+                                  int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!args || !replies || !out_flags || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *a, *r, *f, *e;
+  TRY(sg.map(args, sizeof(mraft_is_args) * n, true, false, &a));
+  TRY(sg.map(replies, sizeof(mraft_is_reply) * n, false, true, &r));
+  TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &f));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  mraft::launch_claim(a, n, sizeof(mraft_is_args), offsetof(mraft_is_args, slot), nullptr, gp_of(h),
+                      h->P, h->claim, h->epoch, (int32_t *)e, h->stream);
+  mraft::launch_handle_is(dev_of(h), (const mraft_is_args *)a, n, (mraft_is_reply *)r, (int32_t *)f,
+                          (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
+int mraft_process_install_snapshot_replies(mraft_engine *h, const mraft_is_result *items, int64_t n,
+                                           const int64_t *seg_begin, int64_t n_seg,
+                                           int32_t *out_flags, int32_t *item_err, int32_t where) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
+  if (n == 0) return MRAFT_OK;
+  const int64_t ns = seg_begin ? n_seg : n;
+  HIP_TRY(hipSetDevice(h->device));
+  TRY(ensure_claim(h));
+  Stage sg(h, where);
+  void *it, *sb, *fl, *e, *se;
+  TRY(sg.map(items, sizeof(mraft_is_result) * n, true, false, &it));
+  TRY(sg.map(seg_begin, sizeof(int64_t) * (size_t)(seg_begin ? n_seg + 1 : 0), true, false, &sb));
+  TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &fl));
+  TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
+  TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
+  HIP_TRY(hipMemsetAsync(fl, 0, sizeof(int32_t) * n, h->stream));
+  HIP_TRY(hipMemsetAsync(e, 0, sizeof(int32_t) * n, h->stream));
+  mraft::launch_claim(it, ns, sizeof(mraft_is_result), offsetof(mraft_is_result, slot),
+                      (const int64_t *)sb, gp_of(h), h->P, h->claim, h->epoch, (int32_t *)se,
+                      h->stream);
+  mraft::launch_process_is(dev_of(h), (const mraft_is_result *)it, n, (const int64_t *)sb, ns,
+                           (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
+  return sg.finish();
+}
+
 int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n, mraft_rv_args *out_args,
                          int32_t *item_err, int32_t where) {
   TRY(check(h));

@@ -129,6 +129,28 @@ __device__ __forceinline__ void wave_copy(const int32_t *__restrict__ E, int32_t
   }
 }
 
+// row[dst + k] = row[from + k] for k in [0, cnt), from > dst (raftLog.setLogs(
+// sliceFrom), raft_log.go:18-21,75-77): ascending chunks, every load of a chunk
+// before its stores, so the overlapping move is safe.
+__device__ __forceinline__ void wave_shift_left(int32_t *__restrict__ row, int from, int cnt,
+                                                int dst = 0) {
+  const int lane = lane_id();
+  for (int base = 0; base < cnt; base += kChunk) {
+    int v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = base + lane + kWave * u;
+      v[u] = k < cnt ? row[from + k] : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = base + lane + kWave * u;
+      if (k < cnt) row[dst + k] = v[u];
+    }
+  }
+}
+
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }
 
 template <typename T>

@@ -31,6 +31,15 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
                   int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st);
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t st);
+void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,
+                     int32_t *err, hipStream_t st);
+void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
+                      mraft_is_args *out, int32_t *err, hipStream_t st);
+void launch_handle_is(const Dev &s, const mraft_is_args *args, int64_t n, mraft_is_reply *rep,
+                      int32_t *flags, int32_t *err, hipStream_t st);
+void launch_process_is(const Dev &s, const mraft_is_result *items, int64_t n, const int64_t *seg_begin,
+                       int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
+                       hipStream_t st);
 void launch_start_election(const Dev &s, const int32_t *slots, int64_t n, mraft_rv_args *out,
                            int32_t *err, hipStream_t st);
 void launch_handle_rv(const Dev &s, const mraft_rv_args *args, int64_t n, mraft_rv_reply *rep,

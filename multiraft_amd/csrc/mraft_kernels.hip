@@ -315,6 +315,144 @@ __global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__re
   }
 }
 
+// ---------------------------------------------------------------- snapshots
+// Snapshot (raft_snapshot.go:3-13): wave per item.
+__global__ __launch_bounds__(256) void k_snapshot(Dev s, const int32_t *__restrict__ slots,
+                                                  const int32_t *__restrict__ index, int64_t n,
+                                                  int32_t *__restrict__ err) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (i >= n || err[i]) return;
+  const int sl = slots[i], x = index[i];
+  const int d = s.dummy[sl], last = s.last[sl];
+  if (x <= d) return;                                                  // :6-9
+  if (x > last) {                                                      // sliceFrom panics
+    if (lane_id() == 0) err[i] = MRAFT_ITEM_PREV_BEYOND_LAST;
+    return;
+  }
+  wave_shift_left(s.log + (int64_t)sl * s.L, x - d, last - x + 1);     // :10
+  if (lane_id() == 0) s.dummy[sl] = x;
+}
+
+// appendOneRound's snapshot branch (raft_append_entry.go:27-34).
+__global__ void k_gather_is(Dev s, const int32_t *__restrict__ slots, const int32_t *__restrict__ peers,
+                            int64_t n, mraft_is_args *__restrict__ out, int32_t *__restrict__ err) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int P = s.P;
+  const int64_t gp = (int64_t)s.G * P;
+  mraft_is_args a = {-1, 0, 0, 0, 0};
+  int e = 0;
+  const int slot = slots[i], peer = peers[i];
+  if (slot < 0 || slot >= gp || peer < 0 || peer >= P || peer == slot % P) {
+    e = MRAFT_ITEM_BAD_SLOT;
+  } else if (s.role[slot] != kLeader) {
+    e = MRAFT_ITEM_BAD_STATE;
+  } else if (s.next[(int64_t)slot * P + peer] - 1 < s.dummy[slot]) {
+    a.slot = (slot / P) * P + peer;
+    a.term = s.term[slot];                                             // :29
+    a.leader_id = slot % P;                                            // :30
+    a.last_included_index = s.dummy[slot];                             // :31
+    a.last_included_term = s.log[(int64_t)slot * s.L];                 // :32 dummyTerm
+  }
+  out[i] = a;
+  err[i] = e;
+}
+
+// HandleInstallSnapshot (raft_snapshot.go:15-54): wave per item.
+__global__ __launch_bounds__(256) void k_handle_is(Dev s, const mraft_is_args *__restrict__ args,
+                                                   int64_t n, mraft_is_reply *__restrict__ rep,
+                                                   int32_t *__restrict__ flags,
+                                                   int32_t *__restrict__ err) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (i >= n) return;
+  const int lane = lane_id();
+  if (err[i]) {
+    if (lane == 0) { rep[i] = mraft_is_reply{0, 0}; flags[i] = 0; }
+    return;
+  }
+  const mraft_is_args a = args[i];
+  const int f = a.slot, fterm = s.term[f];
+  int fl = 0;
+  if (a.term < fterm) {                                                // :20-22
+    if (lane == 0) { rep[i] = mraft_is_reply{fterm, 0}; flags[i] = 0; }
+    return;
+  }
+  const int lii = a.last_included_index;
+  const int fcommit = s.commit[f];
+  int32_t *row = s.log + (int64_t)f * s.L;
+  const bool install = lii > fcommit;                                  // :31-33
+  const int fd = s.dummy[f], flast = s.last[f];
+  if (install && lii <= flast && lii < fd) {                           // sliceFrom panics
+    if (lane == 0) { rep[i] = mraft_is_reply{0, 0}; flags[i] = 0; err[i] = MRAFT_ITEM_BELOW_DUMMY; }
+    return;
+  }
+  int newlast = -1;
+  if (install) {
+    if (lii > flast) {                                                 // :35-37
+      newlast = lii;
+    } else {                                                           // :38-40
+      // entries (lii, flast] move to slots 1..; slot 0 takes LastIncludedTerm
+      // below (:44-45), so no lane rewrites an address another lane stored.
+      if (lii > fd) wave_shift_left(row, lii - fd + 1, flast - lii, 1);
+    }
+    fl = MRAFT_F_SNAPSHOT_INSTALLED;
+  }
+  if (lane == 0) {
+    if (a.term > fterm) { s.term[f] = a.term; s.voted[f] = -1; }       // :23-26
+    s.role[f] = kFollower;                                             // :28
+    if (install) {
+      row[0] = a.last_included_term;                                   // :44-45
+      if (newlast >= 0) s.last[f] = newlast;
+      s.dummy[f] = lii;
+      s.commit[f] = lii;                                               // :42
+      s.applied[f] = lii;                                              // :43
+    }
+    rep[i] = mraft_is_reply{a.term, 0};                                // deferred reply.Term
+    flags[i] = fl;
+  }
+}
+
+// processInstallSnapshotReply (raft_snapshot.go:56-69): lane per segment.
+__global__ void k_process_is(Dev s, const mraft_is_result *__restrict__ items, int64_t n,
+                             const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                             const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
+                             int32_t *__restrict__ item_err) {
+  const int64_t sg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (sg >= n_seg) return;
+  const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
+  if (b >= e) return;
+  const int P = s.P;
+  const int slot = items[b].slot;
+  int bad = seg_err[sg];
+  if (!bad)
+    for (int64_t i = b; i < e; ++i) {
+      const mraft_is_result it = items[i];
+      if (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+    }
+  if (bad) {
+    for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
+    return;
+  }
+  int term = s.term[slot], role = s.role[slot];
+  const int t0 = term;
+  for (int64_t i = b; i < e; ++i) {
+    const mraft_is_result it = items[i];
+    int fl = 0;
+    if (it.reply_term > term) {                                        // :59-64
+      term = it.reply_term;
+      role = kFollower;
+      fl = MRAFT_F_STEPPED_DOWN;
+    } else if (role == kLeader && it.args_term == term) {              // :65-68
+      s.match[(int64_t)slot * P + it.peer] = it.args_last_included_index;
+      s.next[(int64_t)slot * P + it.peer] = it.args_last_included_index + 1;
+      fl = MRAFT_F_APPLIED;
+    }
+    flags[i] = fl;
+    item_err[i] = 0;
+  }
+  if (term != t0) { s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1; }
+}
+
 // ---------------------------------------------------------------- a6 part 1
 __global__ void k_start_election(Dev s, const int32_t *__restrict__ slots, int64_t n,
                                  mraft_rv_args *__restrict__ out, int32_t *__restrict__ err) {
@@ -499,6 +637,34 @@ void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t 
   int blocks = blocks_for((int64_t)s.G * s.P);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_collect_apply, dim3(blocks), dim3(kBlock), 0, st, s, from, to);
+}
+
+void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,
+                     int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_snapshot, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, slots, index, n, err);
+}
+
+void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
+                      mraft_is_args *out, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_gather_is, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, peers, n, out, err);
+}
+
+void launch_handle_is(const Dev &s, const mraft_is_args *args, int64_t n, mraft_is_reply *rep,
+                      int32_t *flags, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_handle_is, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, args, n, rep,
+                     flags, err);
+}
+
+void launch_process_is(const Dev &s, const mraft_is_result *items, int64_t n, const int64_t *seg_begin,
+                       int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
+                       hipStream_t st) {
+  (void)n;
+  if (n_seg <= 0) return;
+  hipLaunchKernelGGL(k_process_is, dim3(blocks_for(n_seg, 64)), dim3(64), 0, st, s, items, n,
+                     seg_begin, n_seg, seg_err, flags, item_err);
 }
 
 void launch_start_election(const Dev &s, const int32_t *slots, int64_t n, mraft_rv_args *out,

@@ -47,7 +47,11 @@ enum : int {
   IC_SCAN,      // term(prev) differs, ConflictIndex needs the backward scan
   IC_MERGE,     // prefix matches, n > 0 entries to merge
   IC_HB,        // prefix matches, heartbeat
-  IC_FULL       // merge would exceed capacity L: rejected
+  IC_FULL,      // merge would exceed capacity L: rejected
+  IC_IS_STALE,  // InstallSnapshot, args.Term < currentTerm (raft_snapshot.go:20-22)
+  IC_IS_OLD,    // InstallSnapshot, outdated snapshot (:31-33)
+  IC_IS_INSTALL,// InstallSnapshot installed (:35-50)
+  IC_IS_PANIC   // InstallSnapshot whose sliceFrom would panic: dropped
 };
 
 enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };
@@ -74,6 +78,39 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+#ifndef MRAFT_TICK_NT
+#define MRAFT_TICK_NT 1    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
+#endif
+
+// Streaming (read-once / write-once) log accesses of the pass.
+__device__ __forceinline__ int4 ld4(const int32_t *p) {
+  if (MRAFT_TICK_NT & 2) {
+    const int4 *q = reinterpret_cast<const int4 *>(p);
+    return make_int4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
+                     __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
+  }
+  return *reinterpret_cast<const int4 *>(p);
+}
+__device__ __forceinline__ int ld1(const int32_t *p) {
+  if (MRAFT_TICK_NT & 2) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ __forceinline__ void st4(int32_t *p, int a, int b, int c, int d) {
+  if (MRAFT_TICK_NT & 1) {
+    int4 *q = reinterpret_cast<int4 *>(p);
+    __builtin_nontemporal_store(a, &q->x);
+    __builtin_nontemporal_store(b, &q->y);
+    __builtin_nontemporal_store(c, &q->z);
+    __builtin_nontemporal_store(d, &q->w);
+  } else {
+    *reinterpret_cast<int4 *>(p) = make_int4(a, b, c, d);
+  }
+}
+__device__ __forceinline__ void st1(int32_t *p, int a) {
+  if (MRAFT_TICK_NT & 1) __builtin_nontemporal_store(a, p);
+  else *p = a;
+}
 
 // One chunk of the streaming pass over the leader's log. The pass serves
 // (1) every follower q's entry merge: compare entries [start_q, cend_q) with
@@ -103,11 +140,11 @@ __device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long 
   for (int v = 0; v < V; ++v) {
     if (VEC) {
       int4 x = make_int4(0, 0, 0, 0);
-      if (idx[v][3] >= plo && idx[v][0] <= phi) x = *reinterpret_cast<const int4 *>(log + eo + idx[v][0]);
+      if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(log + eo + idx[v][0]);
       e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? log[eo + idx[v][u]] : 0;
+      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(log + eo + idx[v][u]) : 0;
     }
   }
   int f[NI][V][4];
@@ -122,13 +159,13 @@ __device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long 
     for (int v = 0; v < V; ++v) {
       if (VEC) {
         if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
-          const int4 x = *reinterpret_cast<const int4 *>(log + fo[q] + idx[v][0]);
+          const int4 x = ld4(log + fo[q] + idx[v][0]);
           f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
         }
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = log[fo[q] + idx[v][u]];
+          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(log + fo[q] + idx[v][u]);
       }
     }
   }
@@ -211,12 +248,11 @@ __device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long 
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
-            *reinterpret_cast<int4 *>(log + fo[q] + idx[v][0]) =
-                make_int4(e[v][0], e[v][1], e[v][2], e[v][3]);
+            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) log[fo[q] + idx[v][u]] = e[v][u];
+              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
           }
         }
       }
@@ -250,11 +286,11 @@ __device__ __forceinline__ void copy_loop(int32_t *__restrict__ log, long long e
     for (int v = 0; v < VC; ++v) {
       if (VEC) {
         int4 x = make_int4(0, 0, 0, 0);
-        if (idx[v][0] <= phi) x = *reinterpret_cast<const int4 *>(log + eo + idx[v][0]);
+        if (idx[v][0] <= phi) x = ld4(log + eo + idx[v][0]);
         e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? log[eo + idx[v][u]] : 0;
+        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? ld1(log + eo + idx[v][u]) : 0;
       }
     }
     if (scan) {
@@ -291,12 +327,11 @@ __device__ __forceinline__ void copy_loop(int32_t *__restrict__ log, long long e
 #pragma unroll
         for (int v = 0; v < VC; ++v) {
           if (VEC && idx[v][3] < nend) {
-            *reinterpret_cast<int4 *>(log + fo[q] + idx[v][0]) =
-                make_int4(e[v][0], e[v][1], e[v][2], e[v][3]);
+            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[v][u] < nend) log[fo[q] + idx[v][u]] = e[v][u];
+              if (idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
           }
         }
       }
@@ -313,9 +348,12 @@ struct Fold {
   int term, stepped, any, mstar;
   int gate[NI], rs[NI], rp[NI], rn[NI], rx[NI], ic[NI];
 
+  // is_m: followers whose reply is an InstallSnapshot reply
+  // (processInstallSnapshotReply, raft_snapshot.go:56-69) for
+  // LastIncludedIndex lii; rp/rn of those items read (lii, 0).
   __device__ __forceinline__ void run(int T, int lp, int (&mm)[P], unsigned long long have_m,
-                                      unsigned long long succ_m, int rterm, int prev, int n,
-                                      int rci, int icls) {
+                                      unsigned long long succ_m, unsigned long long is_m, int lii,
+                                      int rterm, int prev, int n, int rci, int icls) {
     term = T;
     stepped = 0;
     any = 0;
@@ -330,13 +368,26 @@ struct Fold {
       rn[q] = uni(__shfl(n, q, 64));
       rx[q] = rp[q] + 1;                                                 // nextIndex[q] (gathered)
       ic[q] = uni(__shfl(icls, q, 64));
+      if (ic[q] >= IC_IS_STALE) {
+        rp[q] = lii;
+        rn[q] = 0;
+      }
       const int rt = uni(__shfl(rterm, q, 64));
       const int rc = uni(__shfl(rci, q, 64));
       if (!((have_m >> q) & 1)) continue;
-      if (rt > term) {                                                   // :67-72
+      if (rt > term) {                                                   // :67-72, snapshot :59-64
         term = rt;
         role = kFollower;
         stepped = 1;
+      } else if ((is_m >> q) & 1) {
+        if (role == kLeader && T == term) {                              // snapshot :65-67
+          gate[q] = 1;
+          rs[q] = 1;
+#pragma unroll
+          for (int j = 0; j < P; ++j)
+            if (j == pq) mm[j] = lii;
+          rx[q] = lii + 1;
+        }
       } else if (rt == term && role == kLeader && T == term) {           // :73-74 (prev gate holds)
         gate[q] = 1;
         if (rs[q]) {
@@ -447,6 +498,21 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   const int n = last - prev;                                             // :50
   int rterm = 0, rsucc = 0, rci = 0;
   bool adopt = false;
+  // InstallSnapshot (raft_append_entry.go:27-34 -> raft_snapshot.go:15-54),
+  // LastIncludedIndex = leader dummyIndex, LastIncludedTerm = dummyTerm.
+  const int lit = snap_m ? uni(s.log[lrow]) : 0;
+  if (icls == IC_SNAP) {
+    if (T >= fterm && ldummy > fcommit && ldummy <= flast && ldummy < fdummy) {
+      icls = IC_IS_PANIC;                                                // sliceFrom panics
+    } else if (T < fterm) {                                              // :20-22
+      icls = IC_IS_STALE;
+      rterm = fterm;
+    } else {
+      adopt = T > fterm;                                                 // :23-26
+      rterm = T;
+      icls = ldummy <= fcommit ? IC_IS_OLD : IC_IS_INSTALL;              // :31-33
+    }
+  }
   if (icls == IC_GO) {
     if (T < fterm) {                                                     // :112-115
       icls = IC_STALE;
@@ -489,6 +555,17 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
     }
   }
 
+  if (!COUNT) {  // InstallSnapshot sliceFrom(LastIncludedIndex) (:38-40)
+    unsigned long long m = __ballot(icls == IC_IS_INSTALL && ldummy <= flast);
+    while (m) {
+      const int src = first_lane(m);
+      m &= m - 1;
+      const long long sf = (long long)g * P + (src < lp ? src : src + 1);
+      const int sd = __shfl(fdummy, src, 64), sl = __shfl(flast, src, 64);
+      if (ldummy > sd) wave_shift_left(s.log + sf * L, ldummy - sd + 1, sl - ldummy, 1);
+    }
+  }
+
   // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
   long long fo[NI];
@@ -519,10 +596,11 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   // commit scan of a Figure-8 group rides along the same streaming pass.
   Fold<P> fd;
   int commit = c0, top = 0, slo = 1, shi = 0;
-  const unsigned long long have0 = __ballot(icls >= IC_STALE && icls <= IC_HB);
+  const unsigned long long is_m = __ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
+  const unsigned long long have0 = __ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
   const unsigned long long succ0 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
   if (!maybe_full) {
-    fd.run(T, lp, mm, have0, succ0, rterm, prev, n, rci, icls);
+    fd.run(T, lp, mm, have0, succ0, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
@@ -572,9 +650,9 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   if (!maybe_full) {
     if (slo <= shi && found > c0) commit = found;
   } else {
-    const unsigned long long have1 = __ballot(icls >= IC_STALE && icls <= IC_HB);
+    const unsigned long long have1 = __ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
     const unsigned long long succ1 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
-    fd.run(T, lp, mm, have1, succ1, rterm, prev, n, rci, icls);
+    fd.run(T, lp, mm, have1, succ1, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
@@ -624,6 +702,38 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
       }
     }
   }
+  if (icls >= IC_IS_STALE && icls <= IC_IS_INSTALL) {
+    cR = 1;                                                              // term
+    if (icls != IC_IS_STALE) {
+      if (!COUNT) {
+        if (adopt) { s.term[f] = T; s.voted[f] = -1; }
+        s.role[f] = kFollower;                                           // :28
+      }
+      cR += 1;                                                           // commit
+      cW = (adopt ? 2 : 0) + 1;
+      if (icls == IC_IS_INSTALL) {
+        const bool newlog = ldummy > flast;                              // :35-37
+        if (!COUNT) {
+          s.log[f * L] = lit;                                            // :44-45
+          if (newlog) s.last[f] = ldummy;
+          s.dummy[f] = ldummy;
+          s.commit[f] = ldummy;                                          // :42
+          s.applied[f] = ldummy;                                         // :43
+        }
+        cR += 1;                                                         // last
+        cW += 3;
+        if (newlog) {
+          cW += 2;                                                       // log slot 0, last
+        } else {
+          const long long k = (long long)flast - ldummy + 1;
+          cR += 1 + k;                                                   // dummy, sliced terms
+          cW += k;
+        }
+      }
+    }
+  }
+  if (__ballot(icls == IC_IS_INSTALL)) flags |= MRAFT_G_SNAPSHOT_INSTALLED;
+  if (__ballot(icls == IC_IS_PANIC)) flags |= MRAFT_G_FOLLOWER_PANIC;
   if (__ballot(icls == IC_FULL)) flags |= MRAFT_G_LOG_FULL;
   if (__ballot(fcadv != 0)) flags |= MRAFT_G_FOLLOWER_COMMIT;
 
@@ -668,7 +778,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
     u -= interval_len(max(A, a1lo), min((long long)last, a1hi));
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
-      if (fd.ic[q] < IC_STALE) continue;  // a3 read log[prev] for every gathered item
+      if (fd.ic[q] < IC_STALE) continue;  // log[prev] per gathered item, log[dummy] per snapshot
       bool dup = false;
 #pragma unroll
       for (int q2 = 0; q2 < q; ++q2) dup |= (fd.ic[q2] >= IC_STALE && fd.rp[q2] == fd.rp[q]);

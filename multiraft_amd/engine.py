@@ -15,8 +15,8 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (AE_ARGS, AE_REPLY, AE_RESULT, RV_ARGS, RV_REPLY, RV_RESULT, DEVICE, HOST,
-                   STATE_FIELDS, ptr, soa_of)
+from ._abi import (AE_ARGS, AE_REPLY, AE_RESULT, IS_ARGS, IS_REPLY, IS_RESULT, RV_ARGS, RV_REPLY,
+                   RV_RESULT, DEVICE, HOST, STATE_FIELDS, ptr, soa_of)
 
 
 class MraftError(RuntimeError):
@@ -218,6 +218,47 @@ class Engine:
         to = np.zeros(gp, np.int32)
         _ck(self._lib.mraft_collect_apply(self._h, ptr(fr), ptr(to), HOST), "mraft_collect_apply")
         return fr, to
+
+    # ---- snapshots (raft_snapshot.go) -------------------------------------
+    def snapshot(self, slots, index):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        index = np.ascontiguousarray(index, dtype=np.int32)
+        err = np.zeros(len(slots), np.int32)
+        _ck(self._lib.mraft_snapshot(self._h, ptr(slots), ptr(index), len(slots), ptr(err), HOST),
+            "mraft_snapshot")
+        return err
+
+    def gather_install_snapshot_args(self, slots, peers):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=IS_ARGS)
+        err = np.zeros(n, np.int32)
+        _ck(self._lib.mraft_gather_install_snapshot_args(self._h, ptr(slots), ptr(peers), n, ptr(out),
+                                                         ptr(err), HOST),
+            "mraft_gather_install_snapshot_args")
+        return out, err
+
+    def handle_install_snapshot(self, args):
+        args = np.ascontiguousarray(args, dtype=IS_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=IS_REPLY)
+        fl = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        _ck(self._lib.mraft_handle_install_snapshot(self._h, ptr(args), n, ptr(rep), ptr(fl), ptr(err),
+                                                    HOST), "mraft_handle_install_snapshot")
+        return rep, fl, err
+
+    def process_install_snapshot_replies(self, items, seg_begin=None):
+        items = np.ascontiguousarray(items, dtype=IS_RESULT)
+        n = len(items)
+        fl = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        _ck(self._lib.mraft_process_install_snapshot_replies(
+            self._h, ptr(items), n, ptr(sb), 0 if sb is None else len(sb) - 1, ptr(fl), ptr(err), HOST),
+            "mraft_process_install_snapshot_replies")
+        return fl, err
 
     # ---- elections -------------------------------------------------------
     def start_election(self, slots):

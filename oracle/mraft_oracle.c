@@ -387,6 +387,176 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
 }
 
 /* ------------------------------------------------------------------------ */
+/* Snapshots, src/raft/raft_snapshot.go                                      */
+/* ------------------------------------------------------------------------ */
+
+/* raftLog.setLogs(sliceFrom(index)) (raft_log.go:18-21,75-77): keep [index,
+ * last], the entry at index becomes slot 0. Marks the words it reads/writes. */
+static void slice_from(ora_engine *e, int32_t s, int32_t index) {
+  const int64_t row = (int64_t)s * e->L;
+  const int32_t d = S.dummy_index[s], last = S.last_index[s];
+  for (int32_t i = index; i <= last; ++i) {
+    CR(A_LOG, row + i - d);
+    S.log_term[row + i - index] = S.log_term[row + i - d];
+    CW(A_LOG, row + i - index);
+  }
+  S.dummy_index[s] = index;
+}
+
+/* Snapshot(index, snapshot), raft_snapshot.go:3-13 */
+static int32_t snapshot_one(ora_engine *e, int32_t s, int32_t index) {
+  if (index <= S.dummy_index[s]) return MRAFT_ITEM_OK;                /* :6-9 */
+  if (index > S.last_index[s]) return MRAFT_ITEM_PREV_BEYOND_LAST;    /* sliceFrom panics */
+  slice_from(e, s, index);                                            /* :10-11 */
+  return MRAFT_ITEM_OK;
+}
+
+int ora_snapshot(ora_engine *e, const int32_t *slots, const int32_t *index, int64_t n,
+                 int32_t *item_err) {
+  int32_t *first = claim_slots(e, slots, n, sizeof(int32_t), item_err);
+  for (int64_t i = 0; i < n; ++i)
+    if (!item_err[i]) item_err[i] = snapshot_one(e, slots[i], index[i]);
+  free(first);
+  return MRAFT_OK;
+}
+
+/* appendOneRound's snapshot branch, raft_append_entry.go:27-34 */
+static int32_t gather_is_one(ora_engine *e, int32_t slot, int32_t peer, mraft_is_args *a) {
+  const int32_t P = e->P;
+  a->slot = -1;
+  if (peer < 0 || peer >= P || peer == slot % P) return MRAFT_ITEM_BAD_SLOT;
+  if (S.state[slot] != MRAFT_LEADER) return MRAFT_ITEM_BAD_STATE;
+  const int32_t prev = S.next_index[(int64_t)slot * P + peer] - 1;
+  if (prev >= S.dummy_index[slot]) return MRAFT_ITEM_OK;            /* an AppendEntries is due */
+  a->slot = (slot / P) * P + peer;
+  a->term = S.current_term[slot];                                     /* :29 */
+  a->leader_id = slot % P;                                            /* :30 */
+  a->last_included_index = S.dummy_index[slot];                       /* :31 */
+  a->last_included_term = S.log_term[(int64_t)slot * e->L];           /* :32 dummyTerm */
+  return MRAFT_ITEM_OK;
+}
+
+int ora_gather_install_snapshot_args(ora_engine *e, const int32_t *slots, const int32_t *peers,
+                                     int64_t n, mraft_is_args *out, int32_t *item_err) {
+  int64_t gp = (int64_t)e->G * e->P;
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&out[i], 0, sizeof(out[i]));
+    out[i].slot = -1;
+    if (slots[i] < 0 || slots[i] >= gp) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
+    item_err[i] = gather_is_one(e, slots[i], peers[i], &out[i]);
+  }
+  return MRAFT_OK;
+}
+
+/* HandleInstallSnapshot, raft_snapshot.go:15-54 */
+static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, mraft_is_reply *r,
+                             int *installed) {
+  const int64_t row = (int64_t)f * e->L;
+  *installed = 0;
+  r->success = 0;
+  r->term = 0;
+  /* sliceFrom(LastIncludedIndex) below the follower's own dummy panics in Go
+   * (raft_log.go:56-58): rejected before any mutation. */
+  if (a->term >= S.current_term[f] && a->last_included_index > S.commit_index[f] &&
+      a->last_included_index <= S.last_index[f] && a->last_included_index < S.dummy_index[f])
+    return MRAFT_ITEM_BELOW_DUMMY;
+  CR(A_TERM, f);
+  if (a->term < S.current_term[f]) {                                  /* :20-22 */
+    r->term = S.current_term[f];                                      /* deferred :17-19 */
+    return MRAFT_ITEM_OK;
+  }
+  if (a->term > S.current_term[f]) {                                  /* :23-26 */
+    S.current_term[f] = a->term; S.voted_for[f] = -1;
+    CW(A_TERM, f); CW(A_VOTED, f);
+  }
+  S.state[f] = MRAFT_FOLLOWER;                                        /* :28 */
+  CW(A_ROLE, f);
+  r->term = S.current_term[f];
+  CR(A_COMMIT, f);
+  const int32_t lii = a->last_included_index;
+  if (lii <= S.commit_index[f]) return MRAFT_ITEM_OK;                 /* :31-33 outdated */
+  CR(A_LAST, f);
+  if (lii > S.last_index[f]) {                                        /* :35-37 */
+    S.log_term[row] = a->last_included_term;
+    S.last_index[f] = lii;
+    S.dummy_index[f] = lii;
+    CW(A_LOG, row); CW(A_LAST, f);
+  } else {                                                            /* :38-40 */
+    CR(A_DUMMY, f);
+    slice_from(e, f, lii);
+    S.log_term[row] = a->last_included_term;                          /* :45 setDummyTerm */
+  }
+  S.commit_index[f] = lii;                                            /* :42 */
+  S.last_applied[f] = lii;                                            /* :43 */
+  CW(A_DUMMY, f); CW(A_COMMIT, f); CW(A_APPLIED, f);
+  *installed = 1;                                                     /* :49-50 hasSnapshot */
+  return MRAFT_ITEM_OK;
+}
+
+int ora_handle_install_snapshot(ora_engine *e, const mraft_is_args *args, int64_t n,
+                                mraft_is_reply *replies, int32_t *out_flags, int32_t *item_err) {
+  int32_t *first = claim_slots(e, &args[0].slot, n, sizeof(mraft_is_args), item_err);
+  for (int64_t i = 0; i < n; ++i) {
+    memset(&replies[i], 0, sizeof(replies[i]));
+    out_flags[i] = 0;
+    if (item_err[i]) continue;
+    int inst = 0;
+    item_err[i] = handle_is_one(e, args[i].slot, &args[i], &replies[i], &inst);
+    if (inst) out_flags[i] = MRAFT_F_SNAPSHOT_INSTALLED;
+  }
+  free(first);
+  return MRAFT_OK;
+}
+
+/* processInstallSnapshotReply, raft_snapshot.go:56-69 */
+static int32_t process_is_reply_one(ora_engine *e, int32_t slot, int32_t peer, int32_t args_term,
+                                    int32_t lii, int32_t reply_term) {
+  const int64_t pi = (int64_t)slot * e->P + peer;
+  int32_t fl = 0;
+  if (reply_term > S.current_term[slot]) {                            /* :59-64 */
+    S.current_term[slot] = reply_term;
+    S.voted_for[slot] = -1;
+    S.state[slot] = MRAFT_FOLLOWER;
+    CW(A_TERM, slot); CW(A_VOTED, slot); CW(A_ROLE, slot);
+    fl |= MRAFT_F_STEPPED_DOWN;
+  } else if (S.state[slot] == MRAFT_LEADER && args_term == S.current_term[slot]) {  /* :65 */
+    S.match_index[pi] = lii;                                          /* :66 */
+    S.next_index[pi] = lii + 1;                                       /* :67 */
+    CW(A_MATCH, pi); CW(A_NEXT, pi);
+    fl |= MRAFT_F_APPLIED;
+  }
+  return fl;
+}
+
+int ora_process_install_snapshot_replies(ora_engine *e, const mraft_is_result *items, int64_t n,
+                                         const int64_t *seg_begin, int64_t n_seg,
+                                         int32_t *out_flags, int32_t *item_err) {
+  const int32_t P = e->P;
+  int64_t gp = (int64_t)e->G * P;
+  int64_t ns = seg_begin ? n_seg : n;
+  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
+  for (int64_t sg = 0; sg < ns; ++sg) {
+    int64_t b = seg_begin ? seg_begin[sg] : sg, en = seg_begin ? seg_begin[sg + 1] : sg + 1;
+    if (b >= en) continue;
+    int32_t slot = items[b].slot, bad = 0;
+    if (slot < 0 || slot >= gp) bad = MRAFT_ITEM_BAD_SLOT;
+    else if (seen[slot]) bad = MRAFT_ITEM_DUP_SLOT;
+    else
+      for (int64_t i = b; i < en; ++i)
+        if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
+            items[i].peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+    if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
+    seen[slot] = 1;
+    for (int64_t i = b; i < en; ++i)
+      out_flags[i] = process_is_reply_one(e, slot, items[i].peer, items[i].args_term,
+                                          items[i].args_last_included_index, items[i].reply_term);
+  }
+  free(seen);
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Fused tick = for each group: a3 for every peer, a4 at every follower, a2   */
 /* (+a1) at the leader in peer order.                                         */
 /* ------------------------------------------------------------------------ */
@@ -406,12 +576,12 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
     if (group_flags) group_flags[g] = MRAFT_G_ERROR;
     return;
   }
-  int32_t ok[8] = {0};
+  int32_t ok[8] = {0};  /* 1: AppendEntries, 2: InstallSnapshot */
   for (int32_t p = 0; p < P; ++p) {
     if (p == lp) continue;
     CR(A_NEXT, (int64_t)ld * P + p);
     int32_t prev = S.next_index[(int64_t)ld * P + p] - 1;
-    if (prev < S.dummy_index[ld]) flags |= MRAFT_G_NEED_SNAPSHOT;
+    if (prev < S.dummy_index[ld]) { flags |= MRAFT_G_NEED_SNAPSHOT; ok[p] = 2; }
     else if (prev > S.last_index[ld]) flags |= MRAFT_G_ERROR;
     else ok[p] = 1;
   }
@@ -423,8 +593,22 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
 
   mraft_ae_args args[8];
   mraft_ae_reply rep[8];
+  mraft_is_args isa[8];
+  mraft_is_reply isr[8];
   int32_t have[8] = {0};
   for (int32_t p = 0; p < P; ++p) {
+    if (ok[p] == 2) {                                                 /* InstallSnapshot */
+      gather_is_one(e, ld, p, &isa[p]);
+      CR(A_LOG, (int64_t)ld * e->L);                                  /* dummyTerm */
+      int inst = 0;
+      if (handle_is_one(e, g * P + p, &isa[p], &isr[p], &inst)) {
+        flags |= MRAFT_G_FOLLOWER_PANIC;                              /* message dropped */
+        continue;
+      }
+      if (inst) flags |= MRAFT_G_SNAPSHOT_INSTALLED;
+      have[p] = 2;
+      continue;
+    }
     if (!ok[p]) continue;
     gather_one(e, ld, p, &args[p]);                                   /* a3 */
     int32_t prev = args[p].prev_log_index;
@@ -443,15 +627,20 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
   int32_t term0 = S.current_term[ld];
   int32_t mstar = INT32_MIN;
   int any_eval = 0;
-  for (int32_t p = 0; p < P; ++p) {                                   /* a2 (+a1) */
+  for (int32_t p = 0; p < P; ++p) {                                   /* fold, peer order */
     if (!have[p]) continue;
-    int32_t ms = INT32_MIN;
-    int32_t fl = process_reply_one(e, ld, p, args[p].term, args[p].prev_log_index,
-                                   args[p].n_entries, rep[p].term, rep[p].success,
-                                   rep[p].conflict_index, cnt.on ? &ms : NULL);
-    if ((fl & MRAFT_F_APPLIED) && rep[p].success) {
-      any_eval = 1;
-      if (ms > mstar) mstar = ms;
+    int32_t fl;
+    if (have[p] == 2) {
+      fl = process_is_reply_one(e, ld, p, isa[p].term, isa[p].last_included_index, isr[p].term);
+    } else {
+      int32_t ms = INT32_MIN;
+      fl = process_reply_one(e, ld, p, args[p].term, args[p].prev_log_index,
+                             args[p].n_entries, rep[p].term, rep[p].success,
+                             rep[p].conflict_index, cnt.on ? &ms : NULL);
+      if ((fl & MRAFT_F_APPLIED) && rep[p].success) {
+        any_eval = 1;
+        if (ms > mstar) mstar = ms;
+      }
     }
     if (fl & MRAFT_F_STEPPED_DOWN) flags |= MRAFT_G_STEPPED_DOWN;
   }

@@ -65,6 +65,16 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
               int32_t *out_is_leader, int32_t *item_err);
 int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to);
 
+int ora_snapshot(ora_engine *e, const int32_t *slots, const int32_t *index, int64_t n,
+                 int32_t *item_err);
+int ora_gather_install_snapshot_args(ora_engine *e, const int32_t *slots, const int32_t *peers,
+                                     int64_t n, mraft_is_args *out, int32_t *item_err);
+int ora_handle_install_snapshot(ora_engine *e, const mraft_is_args *args, int64_t n,
+                                mraft_is_reply *replies, int32_t *out_flags, int32_t *item_err);
+int ora_process_install_snapshot_replies(ora_engine *e, const mraft_is_result *items, int64_t n,
+                                         const int64_t *seg_begin, int64_t n_seg,
+                                         int32_t *out_flags, int32_t *item_err);
+
 int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
                        mraft_rv_args *out_args, int32_t *item_err);
 int ora_handle_request_vote(ora_engine *e, const mraft_rv_args *args,

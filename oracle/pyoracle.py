@@ -25,6 +25,8 @@ LEADER, CANDIDATE, FOLLOWER = 1, 2, 3  # raft_rpc.go:8-12
 ITEM_OK, PREV_BEYOND_LAST, BELOW_DUMMY, LOG_FULL, NEED_SNAPSHOT, DUP_SLOT, BAD_SLOT, BAD_STATE = range(8)
 F_NEED_MORE, F_COMMITTED, F_STEPPED_DOWN, F_BECAME_LEADER, F_APPLIED = 1, 2, 4, 8, 16
 G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT, G_LOG_FULL = 1, 2, 4, 8, 16, 32, 64
+G_ELECTED, G_SNAPSHOT_INSTALLED, G_FOLLOWER_PANIC = 128, 256, 512
+F_SNAPSHOT_INSTALLED = 32
 
 
 class Panic(Exception):
@@ -61,6 +63,20 @@ class RequestVoteArgs:  # raft_rpc.go:71-76
     Term: int
     LastLogIndex: int
     LastLogTerm: int
+
+
+@dataclass
+class InstallSnapshotArgs:  # raft_rpc.go:84-90 (Snapshot bytes omitted)
+    Term: int
+    LeaderId: int
+    LastIncludedIndex: int
+    LastIncludedTerm: int
+
+
+@dataclass
+class InstallSnapshotReply:  # raft_rpc.go:92-95
+    Term: int = 0
+    Success: bool = False
 
 
 @dataclass
@@ -109,6 +125,9 @@ class RaftLog:  # raft_log.go:3-104
 
     def len(self):
         return len(self.logs)
+
+    def setLogs(self, newlogs):  # raft_log.go:18-21 (copy)
+        self.logs = [Entry(e.Index, e.Term) for e in newlogs]
 
     def matchLog(self, Term, Index):
         return Index <= self.lastIndex() and Term == self.getEntry(Index).Term
@@ -218,6 +237,53 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             follower_commit = True
         reply.Term, reply.Success = self.currentTerm, True
         return follower_commit
+
+    # ---- raft_snapshot.go ----
+    def Snapshot(self, index):  # :3-13
+        if index <= self.raftLog.dummyIndex():
+            return ITEM_OK
+        if index > self.raftLog.lastIndex():
+            return PREV_BEYOND_LAST  # sliceFrom panics
+        self.raftLog.setLogs(self.raftLog.sliceFrom(index))
+        return ITEM_OK
+
+    def gatherInstallSnapshot(self):  # raft_append_entry.go:27-34
+        return InstallSnapshotArgs(Term=self.currentTerm, LeaderId=self.me,
+                                   LastIncludedIndex=self.raftLog.dummyIndex(),
+                                   LastIncludedTerm=self.raftLog.dummyTerm())
+
+    def HandleInstallSnapshot(self, args, reply):  # :15-54
+        try:
+            if args.Term < self.currentTerm:
+                return False
+            if args.Term > self.currentTerm:
+                self.currentTerm, self.votedFor = args.Term, -1
+            self.state = FOLLOWER
+            if args.LastIncludedIndex <= self.commitIndex:
+                return False
+            if args.LastIncludedIndex > self.raftLog.lastIndex():
+                self.raftLog.setLogs([Entry(0, 0)])
+            else:
+                self.raftLog.setLogs(self.raftLog.sliceFrom(args.LastIncludedIndex))
+            self.commitIndex = args.LastIncludedIndex
+            self.lastApplied = args.LastIncludedIndex
+            self.raftLog.logs[0].Index = args.LastIncludedIndex
+            self.raftLog.logs[0].Term = args.LastIncludedTerm
+            return True
+        finally:
+            reply.Term = self.currentTerm
+
+    def processInstallSnapshotReply(self, peer, args, reply):  # :56-69
+        if reply.Term > self.currentTerm:
+            self.currentTerm = reply.Term
+            self.votedFor = -1
+            self.state = FOLLOWER
+            return F_STEPPED_DOWN
+        if self.state == LEADER and args.Term == self.currentTerm:
+            self.matchIndex[peer] = args.LastIncludedIndex
+            self.nextIndex[peer] = args.LastIncludedIndex + 1
+            return F_APPLIED
+        return 0
 
     # ---- raft_election.go ----
     def StartElection(self):  # :4-15
@@ -330,13 +396,14 @@ def replicate_tick(st: dict, G: int, P: int, L: int, leader_peer) -> tuple:
             gflags[g] = G_ERROR
             continue
         flags = 0
-        ok = {}
+        ok, snap = {}, {}
         for p in range(P):
             if p == lp:
                 continue
             args, err = ld.gatherArgs(p)
             if err == NEED_SNAPSHOT:
                 flags |= G_NEED_SNAPSHOT
+                snap[p] = ld.gatherInstallSnapshot()
             elif err == PREV_BEYOND_LAST:
                 flags |= G_ERROR
             else:
@@ -345,8 +412,20 @@ def replicate_tick(st: dict, G: int, P: int, L: int, leader_peer) -> tuple:
             gflags[g] = G_ERROR | (flags & G_NEED_SNAPSHOT)
             continue
         flags |= G_ACTIVE
-        replies = {}
-        for p, args in ok.items():
+        replies, isreplies = {}, {}
+        for p in range(P):
+            if p in snap:
+                rep = InstallSnapshotReply()
+                if _is_would_panic(rafts[g * P + p], snap[p]):
+                    flags |= G_FOLLOWER_PANIC
+                    continue
+                if rafts[g * P + p].HandleInstallSnapshot(snap[p], rep):
+                    flags |= G_SNAPSHOT_INSTALLED
+                isreplies[p] = rep
+                continue
+            if p not in ok:
+                continue
+            args = ok[p]
             fr = rafts[g * P + p]
             if _would_overflow(fr, args, L):
                 flags |= G_LOG_FULL
@@ -357,14 +436,26 @@ def replicate_tick(st: dict, G: int, P: int, L: int, leader_peer) -> tuple:
                 flags |= G_FOLLOWER_COMMIT
             replies[p] = reply
         c0 = ld.commitIndex
-        for p in sorted(replies):
-            fl = ld.processAppendEntriesReply(p, ok[p], replies[p])
+        for p in range(P):
+            if p in isreplies:
+                fl = ld.processInstallSnapshotReply(p, snap[p], isreplies[p])
+            elif p in replies:
+                fl = ld.processAppendEntriesReply(p, ok[p], replies[p])
+            else:
+                continue
             if fl & F_STEPPED_DOWN:
                 flags |= G_STEPPED_DOWN
         if ld.commitIndex != c0:
             flags |= G_COMMITTED
         gflags[g] = flags
     return to_soa(rafts, st, G, P, L), gflags
+
+
+def _is_would_panic(fr: Raft, a: InstallSnapshotArgs) -> bool:
+    """HandleInstallSnapshot's sliceFrom below the follower's dummy (Go panic)."""
+    lg = fr.raftLog
+    return (a.Term >= fr.currentTerm and a.LastIncludedIndex > fr.commitIndex and
+            a.LastIncludedIndex <= lg.lastIndex() and a.LastIncludedIndex < lg.dummyIndex())
 
 
 def _would_overflow(fr: Raft, args: AppendEntriesArgs, L: int) -> bool:

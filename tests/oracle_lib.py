@@ -7,8 +7,8 @@ import os
 
 import numpy as np
 
-from multiraft_amd._abi import (AE_ARGS, AE_REPLY, AE_RESULT, RV_ARGS, RV_REPLY, RV_RESULT,
-                                MraftSoa, ptr, soa_of)
+from multiraft_amd._abi import (AE_ARGS, AE_REPLY, AE_RESULT, IS_ARGS, IS_REPLY, IS_RESULT,
+                                RV_ARGS, RV_REPLY, RV_RESULT, MraftSoa, ptr, soa_of)
 from multiraft_amd.engine import copy_state
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -43,6 +43,10 @@ def lib():
             "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
             "ora_export_group_status": [E, vp, vp, vp],
             "ora_election_rounds": [E, vp, i32, vp],
+            "ora_snapshot": [E, vp, vp, i64, vp],
+            "ora_gather_install_snapshot_args": [E, vp, vp, i64, vp, vp],
+            "ora_handle_install_snapshot": [E, vp, i64, vp, vp, vp],
+            "ora_process_install_snapshot_replies": [E, vp, i64, vp, i64, vp, vp],
         }
         for n, a in sigs.items():
             f = getattr(l, n)
@@ -132,6 +136,42 @@ class Oracle:
 
     def store_state(self):
         return copy_state(self.st)
+
+    # ---- snapshots ---------------------------------------------------------
+    def snapshot(self, slots, index):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        index = np.ascontiguousarray(index, dtype=np.int32)
+        err = np.zeros(len(slots), np.int32)
+        lib().ora_snapshot(ctypes.byref(self._e), ptr(slots), ptr(index), len(slots), ptr(err))
+        return err
+
+    def gather_install_snapshot_args(self, slots, peers):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        peers = np.ascontiguousarray(peers, dtype=np.int32)
+        n = len(slots)
+        out = np.zeros(n, dtype=IS_ARGS)
+        err = np.zeros(n, np.int32)
+        lib().ora_gather_install_snapshot_args(ctypes.byref(self._e), ptr(slots), ptr(peers), n, ptr(out), ptr(err))
+        return out, err
+
+    def handle_install_snapshot(self, args):
+        args = np.ascontiguousarray(args, dtype=IS_ARGS)
+        n = len(args)
+        rep = np.zeros(n, dtype=IS_REPLY)
+        fl = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        lib().ora_handle_install_snapshot(ctypes.byref(self._e), ptr(args), n, ptr(rep), ptr(fl), ptr(err))
+        return rep, fl, err
+
+    def process_install_snapshot_replies(self, items, seg_begin=None):
+        items = np.ascontiguousarray(items, dtype=IS_RESULT)
+        n = len(items)
+        fl = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        sb = None if seg_begin is None else np.ascontiguousarray(seg_begin, dtype=np.int64)
+        lib().ora_process_install_snapshot_replies(ctypes.byref(self._e), ptr(items), n, ptr(sb),
+                                                   0 if sb is None else len(sb) - 1, ptr(fl), ptr(err))
+        return fl, err
 
     def start_election(self, slots):
         slots = np.ascontiguousarray(slots, dtype=np.int32)

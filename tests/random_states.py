@@ -10,7 +10,12 @@ import numpy as np
 from multiraft_amd.engine import new_state
 
 
-def random_tick_state(rng: np.random.Generator, G: int, P: int, L: int, monotone: bool = False):
+def random_tick_state(rng: np.random.Generator, G: int, P: int, L: int, monotone: bool = False,
+                      snap: bool = False):
+    """snap=True: snapshot-heavy variant — leader dummies up to L/2 and half of
+    the nextIndex values at or below the leader dummy, so the fused tick's
+    InstallSnapshot branch (stale, outdated, install by new log or by slice,
+    dropped-on-panic) is hit in most groups."""
     st = new_state(G, P, L)
     lt = st["log_term"].reshape(G * P, L)
     lp = rng.integers(0, P, size=G).astype(np.int32)
@@ -18,6 +23,8 @@ def random_tick_state(rng: np.random.Generator, G: int, P: int, L: int, monotone
         ld = g * P + lp[g]
         alpha = int(rng.integers(2, 6))
         ldummy = int(rng.integers(0, 4)) if rng.random() < 0.3 else 0
+        if snap:
+            ldummy = int(rng.integers(0, max(2, L // 2)))
         llen = L if rng.random() < 0.3 else int(rng.integers(1, L + 1))  # slots used
         base = rng.integers(0, alpha, size=llen)
         if monotone:
@@ -40,6 +47,8 @@ def random_tick_state(rng: np.random.Generator, G: int, P: int, L: int, monotone
             u = rng.random()
             fd = ldummy if u < 0.7 else (int(rng.integers(0, 6)) if u < 0.85
                                          else max(0, ldummy - 1 - int(rng.integers(0, 2))))
+            if snap:
+                fd = int(rng.integers(0, ldummy + 3))
             # follower = leader prefix (from fd) + random tail
             share = int(rng.integers(0, max(1, lastl - fd + 2)))
             flen = min(L, max(1, share + int(rng.integers(0, 6))))
@@ -60,8 +69,12 @@ def random_tick_state(rng: np.random.Generator, G: int, P: int, L: int, monotone
             st["voted_for"][f] = int(rng.integers(-1, P))
             st["state"][f] = int(rng.integers(1, 4))
             st["commit_index"][f] = int(rng.integers(fd, fd + flen))
+            if snap and rng.random() < 0.15:
+                st["commit_index"][f] = fd - 1 - int(rng.integers(0, 2))   # commit < dummy
             nxt = int(rng.integers(ldummy - 1, lastl + 3)) if rng.random() < 0.1 else \
                 int(rng.integers(ldummy + 1, lastl + 2))
+            if snap and rng.random() < 0.5:
+                nxt = int(rng.integers(max(0, ldummy - 4), ldummy + 1))
             st["next_index"][ld * P + p] = nxt
             st["match_index"][ld * P + p] = int(rng.integers(0, lastl + 2))
     st["last_applied"][:] = st["commit_index"]

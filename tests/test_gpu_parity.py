@@ -183,6 +183,24 @@ def test_tick_random_adversarial_gpu(P, L, mono):
         assert_states_equal(e.store_state(), o.state(), G, P, L, "adversarial tick")
 
 
+@pytest.mark.parametrize("P,L", [(2, 8), (3, 16), (5, 12), (5, 256), (8, 40), (5, 1024)])
+def test_tick_snapshot_heavy_gpu(P, L):
+    """InstallSnapshot inside the fused tick: stale, outdated, new-log and
+    sliced installs, dropped-on-panic items, and the fold's match/next update."""
+    from random_states import random_tick_state
+    rng = np.random.default_rng(2500 + P * 100 + L)
+    G = 700
+    st, lp = random_tick_state(rng, G, P, L, snap=True)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        assert e.replicate_tick_count(lp) == o.replicate_tick_count(lp)
+        gf = e.replicate_tick(lp)
+        ogf = o.replicate_tick(lp)
+        assert np.array_equal(gf, ogf)
+        assert (ogf & 256).any()
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "snapshot-heavy tick")
+
+
 @pytest.mark.parametrize("P,R", [(3, 16), (5, 8), (7, 64), (8, 5), (2, 7), (1, 3)])
 def test_election_rounds_gpu(P, R):
     from multiraft_amd import synth_election_state
@@ -193,3 +211,20 @@ def test_election_rounds_gpu(P, R):
         gf = e.election_rounds(mask)
         assert np.array_equal(gf, o.election_rounds(mask))
         assert_states_equal(e.store_state(), o.state(), G, P, L, "election rounds")
+
+
+@pytest.mark.parametrize("P,L", [(3, 16), (5, 12), (7, 32), (5, 300)])
+def test_snapshot_install_gpu(P, L):
+    from random_states import random_tick_state
+    from snapshot_cases import run_snapshot_scenario
+    G = 400
+    rng = np.random.default_rng(700 + P + L)
+    st, lp = random_tick_state(rng, G, P, L)
+    lp = np.where((lp >= 0) & (lp < P), lp, 0).astype(np.int32)
+    o = Oracle(G, P, L, st)
+    oo = run_snapshot_scenario(o, st, G, P, L, lp, seed=9)
+    with _engine(G, P, L, st) as e:
+        go = run_snapshot_scenario(e, st, G, P, L, lp, seed=9)
+        for k in oo:
+            assert np.array_equal(go[k], oo[k]), k
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "snapshot scenario")

@@ -238,6 +238,22 @@ def test_tick_random_adversarial_c_vs_py(P, L, mono):
         assert (gf & bit).any() or bit in (8, 64), bit
 
 
+@pytest.mark.parametrize("P,L", [(2, 8), (3, 16), (5, 12), (5, 256), (8, 40)])
+def test_tick_snapshot_heavy_c_vs_py(P, L):
+    """Fused tick with the InstallSnapshot branch in most groups
+    (raft_append_entry.go:27-34 -> raft_snapshot.go:15-69)."""
+    from random_states import random_tick_state
+    rng = np.random.default_rng(1500 + P * 100 + L)
+    G = 300
+    st, lp = random_tick_state(rng, G, P, L, snap=True)
+    o = Oracle(G, P, L, st)
+    gf = o.replicate_tick(lp)
+    pst, pgf = po.replicate_tick(st, G, P, L, lp)
+    assert np.array_equal(gf, pgf)
+    assert_states_equal(o.state(), pst, G, P, L, "snapshot-heavy tick")
+    assert (gf & 8).any() and (gf & 256).any()
+
+
 def _py_election_rounds(st, G, P, L, mask):
     rafts = po.from_soa(st, G, P, L)
     gf = np.zeros(G, np.int32)
@@ -275,3 +291,55 @@ def test_election_rounds_c_vs_py(P):
     assert np.array_equal(gf, pgf)
     assert_states_equal(o.state(), pst, G, P, L, "election rounds")
     assert (gf & 128).any() and (gf & 4).any()
+
+
+def _py_snapshot_scenario(st, G, P, L, lp, seed):
+    """The same scenario on the Python restatement (object model)."""
+    from multiraft_amd._abi import IS_ARGS
+    rng = np.random.default_rng(seed)
+    rafts = po.from_soa(st, G, P, L)
+    last, dummy = st["last_index"], st["dummy_index"]
+    idx = np.minimum(dummy + rng.integers(-1, 6, size=G * P), last).astype(np.int32)
+    bump = rng.random(G * P) < 0.05
+    idx[bump] = last[bump] + 1  # index > lastIndex: sliceFrom panics in Go
+    snap_err = np.array([rafts[s].Snapshot(int(idx[s])) for s in range(G * P)], np.int32)
+    pairs = [(g * P + lp[g], p) for g in range(G) for p in range(P) if p != lp[g] and lp[g] >= 0]
+    args = {}
+    for (ld, p) in pairs:
+        rf = rafts[ld]
+        if rf.state == po.LEADER and rf.nextIndex[p] - 1 < rf.raftLog.dummyIndex():
+            args[(ld, p)] = rf.gatherInstallSnapshot()
+    reps, fls, errs = {}, {}, {}
+    for (ld, p), a in args.items():
+        rep = po.InstallSnapshotReply()
+        fr = rafts[(ld // P) * P + p]
+        if po._is_would_panic(fr, a):
+            errs[(ld, p)] = 2
+            reps[(ld, p)], fls[(ld, p)] = rep, 0
+            continue
+        inst = fr.HandleInstallSnapshot(a, rep)
+        errs[(ld, p)] = 0
+        reps[(ld, p)], fls[(ld, p)] = rep, (32 if inst else 0)
+    prfl = []
+    for (ld, p) in sorted([k for k in args if errs[k] == 0], key=lambda t: t[0]):
+        prfl.append(rafts[ld].processInstallSnapshotReply(p, args[(ld, p)], reps[(ld, p)]))
+    return snap_err, po.to_soa(rafts, st, G, P, L), [fls[k] for k in args], prfl, [errs[k] for k in args]
+
+
+@pytest.mark.parametrize("P,L", [(3, 16), (5, 12), (7, 32)])
+def test_snapshot_install_c_vs_py(P, L):
+    from random_states import random_tick_state
+    from snapshot_cases import run_snapshot_scenario
+    G = 200
+    rng = np.random.default_rng(500 + P)
+    st, lp = random_tick_state(rng, G, P, L)
+    lp = np.where((lp >= 0) & (lp < P), lp, 0).astype(np.int32)
+    o = Oracle(G, P, L, st)
+    out = run_snapshot_scenario(o, st, G, P, L, lp, seed=7)
+    snap_err, pst, fls, prfl, errs = _py_snapshot_scenario(st, G, P, L, lp, seed=7)
+    assert np.array_equal(out["snap_err"], snap_err)
+    assert out["is_fl"].tolist() == fls
+    assert out["is_herr"].tolist() == errs
+    assert out["pr_fl"].tolist() == prfl
+    assert_states_equal(o.state(), pst, G, P, L, "snapshot scenario")
+    assert (out["is_fl"] == 32).any() and (snap_err == 1).any()

@@ -1,25 +1,26 @@
 #!/bin/bash
 # Builds tick-kernel tuning variants as tools/variants/libmraft_hip_<tag>.so
 # (same sources, different compile-time knobs); tools/tune.sh times them.
-# spec = V:MINW:VC:XCD
+# spec = V:MINW:VC:XCD:NT
 set -e
 cd "$(dirname "$0")/../multiraft_amd/csrc"
 mkdir -p ../../tools/variants
 rm -f ../../tools/variants/*.so
 for spec in "$@"; do
-  IFS=: read V W VC X <<< "$spec"
-  tag="v${V}w${W}c${VC}x${X}"
+  IFS=: read V W VC X NT <<< "$spec"
+  NT=${NT:-3}
+  tag="v${V}w${W}c${VC}x${X}n${NT}"
   mkdir -p build_$tag
   for f in mraft_abi mraft_kernels mraft_tick mraft_elect; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
-      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X \
+      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X -DMRAFT_TICK_NT=$NT \
       -c $f.hip -o build_$tag/$f.o 2>/dev/null &
   done
   wait
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o
   rm -rf build_$tag
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
-      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X \
+      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X -DMRAFT_TICK_NT=$NT \
       -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
       grep -A9 "k_tick_groupILi5ELb0" | grep -E "VGPRs:|Scratch" | sed -E "s/.*(VGPRs|ScratchSize)[^:]*: ([0-9]+).*/\1=\2/" | tr "\n" " "; echo
 done

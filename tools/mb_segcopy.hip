@@ -47,6 +47,37 @@ __global__ void seqcopy4(const int4 *__restrict__ a, int4 *__restrict__ b, long 
     for (int u = 0; u < 4; ++u) { long i = t + u * 256 + threadIdx.x; if (i < n4) b[i] = v[u]; }
   }
 }
+// Same with non-temporal loads and/or stores.
+template <bool NTL, bool NTS>
+__global__ void seqcopy4nt(const int4 *__restrict__ a, int4 *__restrict__ b, long n4) {
+  for (long t = (long)blockIdx.x * 1024; t < n4; t += (long)gridDim.x * 1024) {
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      long i = t + u * 256 + threadIdx.x;
+      if (i < n4) {
+        if (NTL) {
+          v[u].x = __builtin_nontemporal_load(&a[i].x); v[u].y = __builtin_nontemporal_load(&a[i].y);
+          v[u].z = __builtin_nontemporal_load(&a[i].z); v[u].w = __builtin_nontemporal_load(&a[i].w);
+        } else {
+          v[u] = a[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      long i = t + u * 256 + threadIdx.x;
+      if (i < n4) {
+        if (NTS) {
+          __builtin_nontemporal_store(v[u].x, &b[i].x); __builtin_nontemporal_store(v[u].y, &b[i].y);
+          __builtin_nontemporal_store(v[u].z, &b[i].z); __builtin_nontemporal_store(v[u].w, &b[i].w);
+        } else {
+          b[i] = v[u];
+        }
+      }
+    }
+  }
+}
 __global__ void seqread4(const int4 *__restrict__ a, int *__restrict__ out, long n4) {
   int acc = 0;
   for (long t = (long)blockIdx.x * 1024; t < n4; t += (long)gridDim.x * 1024) {
@@ -95,6 +126,15 @@ int main() {
   run("segcopy VC=4", [&] { hipLaunchKernelGGL(segcopy<4>, dim3(blocks), dim3(256), 0, 0, log, seg, (int)G); }, bytes);
   const long n4 = (long)(bytes / 2 / 16);
   run("sequential copy same bytes", [&] { hipLaunchKernelGGL(seqcopy, dim3(8192), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+  for (int grid : {4096, 16384}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "copy x4 nt-store grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL((seqcopy4nt<false, true>), dim3(grid), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+    snprintf(nm, sizeof nm, "copy x4 nt-load grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL((seqcopy4nt<true, false>), dim3(grid), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+    snprintf(nm, sizeof nm, "copy x4 nt-both grid %d", grid);
+    run(nm, [&] { hipLaunchKernelGGL((seqcopy4nt<true, true>), dim3(grid), dim3(256), 0, 0, (const int4 *)log, (int4 *)(log + 4 * n4 + 1024), n4); }, (double)n4 * 32);
+  }
   for (int grid : {2048, 4096, 8192, 16384}) {
     char nm[64];
     snprintf(nm, sizeof nm, "copy x4 grid %d", grid);
