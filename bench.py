@@ -46,6 +46,16 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     """The CPU oracle (C restatement of the Go control flow, incl. the
     per-message entries copy of raft_append_entry.go:50-54 and a1's downward
@@ -72,12 +82,36 @@ def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     vt, dt, stt = run(threads, budget_s)
     log(rank, f"cpu baseline: {vt:.4g} decisions/s on {threads} threads, {v1:.4g} on 1 thread")
     return {"value": vt, "unit": "decisions/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "compiler": "gcc -O3 -march=x86-64-v3 (oracle/Makefile)",
             "sample": (f"oracle/mraft_oracle.c replicate_tick over groups 0..{Gs - 1} of the same "
                        f"seeded config-#3 workload ({P} peers, L={L}), fresh state per pass, "
                        f"{d1 // Gs + dt // Gs} passes; {threads} threads: {dt} decisions in {stt:.2f} s; "
                        f"1 thread: {v1:.4g} decisions/s; excludes gob persist()/labrpc encoding "
                        f"the Go reference also pays per handler"),
             "single_thread_value": v1}
+
+
+def permute_groups(st, lp, G, P, L, how):
+    """Dispatch-order experiment: the same groups in another order. lpt-xcd
+    sorts each XCD's contiguous range (the tick's XCD-aware mapping) by
+    descending estimated work (entries past each follower's prev)."""
+    ld = np.arange(G) * P + lp
+    last = st["last_index"][ld].astype(np.int64)
+    nxt = st["next_index"].reshape(G * P, P)[ld]
+    work = np.clip(last[:, None] + 1 - nxt, 0, None).sum(axis=1)
+    if how == "random":
+        perm = np.random.default_rng(0).permutation(G)
+    else:
+        per = G // 8
+        perm = np.concatenate([x * per + np.argsort(-work[x * per:(x + 1) * per], kind="stable")
+                               for x in range(8)] + [np.arange(8 * per, G)])
+    out = {}
+    for k, v in st.items():
+        w = v.size // G
+        out[k] = np.ascontiguousarray(v.reshape(G, w)[perm].reshape(-1))
+    # the leader's matchIndex/nextIndex rows are per replica; leader_peer per group
+    return out, np.ascontiguousarray(lp[perm])
 
 
 def main():
@@ -91,6 +125,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--group-order", default="natural", choices=["natural", "lpt-xcd", "random"],
+                    help="experiment: permute the groups (same work, different dispatch order)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (CPU rehearsal)")
     args = ap.parse_args()
@@ -122,6 +158,8 @@ def main():
     st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=rank * G, g_end=(rank + 1) * G,
                                  nthreads=min(16, os.cpu_count() or 1))
     log(rank, f"generated {G}x{P}x{L} state in {time.perf_counter() - t:.1f}s")
+    if args.group_order != "natural":
+        st, lp = permute_groups(st, lp, G, P, L, args.group_order)
 
     # Ranks allocate in turn (a CPU rehearsal may put several ranks on one GPU).
     for r in range(world):
@@ -191,6 +229,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     ker_ms = [a.elapsed_time(b) for a, b in ev]
+    log(rank, "tick kernel ms per step: " + " ".join(f"{x:.3f}" for x in ker_ms))
     flags = gf_d.cpu().numpy()
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if on_host else dev)

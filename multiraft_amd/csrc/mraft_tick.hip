@@ -80,7 +80,7 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 #ifndef MRAFT_TICK_NT
-#define MRAFT_TICK_NT 1    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
+#define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
 #endif
 
 // Streaming (read-once / write-once) log accesses of the pass.
@@ -414,6 +414,12 @@ struct Fold {
 #ifndef MRAFT_TICK_VC
 #define MRAFT_TICK_VC 1    // dwordx4 vectors per lane in the copy-only loop
 #endif
+#ifndef MRAFT_TICK_EXP
+#define MRAFT_TICK_EXP 0   // traffic experiments only (wrong results): 1 = no pass, 2 = no pass, no scans
+#endif
+#ifndef MRAFT_TICK_ALIGN
+#define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
+#endif
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
@@ -542,6 +548,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   int scan_extra = 0;
   {
     unsigned long long m = __ballot(icls == IC_SCAN);
+    if (MRAFT_TICK_EXP == 2) m = 0;
     while (m) {
       const int src = first_lane(m);
       m &= m - 1;
@@ -611,12 +618,12 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
     }
   }
   int fullmask = 0, found = -1;
-  if (merge_m || slo <= shi) {
+  if (MRAFT_TICK_EXP == 0 && (merge_m || slo <= shi)) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
     constexpr int VC = MRAFT_TICK_VC;
     if (vec) {
-      int c = plo - (int)((eo + plo) & 3);
+      int c = plo - (int)((eo + plo) & (MRAFT_TICK_ALIGN - 1));
       for (; c <= phi; c += 256 * V) {
         bool cmp = false;
 #pragma unroll

@@ -1,26 +1,23 @@
 #!/bin/bash
-# Builds tick-kernel tuning variants as tools/variants/libmraft_hip_<tag>.so
-# (same sources, different compile-time knobs); tools/tune.sh times them.
-# spec = V:MINW:VC:XCD:NT
+# Builds tick-kernel variants as tools/variants/libmraft_hip_<tag>.so (same
+# sources, different compile-time knobs); tools/tune.sh times them.
+# Each argument is  tag=DEFINES  e.g.  "v2=-DMRAFT_TICK_V=2 -DMRAFT_TICK_MINW=6"
 set -e
 cd "$(dirname "$0")/../multiraft_amd/csrc"
 mkdir -p ../../tools/variants
 rm -f ../../tools/variants/*.so
 for spec in "$@"; do
-  IFS=: read V W VC X NT <<< "$spec"
-  NT=${NT:-3}
-  tag="v${V}w${W}c${VC}x${X}n${NT}"
+  tag=${spec%%=*}
+  defs=${spec#*=}
   mkdir -p build_$tag
   for f in mraft_abi mraft_kernels mraft_tick mraft_elect; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
-      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X -DMRAFT_TICK_NT=$NT \
-      -c $f.hip -o build_$tag/$f.o 2>/dev/null &
+      $defs -c $f.hip -o build_$tag/$f.o 2>/dev/null &
   done
   wait
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o
   rm -rf build_$tag
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
-      -DMRAFT_TICK_V=$V -DMRAFT_TICK_MINW=$W -DMRAFT_TICK_VC=$VC -DMRAFT_TICK_XCD=$X -DMRAFT_TICK_NT=$NT \
-      -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
-      grep -A9 "k_tick_groupILi5ELb0" | grep -E "VGPRs:|Scratch" | sed -E "s/.*(VGPRs|ScratchSize)[^:]*: ([0-9]+).*/\1=\2/" | tr "\n" " "; echo
+      $defs -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
+      grep -A9 "k_tick_groupILi5ELb0" | grep -E "VGPRs:|Scratch|Occupancy" | sed -E "s/.*(VGPRs|ScratchSize|Occupancy)[^:]*: ([0-9]+).*/\1=\2/" | tr "\n" " "; echo
 done
