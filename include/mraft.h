@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MRAFT_ABI_VERSION 1
+#define MRAFT_ABI_VERSION 2
 
 /* Node states, raft_rpc.go:8-12 (values preserved). */
 enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
@@ -124,7 +124,41 @@ typedef struct {
   int32_t *log_term;      /* [G*P*L] log[slot*L + (Index - dummy)] = Term   */
   int32_t *match_index;   /* [G*P*P] matchIndex[slot*P + peer]              */
   int32_t *next_index;    /* [G*P*P] nextIndex[slot*P + peer]               */
+  int32_t *persist_dirty; /* MRAFT_PERSIST_* bits: persist() call sites run
+                             since the last mraft_collect_persist (below)  */
 } mraft_soa;
+
+/* Persistence (SURVEY.md §5 "Checkpoint / resume", §8f #4). The reference
+ * persists currentTerm, votedFor and the log (raft.go:205-216) at fixed call
+ * sites; the engine ORs one of these bits into persist_dirty[slot] wherever
+ * the reference would have called:
+ *   persist()              -> MRAFT_PERSIST_STATE:
+ *       Start (raft.go:101, leader only), processAppendEntriesReply step-down
+ *       (raft_append_entry.go:72), HandleAppendEntries on every handled call
+ *       (deferred, :111 — the stale-term reply included), StartElection
+ *       (raft_election.go:15), the tally's step-down (:45), HandleRequestVote
+ *       on every handled call (deferred, :57), HandleInstallSnapshot's term
+ *       adoption (raft_snapshot.go:26), processInstallSnapshotReply's
+ *       step-down (:64);
+ *   SaveStateAndSnapshot() -> MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT:
+ *       Snapshot above dummyIndex (raft_snapshot.go:12, the service's bytes),
+ *       HandleInstallSnapshot installing (:47, the leader's bytes).
+ * Items the engine rejects (item_err != 0) mark nothing. */
+enum { MRAFT_PERSIST_STATE = 1, MRAFT_PERSIST_SNAPSHOT = 2 };
+
+/* The persistent part of one replica (SaveState, raft.go:209-216): the terms
+ * of its log entries dummyIndex..lastIndex (the dummy entry first) are
+ * terms[terms_offset .. terms_offset + last_index - dummy_index]. Commands
+ * stay on the host, index-aligned. */
+typedef struct {
+  int32_t slot;
+  int32_t current_term;
+  int32_t voted_for;
+  int32_t dummy_index;
+  int32_t last_index;
+  int32_t _pad;
+  int64_t terms_offset;
+} mraft_persistent;
 
 /* AppendEntriesArgs, raft_rpc.go:55-62. Entries are passed by reference:
  * entry k (0 <= k < n_entries) has Index prev_log_index+1+k (as built by
@@ -386,6 +420,44 @@ int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items,
  * MRAFT_G_STEPPED_DOWN. P <= 8 (one mask byte per group and round). */
 int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask,
                           int32_t rounds, int32_t *group_flags, int32_t where);
+
+/* ---- persistence (raft.go:205-235, persister.go) ------------------------- */
+
+/* out_bits[slot] = persist_dirty[slot] for all G*P slots, then clears them:
+ * the slots whose raft state (and snapshot) the host must save now. */
+int mraft_collect_persist(mraft_engine *h, int32_t *out_bits, int32_t where);
+
+/* SaveState (raft.go:209-216) for n slots, host buffers, synchronous:
+ * out[i] gets slot i's currentTerm, votedFor, dummyIndex, lastIndex and a
+ * terms_offset into out_terms, where its last-dummy+1 log terms are packed in
+ * slot order. If terms_cap is too small, out[] is still filled (so the caller
+ * can size the buffer), nothing is copied and MRAFT_E_INVAL is returned. */
+int mraft_read_persistent(mraft_engine *h, const int32_t *slots, int64_t n,
+                          mraft_persistent *out, int32_t *out_terms,
+                          int64_t terms_cap);
+
+/* Crash + restart of n replicas: Make (raft.go:51-87) followed by
+ * readPersist (:217-235) of the given persistent state (host buffers,
+ * synchronous). Per slot: currentTerm, votedFor and the log from `in`;
+ * state Follower; commitIndex = lastApplied = dummyIndex (:79-80);
+ * matchIndex = nextIndex = 0; grantedVotes 0; persist_dirty 0. item_err:
+ * MRAFT_ITEM_BAD_SLOT (slot out of range or last < dummy),
+ * MRAFT_ITEM_LOG_FULL (more than L entries), MRAFT_ITEM_DUP_SLOT. */
+int mraft_restore(mraft_engine *h, const mraft_persistent *in, int64_t n,
+                  const int32_t *terms, int64_t n_terms, int32_t *item_err);
+
+/* Host-only codec of one replica's persistent state (the bytes a Persister
+ * holds, persister.go:39-64). Not gob (labgob.go): little-endian
+ * "MRPS" | u32 version 1 | i64 currentTerm | i64 votedFor | i64 dummyIndex |
+ * u32 count | count x i64 term (count = lastIndex - dummyIndex + 1; Go's int
+ * is 64-bit on the wire). encode returns the byte size (or the size needed,
+ * writing nothing, when cap is too small); decode returns MRAFT_OK, or
+ * MRAFT_E_INVAL on a malformed buffer or terms_cap < count (terms_offset of
+ * `out` is set to 0 and out->slot is left to the caller). */
+int64_t mraft_encode_persistent(const mraft_persistent *in, const int32_t *terms,
+                                uint8_t *out, int64_t cap);
+int mraft_decode_persistent(const uint8_t *buf, int64_t len, mraft_persistent *out,
+                            int32_t *terms, int64_t terms_cap);
 
 /* ---- read-out (GetState, raft.go:237-246) -------------------------------- */
 

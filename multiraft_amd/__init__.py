@@ -5,13 +5,15 @@ ABI in include/mraft.h); this package is its host-side mirror:
   * `engine.Engine`  — one handle per GPU: HBM-resident replica state and the
     batched decision entry points (AppendEntries, replies/commit, RequestVote,
     vote tally, the fused replication tick);
-  * `raft`           — the reference's per-instance API (Make / Start /
-    GetState / handlers) for one group, driven through the same ABI, plus the
-    deterministic 2B-scenario simulator.
+  * `persister`      — persister.go for every replica, fed by the engine's
+    persist_dirty set (flush after a batch; crash + restart via readPersist);
+  * `router`         — the shard router's view of the all-gathered GetState
+    words (one RCCL all-gather per tick on multi-GPU).
 """
 from ._abi import (CANDIDATE, DEVICE, FOLLOWER, HOST, LEADER, synth_seed)  # noqa: F401
-from .engine import (Engine, MraftError, copy_state, new_state, state_sizes,  # noqa: F401
-                     synth_election_state, synth_fold_batch, synth_tick_state)
+from .engine import (Engine, MraftError, copy_state, decode_persistent,  # noqa: F401
+                     encode_persistent, new_state, state_sizes, synth_election_state,
+                     synth_fold_batch, synth_tick_state)
 
 __all__ = ["Engine", "MraftError", "new_state", "copy_state", "state_sizes", "synth_tick_state",
-           "synth_fold_batch", "synth_election_state", "synth_seed", "LEADER", "CANDIDATE", "FOLLOWER", "HOST", "DEVICE"]
+           "synth_fold_batch", "synth_election_state", "encode_persistent", "decode_persistent", "synth_seed", "LEADER", "CANDIDATE", "FOLLOWER", "HOST", "DEVICE"]

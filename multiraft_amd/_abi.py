@@ -27,6 +27,8 @@ F_SNAPSHOT_INSTALLED = 32
 G_SNAPSHOT_INSTALLED = 256
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
  G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
+PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
+ABI_VERSION = 2
 SYN_MATCH, SYN_MISMATCH, SYN_BEYOND, SYN_STALE, SYN_BELOW_DUMMY, SYN_HEARTBEAT = range(6)
 
 
@@ -39,7 +41,7 @@ _P32 = ctypes.POINTER(ctypes.c_int32)
 
 STATE_FIELDS = ("current_term", "voted_for", "state", "commit_index", "last_applied",
                 "dummy_index", "last_index", "granted_votes", "log_term", "match_index",
-                "next_index")
+                "next_index", "persist_dirty")
 
 
 class MraftSoa(ctypes.Structure):
@@ -66,6 +68,10 @@ IS_RESULT = np.dtype([("slot", "<i4"), ("peer", "<i4"), ("args_term", "<i4"),
                       ("args_last_included_index", "<i4"), ("reply_term", "<i4")])
 RV_RESULT = np.dtype([("slot", "<i4"), ("peer", "<i4"), ("args_term", "<i4"),
                       ("reply_term", "<i4"), ("vote_granted", "<i4")])
+PERSISTENT = np.dtype([("slot", "<i4"), ("current_term", "<i4"), ("voted_for", "<i4"),
+                       ("dummy_index", "<i4"), ("last_index", "<i4"), ("_pad", "<i4"),
+                       ("terms_offset", "<i8")])
+assert PERSISTENT.itemsize == 32
 assert AE_ARGS.itemsize == 40 and AE_RESULT.itemsize == 32 and RV_ARGS.itemsize == 20
 
 # Every symbol include/mraft.h declares (checked by tests/test_abi.py).
@@ -79,7 +85,8 @@ ABI_SYMBOLS = (
     "mraft_snapshot", "mraft_gather_install_snapshot_args", "mraft_handle_install_snapshot",
     "mraft_process_install_snapshot_replies",
     "mraft_start_election", "mraft_handle_request_vote", "mraft_process_vote_replies",
-    "mraft_export_group_status",
+    "mraft_export_group_status", "mraft_collect_persist", "mraft_read_persistent",
+    "mraft_restore", "mraft_encode_persistent", "mraft_decode_persistent",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -113,6 +120,11 @@ _SIGS = {
     "mraft_handle_request_vote": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i32]),
     "mraft_process_vote_replies": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32]),
     "mraft_export_group_status": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32]),
+    "mraft_collect_persist": (ctypes.c_int, [_vp, _vp, _i32]),
+    "mraft_read_persistent": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _i64]),
+    "mraft_restore": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp]),
+    "mraft_encode_persistent": (ctypes.c_int64, [_vp, _vp, _vp, _i64]),
+    "mraft_decode_persistent": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

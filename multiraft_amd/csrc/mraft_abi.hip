@@ -54,7 +54,7 @@ mraft::Dev dev_of(const mraft_engine *h) {
   d.term = h->dev.current_term; d.voted = h->dev.voted_for; d.role = h->dev.state;
   d.commit = h->dev.commit_index; d.applied = h->dev.last_applied; d.dummy = h->dev.dummy_index;
   d.last = h->dev.last_index; d.votes = h->dev.granted_votes; d.log = h->dev.log_term;
-  d.match = h->dev.match_index; d.next = h->dev.next_index;
+  d.match = h->dev.match_index; d.next = h->dev.next_index; d.pdirty = h->dev.persist_dirty;
   d.G = h->G; d.P = h->P; d.L = h->L;
   return d;
 }
@@ -65,7 +65,7 @@ const ArrDesc kArrays[] = {
     {&mraft_soa::current_term, 0}, {&mraft_soa::voted_for, 0},   {&mraft_soa::state, 0},
     {&mraft_soa::commit_index, 0}, {&mraft_soa::last_applied, 0}, {&mraft_soa::dummy_index, 0},
     {&mraft_soa::last_index, 0},   {&mraft_soa::granted_votes, 0}, {&mraft_soa::log_term, 1},
-    {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2}};
+    {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2},  {&mraft_soa::persist_dirty, 0}};
 
 size_t arr_bytes(const mraft_engine *h, int kind) {
   int64_t gp = gp_of(h);
@@ -608,6 +608,90 @@ int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask, int32_t rou
   TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
   mraft::launch_election_rounds(dev_of(h), (const uint8_t *)m, rounds, (int32_t *)gf, h->stream);
   return sg.finish();
+}
+
+// ---------------------------------------------------------------- persistence
+
+int mraft_collect_persist(mraft_engine *h, int32_t *out_bits, int32_t where) {
+  TRY(check(h));
+  if (!out_bits) return fail(MRAFT_E_INVAL, "out_bits is null");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *o;
+  TRY(sg.map(out_bits, sizeof(int32_t) * (size_t)gp_of(h), false, true, &o));
+  mraft::launch_collect_persist(dev_of(h), (int32_t *)o, h->stream);
+  return sg.finish();
+}
+
+int mraft_read_persistent(mraft_engine *h, const int32_t *slots, int64_t n, mraft_persistent *out,
+                          int32_t *out_terms, int64_t terms_cap) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!slots || !out))) return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  for (int64_t i = 0; i < n; ++i)
+    if (slots[i] < 0 || slots[i] >= gp_of(h)) return fail(MRAFT_E_INVAL, "slot %d out of range", slots[i]);
+  HIP_TRY(hipSetDevice(h->device));
+  void *ds, *dh, *dt;
+  TRY(scratch(h, 2, sizeof(int32_t) * (size_t)n, &ds));
+  TRY(scratch(h, 3, sizeof(mraft_persistent) * (size_t)n, &dh));
+  HIP_TRY(hipMemcpyAsync(ds, slots, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
+  mraft::launch_read_persistent_hdr(dev_of(h), (const int32_t *)ds, n, (mraft_persistent *)dh, h->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, dh, sizeof(mraft_persistent) * n, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  int64_t off = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    out[i].terms_offset = off;
+    off += (int64_t)out[i].last_index - out[i].dummy_index + 1;
+  }
+  if (!out_terms || terms_cap < off)
+    return fail(MRAFT_E_INVAL, "read_persistent: %lld terms needed, capacity %lld", (long long)off,
+                (long long)terms_cap);
+  TRY(scratch(h, 4, sizeof(int32_t) * (size_t)off, &dt));
+  HIP_TRY(hipMemcpyAsync(dh, out, sizeof(mraft_persistent) * n, hipMemcpyHostToDevice, h->stream));
+  mraft::launch_read_persistent_terms(dev_of(h), (const mraft_persistent *)dh, n, (int32_t *)dt,
+                                      h->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_terms, dt, sizeof(int32_t) * off, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MRAFT_OK;
+}
+
+int mraft_restore(mraft_engine *h, const mraft_persistent *in, int64_t n, const int32_t *terms,
+                  int64_t n_terms, int32_t *item_err) {
+  TRY(check(h));
+  if (n < 0 || (n > 0 && (!in || !item_err || (n_terms > 0 && !terms))))
+    return fail(MRAFT_E_INVAL, "null argument");
+  if (n == 0) return MRAFT_OK;
+  std::vector<char> seen((size_t)gp_of(h), 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const mraft_persistent &r = in[i];
+    const int64_t cnt = (int64_t)r.last_index - r.dummy_index + 1;
+    int e = MRAFT_ITEM_OK;
+    if (r.slot < 0 || r.slot >= gp_of(h) || cnt < 1 || r.dummy_index < 0 || r.terms_offset < 0 ||
+        r.terms_offset + cnt > n_terms)
+      e = MRAFT_ITEM_BAD_SLOT;
+    else if (cnt > h->L)
+      e = MRAFT_ITEM_LOG_FULL;
+    else if (seen[(size_t)r.slot])
+      e = MRAFT_ITEM_DUP_SLOT;
+    if (e == MRAFT_ITEM_OK) seen[(size_t)r.slot] = 1;
+    item_err[i] = e;
+  }
+  HIP_TRY(hipSetDevice(h->device));
+  void *dh, *dt, *de;
+  TRY(scratch(h, 3, sizeof(mraft_persistent) * (size_t)n, &dh));
+  TRY(scratch(h, 4, sizeof(int32_t) * (size_t)(n_terms > 0 ? n_terms : 1), &dt));
+  TRY(scratch(h, 5, sizeof(int32_t) * (size_t)n, &de));
+  HIP_TRY(hipMemcpyAsync(dh, in, sizeof(mraft_persistent) * n, hipMemcpyHostToDevice, h->stream));
+  if (n_terms > 0)
+    HIP_TRY(hipMemcpyAsync(dt, terms, sizeof(int32_t) * n_terms, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(de, item_err, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
+  mraft::launch_restore(dev_of(h), (const mraft_persistent *)dh, n, (const int32_t *)dt,
+                        (const int32_t *)de, h->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MRAFT_OK;
 }
 
 int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer, int32_t *commit,

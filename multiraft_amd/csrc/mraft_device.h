@@ -25,8 +25,15 @@ constexpr int kChunk = kWave * kUnroll;    // terms per wave iteration
 struct Dev {
   int32_t *term, *voted, *role, *commit, *applied, *dummy, *last, *votes;
   int32_t *log, *match, *next;
+  int32_t *pdirty;  // persist_dirty (include/mraft.h MRAFT_PERSIST_*); may be null
   int32_t G, P, L;
 };
+
+// Records a persist() / SaveStateAndSnapshot() call site of the reference for
+// replica `slot` (one writer per slot per launch).
+__device__ __forceinline__ void mark_persist(const Dev &s, int64_t slot, int bits) {
+  if (s.pdirty && bits) s.pdirty[slot] |= bits;
+}
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 

@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
 #pragma unroll
   for (int p = 0; p < P; ++p) lterm[p] = s.log[(b + p) * s.L + (last[p] - s.dummy[b + p])];  // lastEntry
-  int fl = 0;
+  int fl = 0, pdm = 0;  // pdm: replicas that ran persist() (StartElection :15, HandleRequestVote :57)
   for (int r = 0; r < R; ++r) {
     const int m = cand[(long long)r * s.G + g];
     int isc[P], at[P];
@@ -39,6 +39,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     for (int p = 0; p < P; ++p) {                                      // StartElection :6-17
       isc[p] = ((m >> p) & 1) && role[p] != kLeader;
       if (isc[p]) {
+        pdm |= 1 << p;
         role[p] = kCandidate;
         term[p] += 1;
         voted[p] = p;
@@ -54,6 +55,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
         rt[c][v] = 0;
         rg[c][v] = 0;
         if (!isc[c] || c == v) continue;
+        pdm |= 1 << v;
         if (at[c] < term[v]) {                                         // :59-62
           rt[c][v] = term[v];
           continue;
@@ -101,6 +103,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     s.voted[b + p] = voted[p];
     s.role[b + p] = role[p];
     s.votes[b + p] = votes[p];
+    if ((pdm >> p) & 1) mark_persist(s, b + p, MRAFT_PERSIST_STATE);
     if (became[p]) {
       for (int j = 0; j < P; ++j) {
         s.match[(b + p) * P + j] = 0;

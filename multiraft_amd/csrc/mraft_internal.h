@@ -49,6 +49,13 @@ void launch_tally(const Dev &s, const mraft_rv_result *items, int64_t n, const i
                   hipStream_t st);
 void launch_election_rounds(const Dev &s, const uint8_t *cand, int R, int32_t *gflags,
                             hipStream_t st);
+void launch_collect_persist(const Dev &s, int32_t *out, hipStream_t st);
+void launch_read_persistent_hdr(const Dev &s, const int32_t *slots, int64_t n,
+                                mraft_persistent *out, hipStream_t st);
+void launch_read_persistent_terms(const Dev &s, const mraft_persistent *hdr, int64_t n,
+                                  int32_t *out, hipStream_t st);
+void launch_restore(const Dev &s, const mraft_persistent *in, int64_t n, const int32_t *terms,
+                    const int32_t *err, hipStream_t st);
 void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t *term_leader,
                    hipStream_t st);
 

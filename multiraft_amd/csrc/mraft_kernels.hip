@@ -25,6 +25,7 @@ __global__ void k_init_state(Dev s) {
     // commitIndex = lastApplied = dummyIndex.
     s.term[i] = 0; s.voted[i] = -1; s.role[i] = kFollower; s.commit[i] = 0; s.applied[i] = 0;
     s.dummy[i] = 0; s.last[i] = 0; s.votes[i] = 0;
+    if (s.pdirty) s.pdirty[i] = 0;
   }
 }
 
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void k_handle_ae(Dev s, const mraft_ae_args *_
   const int fterm = s.term[f];
   if (a.term < fterm) {                                                // :112-115
     r.term = fterm;
-    if (lane == 0) rep[i] = r;
+    if (lane == 0) { rep[i] = r; mark_persist(s, f, MRAFT_PERSIST_STATE); }  // deferred :111
     return;
   }
   const bool adopt = a.term > fterm;                                   // :116-118
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(256) void k_handle_ae(Dev s, const mraft_ae_args *_
     s.role[f] = kFollower;                                             // :120
     if (newlast >= 0) s.last[f] = newlast;
     if (fcommit_new >= 0) s.commit[f] = fcommit_new;
+    mark_persist(s, f, MRAFT_PERSIST_STATE);                           // deferred :111
     rep[i] = r;
   }
 }
@@ -270,6 +272,7 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
   }
   if (term != t0 || role != r0) {
     s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
+    mark_persist(s, slot, MRAFT_PERSIST_STATE);                        // :72
   }
   if (commit != c0) s.commit[slot] = commit;
   if (touched_mn) {
@@ -296,6 +299,7 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
       } else {
         for (int j = 1; j <= k; ++j) s.log[(int64_t)sl * s.L + (last + j - dummy)] = t;  // :96-100
         s.last[sl] = last + k;
+        mark_persist(s, sl, MRAFT_PERSIST_STATE);                      // :101
         idx = last + 1; term = t; isl = 1;                             // :103
       }
     }
@@ -330,7 +334,10 @@ __global__ __launch_bounds__(256) void k_snapshot(Dev s, const int32_t *__restri
     return;
   }
   wave_shift_left(s.log + (int64_t)sl * s.L, x - d, last - x + 1);     // :10
-  if (lane_id() == 0) s.dummy[sl] = x;
+  if (lane_id() == 0) {
+    s.dummy[sl] = x;
+    mark_persist(s, sl, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);  // :12
+  }
 }
 
 // appendOneRound's snapshot branch (raft_append_entry.go:27-34).
@@ -407,6 +414,8 @@ __global__ __launch_bounds__(256) void k_handle_is(Dev s, const mraft_is_args *_
       s.commit[f] = lii;                                               // :42
       s.applied[f] = lii;                                              // :43
     }
+    mark_persist(s, f, (a.term > fterm ? MRAFT_PERSIST_STATE : 0) |   // :26
+                           (install ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
     rep[i] = mraft_is_reply{a.term, 0};                                // deferred reply.Term
     flags[i] = fl;
   }
@@ -450,7 +459,10 @@ __global__ void k_process_is(Dev s, const mraft_is_result *__restrict__ items, i
     flags[i] = fl;
     item_err[i] = 0;
   }
-  if (term != t0) { s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1; }
+  if (term != t0) {
+    s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
+    mark_persist(s, slot, MRAFT_PERSIST_STATE);                        // :64
+  }
 }
 
 // ---------------------------------------------------------------- a6 part 1
@@ -467,6 +479,7 @@ __global__ void k_start_election(Dev s, const int32_t *__restrict__ slots, int64
     s.term[sl] = t;
     s.voted[sl] = sl % s.P;                                            // :14
     s.votes[sl] = 1;                                                   // :17
+    mark_persist(s, sl, MRAFT_PERSIST_STATE);                          // :15
     a.slot = sl;
     a.term = t;
     a.candidate_id = sl % s.P;
@@ -487,6 +500,7 @@ __global__ void k_handle_rv(Dev s, const mraft_rv_args *__restrict__ args, int64
     const int v = a.slot;
     int term = s.term[v], voted = s.voted[v], role = s.role[v];
     const int t0 = term, v0 = voted, r0 = role;
+    mark_persist(s, v, MRAFT_PERSIST_STATE);                           // deferred :57
     if (a.term < term) {                                               // raft_election.go:59-62
       r.term = term;
     } else {
@@ -532,7 +546,7 @@ __global__ void k_tally(Dev s, const mraft_rv_result *__restrict__ items, int64_
   }
   int term = s.term[c], role = s.role[c], votes = s.votes[c], voted = s.voted[c];
   const int t0 = term, r0 = role, vs0 = votes, vd0 = voted;
-  bool lead = false;
+  bool lead = false, stepped = false;
   for (int64_t i = b; i < e; ++i) {
     const mraft_rv_result it = items[i];
     int fl = 0;
@@ -547,6 +561,7 @@ __global__ void k_tally(Dev s, const mraft_rv_result *__restrict__ items, int64_
       } else if (it.reply_term > term) {                               // :42-45
         role = kFollower; term = it.reply_term; voted = -1;
         fl |= MRAFT_F_STEPPED_DOWN;
+        stepped = true;
       }
     }
     flags[i] = fl;
@@ -556,9 +571,73 @@ __global__ void k_tally(Dev s, const mraft_rv_result *__restrict__ items, int64_
   if (role != r0) s.role[c] = role;
   if (votes != vs0) s.votes[c] = votes;
   if (voted != vd0) s.voted[c] = voted;
+  if (stepped) mark_persist(s, c, MRAFT_PERSIST_STATE);                // :45
   if (lead) {                                                          // :34-38
     const int nx = s.last[c] + 1;
     for (int j = 0; j < P; ++j) { s.match[(int64_t)c * P + j] = 0; s.next[(int64_t)c * P + j] = nx; }
+  }
+}
+
+// ---------------------------------------------------------------- persistence
+// persist_dirty read-out (copy + clear): the slots the host must save.
+__global__ void k_collect_persist(Dev s, int32_t *__restrict__ out) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < gp;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int v = s.pdirty[i];
+    out[i] = v;
+    if (v) s.pdirty[i] = 0;
+  }
+}
+
+// SaveState (raft.go:209-216), scalar part: lane per slot.
+__global__ void k_read_persistent_hdr(Dev s, const int32_t *__restrict__ slots, int64_t n,
+                                      mraft_persistent *__restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int sl = slots[i];
+  mraft_persistent r = {};
+  r.slot = sl;
+  r.current_term = s.term[sl];
+  r.voted_for = s.voted[sl];
+  r.dummy_index = s.dummy[sl];
+  r.last_index = s.last[sl];
+  out[i] = r;
+}
+
+// SaveState, log part: wave per slot streams terms[0 .. last-dummy] of its row.
+__global__ __launch_bounds__(256) void k_read_persistent_terms(Dev s,
+                                                               const mraft_persistent *__restrict__ hdr,
+                                                               int64_t n, int32_t *__restrict__ out) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (i >= n) return;
+  const mraft_persistent r = hdr[i];
+  wave_copy(s.log + (int64_t)r.slot * s.L, out + r.terms_offset, r.last_index - r.dummy_index + 1);
+}
+
+// Make (raft.go:51-87) + readPersist (:217-235): wave per (validated) item.
+__global__ __launch_bounds__(256) void k_restore(Dev s, const mraft_persistent *__restrict__ in,
+                                                 int64_t n, const int32_t *__restrict__ terms,
+                                                 const int32_t *__restrict__ err) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  if (i >= n || err[i]) return;
+  const mraft_persistent r = in[i];
+  const int64_t sl = r.slot;
+  wave_copy(terms + r.terms_offset, s.log + sl * s.L, r.last_index - r.dummy_index + 1);  // :233
+  if (lane_id() == 0) {
+    s.term[sl] = r.current_term;                                       // :231
+    s.voted[sl] = r.voted_for;                                         // :232
+    s.role[sl] = kFollower;                                            // :58
+    s.dummy[sl] = r.dummy_index;
+    s.last[sl] = r.last_index;
+    s.commit[sl] = r.dummy_index;                                      // :79
+    s.applied[sl] = r.dummy_index;                                     // :80
+    s.votes[sl] = 0;
+    if (s.pdirty) s.pdirty[sl] = 0;
+  }
+  for (int j = lane_id(); j < s.P; j += 64) {                          // :64-65 make([]int, P)
+    s.match[sl * s.P + j] = 0;
+    s.next[sl * s.P + j] = 0;
   }
 }
 
@@ -687,6 +766,31 @@ void launch_tally(const Dev &s, const mraft_rv_result *items, int64_t n, const i
   if (n_seg <= 0) return;
   hipLaunchKernelGGL(k_tally, dim3(blocks_for(n_seg, 64)), dim3(64), 0, st, s, items, n, seg_begin,
                      n_seg, seg_err, flags, item_err);
+}
+
+void launch_collect_persist(const Dev &s, int32_t *out, hipStream_t st) {
+  int blocks = blocks_for((int64_t)s.G * s.P);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_collect_persist, dim3(blocks), dim3(kBlock), 0, st, s, out);
+}
+
+void launch_read_persistent_hdr(const Dev &s, const int32_t *slots, int64_t n,
+                                mraft_persistent *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_read_persistent_hdr, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, n, out);
+}
+
+void launch_read_persistent_terms(const Dev &s, const mraft_persistent *hdr, int64_t n,
+                                  int32_t *out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_read_persistent_terms, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, hdr,
+                     n, out);
+}
+
+void launch_restore(const Dev &s, const mraft_persistent *in, int64_t n, const int32_t *terms,
+                    const int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_restore, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, in, n, terms, err);
 }
 
 void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t *term_leader,

@@ -145,6 +145,8 @@ void gen_group(uint64_t seed, int32_t g, int32_t gl, int32_t P, int32_t L,
   st->dummy_index[ld] = 0;
   st->last_index[ld] = last;
   st->granted_votes[ld] = 0;
+  if (st->persist_dirty)
+    for (int32_t p = 0; p < P; ++p) st->persist_dirty[sb + p] = 0;
 
   for (int32_t p = 0; p < P; ++p) {
     if (p == lp) continue;
@@ -254,6 +256,7 @@ extern "C" int mraft_synth_election_state(uint64_t seed, int32_t G, int32_t P, i
         st->voted_for[s] = rng.below(2) ? -1 : (int32_t)rng.below((uint32_t)P);
         st->state[s] = rng.below(8) == 0 ? MRAFT_CANDIDATE : MRAFT_FOLLOWER;
         st->granted_votes[s] = 0;
+        if (st->persist_dirty) st->persist_dirty[s] = 0;
         st->dummy_index[s] = 0;
         int32_t last = B + (int32_t)rng.below(5) - 2;
         last = std::max(1, std::min(L - 1, last));

@@ -677,6 +677,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   int fcadv = 0;
   long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
   if (icls >= IC_STALE && icls <= IC_HB) {
+    if (!COUNT) mark_persist(s, f, MRAFT_PERSIST_STATE);                 // deferred :111
     if (icls == IC_STALE) {
       cR = 1;
     } else {
@@ -711,6 +712,9 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
   }
   if (icls >= IC_IS_STALE && icls <= IC_IS_INSTALL) {
     cR = 1;                                                              // term
+    if (!COUNT)
+      mark_persist(s, f, (adopt ? MRAFT_PERSIST_STATE : 0) |            // raft_snapshot.go:26
+                             (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
     if (icls != IC_IS_STALE) {
       if (!COUNT) {
         if (adopt) { s.term[f] = T; s.voted[f] = -1; }
@@ -753,6 +757,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
         s.term[ld] = fd.term;
         s.voted[ld] = -1;
         s.role[ld] = kFollower;
+        mark_persist(s, ld, MRAFT_PERSIST_STATE);                        // :72, snapshot :64
       }
       if (commit != c0) s.commit[ld] = commit;
       if (gflags) gflags[g] = flags;

@@ -15,8 +15,8 @@ import os
 import numpy as np
 
 from . import _abi
-from ._abi import (AE_ARGS, AE_REPLY, AE_RESULT, IS_ARGS, IS_REPLY, IS_RESULT, RV_ARGS, RV_REPLY,
-                   RV_RESULT, DEVICE, HOST, STATE_FIELDS, ptr, soa_of)
+from ._abi import (AE_ARGS, AE_REPLY, AE_RESULT, IS_ARGS, IS_REPLY, IS_RESULT, PERSISTENT, RV_ARGS,
+                   RV_REPLY, RV_RESULT, DEVICE, HOST, STATE_FIELDS, ptr, soa_of)
 
 
 class MraftError(RuntimeError):
@@ -303,6 +303,37 @@ class Engine:
             "mraft_election_rounds")
         return group_flags
 
+    # ---- persistence (raft.go:205-235) ------------------------------------
+    def collect_persist(self):
+        """persist_dirty of every slot (MRAFT_PERSIST_* bits), cleared on read."""
+        out = np.zeros(self.G * self.P, np.int32)
+        _ck(self._lib.mraft_collect_persist(self._h, ptr(out), HOST), "mraft_collect_persist")
+        return out
+
+    def read_persistent(self, slots):
+        """SaveState (raft.go:209-216) of the given slots: (PERSISTENT records,
+        packed log terms)."""
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        hdr = np.zeros(n, dtype=PERSISTENT)
+        if n == 0:
+            return hdr, np.zeros(0, np.int32)
+        cap = n * self.L
+        terms = np.zeros(cap, np.int32)
+        _ck(self._lib.mraft_read_persistent(self._h, ptr(slots), n, ptr(hdr), ptr(terms), cap),
+            "mraft_read_persistent")
+        used = int(hdr["terms_offset"][-1] + hdr["last_index"][-1] - hdr["dummy_index"][-1] + 1)
+        return hdr, terms[:used].copy()
+
+    def restore(self, hdr, terms):
+        """Crash + restart (Make + readPersist, raft.go:51-87,217-235)."""
+        hdr = np.ascontiguousarray(hdr, dtype=PERSISTENT)
+        terms = np.ascontiguousarray(terms, dtype=np.int32)
+        err = np.zeros(len(hdr), np.int32)
+        _ck(self._lib.mraft_restore(self._h, ptr(hdr), len(hdr), ptr(terms), len(terms), ptr(err)),
+            "mraft_restore")
+        return err
+
     def export_group_status(self, leader_peer=None):
         commit = np.zeros(self.G, dtype=np.int32)
         tl = np.zeros(self.G, dtype=np.int32)
@@ -316,3 +347,33 @@ def export_group_status_into(eng: Engine, leader_peer, commit, term_leader, wher
     """GetState for every group into caller buffers (device tensors by default)."""
     _ck(eng._lib.mraft_export_group_status(eng._h, ptr(leader_peer), ptr(commit), ptr(term_leader),
                                            where), "mraft_export_group_status")
+
+
+def encode_persistent(rec, terms) -> bytes:
+    """One replica's persistent state as bytes (mraft_encode_persistent)."""
+    r = np.zeros(1, dtype=PERSISTENT)
+    for f in ("current_term", "voted_for", "dummy_index", "last_index"):
+        r[f][0] = rec[f]
+    r["terms_offset"][0] = 0
+    t = np.ascontiguousarray(terms, dtype=np.int32)
+    L = _abi.lib()
+    size = L.mraft_encode_persistent(ptr(r), ptr(t), None, 0)
+    if size < 0:
+        raise MraftError(f"mraft_encode_persistent failed ({size})")
+    buf = ctypes.create_string_buffer(size)
+    got = L.mraft_encode_persistent(ptr(r), ptr(t), ctypes.addressof(buf), size)
+    assert got == size
+    return buf.raw
+
+
+def decode_persistent(data: bytes):
+    """Inverse of encode_persistent: (PERSISTENT record with slot 0, terms)."""
+    r = np.zeros(1, dtype=PERSISTENT)
+    cap = max(1, (len(data) - 36) // 8)
+    terms = np.zeros(cap, np.int32)
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    rc = _abi.lib().mraft_decode_persistent(ctypes.addressof(buf), len(data), ptr(r), ptr(terms), cap)
+    if rc != _abi.OK:
+        raise MraftError(f"mraft_decode_persistent: malformed buffer ({rc})")
+    n = int(r["last_index"][0] - r["dummy_index"][0] + 1)
+    return r[0], terms[:n].copy()

@@ -76,6 +76,14 @@ static inline void CW(int a, int64_t i) {
 
 #define S (e->s)
 
+/* A persist() (bits = MRAFT_PERSIST_STATE) or SaveStateAndSnapshot()
+ * (| MRAFT_PERSIST_SNAPSHOT) call site of the reference ran for replica s
+ * (raft.go:205-216; include/mraft.h lists the sites). Not an algorithmic
+ * state word: never counted. */
+static inline void persist(ora_engine *e, int64_t s, int32_t bits) {
+  if (S.persist_dirty) S.persist_dirty[s] |= bits;
+}
+
 /* getEntry(index).Term, raft_log.go:40-42 + convertIndex :55-60 (caller
  * guarantees index >= dummyIndex; the panic is handled by callers). */
 static inline int32_t term_at(const ora_engine *e, int64_t slot, int32_t index) {
@@ -167,6 +175,7 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
     }
   }
 
+  persist(e, f, MRAFT_PERSIST_STATE);                                 /* defer rf.persist(), :111 */
   CR(A_TERM, f);
   if (a->term < S.current_term[f]) {                                  /* :112-115 */
     r->term = S.current_term[f]; r->success = 0;
@@ -322,6 +331,7 @@ static int32_t process_reply_one(ora_engine *e, int32_t slot, int32_t peer,
     S.voted_for[slot] = -1;
     S.state[slot] = MRAFT_FOLLOWER;
     CW(A_TERM, slot); CW(A_VOTED, slot); CW(A_ROLE, slot);
+    persist(e, slot, MRAFT_PERSIST_STATE);                            /* :72 */
     flags |= MRAFT_F_STEPPED_DOWN;
   } else if (reply_term == S.current_term[slot] &&                    /* :73-74 */
              S.state[slot] == MRAFT_LEADER &&
@@ -408,6 +418,7 @@ static int32_t snapshot_one(ora_engine *e, int32_t s, int32_t index) {
   if (index <= S.dummy_index[s]) return MRAFT_ITEM_OK;                /* :6-9 */
   if (index > S.last_index[s]) return MRAFT_ITEM_PREV_BEYOND_LAST;    /* sliceFrom panics */
   slice_from(e, s, index);                                            /* :10-11 */
+  persist(e, s, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);        /* :12 */
   return MRAFT_ITEM_OK;
 }
 
@@ -468,6 +479,7 @@ static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, m
   if (a->term > S.current_term[f]) {                                  /* :23-26 */
     S.current_term[f] = a->term; S.voted_for[f] = -1;
     CW(A_TERM, f); CW(A_VOTED, f);
+    persist(e, f, MRAFT_PERSIST_STATE);                               /* :26 */
   }
   S.state[f] = MRAFT_FOLLOWER;                                        /* :28 */
   CW(A_ROLE, f);
@@ -489,6 +501,7 @@ static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, m
   S.commit_index[f] = lii;                                            /* :42 */
   S.last_applied[f] = lii;                                            /* :43 */
   CW(A_DUMMY, f); CW(A_COMMIT, f); CW(A_APPLIED, f);
+  persist(e, f, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);        /* :47 */
   *installed = 1;                                                     /* :49-50 hasSnapshot */
   return MRAFT_ITEM_OK;
 }
@@ -518,6 +531,7 @@ static int32_t process_is_reply_one(ora_engine *e, int32_t slot, int32_t peer, i
     S.voted_for[slot] = -1;
     S.state[slot] = MRAFT_FOLLOWER;
     CW(A_TERM, slot); CW(A_VOTED, slot); CW(A_ROLE, slot);
+    persist(e, slot, MRAFT_PERSIST_STATE);                            /* :64 */
     fl |= MRAFT_F_STEPPED_DOWN;
   } else if (S.state[slot] == MRAFT_LEADER && args_term == S.current_term[slot]) {  /* :65 */
     S.match_index[pi] = lii;                                          /* :66 */
@@ -729,6 +743,7 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
     for (int32_t j = 1; j <= k; ++j)                                  /* :96-100 */
       S.log_term[(int64_t)s * e->L + (last + j - dummy)] = S.current_term[s];
     S.last_index[s] = last + k;
+    persist(e, s, MRAFT_PERSIST_STATE);                               /* :101 */
     out_index[i] = last + 1; out_term[i] = S.current_term[s]; out_is_leader[i] = 1;  /* :103 */
   }
   free(first);
@@ -760,6 +775,7 @@ static void start_election_one(ora_engine *e, int32_t s, mraft_rv_args *a) {
   a->last_log_index = last;                                           /* :12 */
   a->last_log_term = term_at(e, s, last);                             /* :13 */
   S.voted_for[s] = s % e->P;                                          /* :14 */
+  persist(e, s, MRAFT_PERSIST_STATE);                                 /* :15 */
   S.granted_votes[s] = 1;                                             /* :17 */
 }
 
@@ -781,6 +797,7 @@ int ora_start_election(ora_engine *e, const int32_t *slots, int64_t n,
 
 static void handle_rv_one(ora_engine *e, int32_t v, const mraft_rv_args *a, mraft_rv_reply *r) {
   r->term = 0; r->vote_granted = 0;
+  persist(e, v, MRAFT_PERSIST_STATE);                                 /* defer rf.persist(), :57 */
   if (a->term < S.current_term[v]) {                                  /* :59-62 */
     r->term = S.current_term[v];
     return;
@@ -835,6 +852,7 @@ static int32_t tally_one(ora_engine *e, int32_t c, int32_t args_term, int32_t re
     } else if (reply_term > S.current_term[c]) {                      /* :42-45 */
       S.state[c] = MRAFT_FOLLOWER;
       S.current_term[c] = reply_term; S.voted_for[c] = -1;
+      persist(e, c, MRAFT_PERSIST_STATE);                             /* :45 */
       fl |= MRAFT_F_STEPPED_DOWN;
     }
   }
@@ -924,5 +942,77 @@ int ora_export_group_status(ora_engine *e, const int32_t *leader_peer,
     commit[g] = S.commit_index[s];
     term_leader[g] = (int32_t)(((uint32_t)S.current_term[s] << 1) | (S.state[s] == MRAFT_LEADER));
   }
+  return MRAFT_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Persistence: the dirty set, SaveState and Make + readPersist               */
+/* ------------------------------------------------------------------------ */
+
+int ora_collect_persist(ora_engine *e, int32_t *out_bits) {
+  const int64_t gp = (int64_t)e->G * e->P;
+  for (int64_t s = 0; s < gp; ++s) {
+    out_bits[s] = S.persist_dirty ? S.persist_dirty[s] : 0;
+    if (S.persist_dirty) S.persist_dirty[s] = 0;
+  }
+  return MRAFT_OK;
+}
+
+/* SaveState, raft.go:209-216: currentTerm, votedFor, logs (terms here). */
+int ora_read_persistent(ora_engine *e, const int32_t *slots, int64_t n, mraft_persistent *out,
+                        int32_t *out_terms, int64_t terms_cap) {
+  int64_t off = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t s = slots[i];
+    memset(&out[i], 0, sizeof(out[i]));
+    out[i].slot = s;
+    out[i].current_term = S.current_term[s];
+    out[i].voted_for = S.voted_for[s];
+    out[i].dummy_index = S.dummy_index[s];
+    out[i].last_index = S.last_index[s];
+    out[i].terms_offset = off;
+    off += (int64_t)S.last_index[s] - S.dummy_index[s] + 1;
+  }
+  if (!out_terms || terms_cap < off) return MRAFT_E_INVAL;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t cnt = (int64_t)out[i].last_index - out[i].dummy_index + 1;
+    memcpy(out_terms + out[i].terms_offset, S.log_term + (int64_t)out[i].slot * e->L,
+           sizeof(int32_t) * (size_t)cnt);
+  }
+  return MRAFT_OK;
+}
+
+/* Make (raft.go:51-87) + readPersist (:217-235). */
+int ora_restore(ora_engine *e, const mraft_persistent *in, int64_t n, const int32_t *terms,
+                int64_t n_terms, int32_t *item_err) {
+  const int32_t P = e->P;
+  const int64_t gp = (int64_t)e->G * P;
+  char *seen = (char *)calloc((size_t)(gp ? gp : 1), 1);
+  for (int64_t i = 0; i < n; ++i) {
+    const mraft_persistent *r = &in[i];
+    const int64_t cnt = (int64_t)r->last_index - r->dummy_index + 1;
+    if (r->slot < 0 || r->slot >= gp || cnt < 1 || r->dummy_index < 0 || r->terms_offset < 0 ||
+        r->terms_offset + cnt > n_terms) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
+    if (cnt > e->L) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
+    if (seen[r->slot]) { item_err[i] = MRAFT_ITEM_DUP_SLOT; continue; }
+    seen[r->slot] = 1;
+    item_err[i] = MRAFT_ITEM_OK;
+    const int64_t s = r->slot;
+    S.state[s] = MRAFT_FOLLOWER;                                      /* :58 */
+    S.current_term[s] = r->current_term;                              /* :231 */
+    S.voted_for[s] = r->voted_for;                                    /* :232 */
+    memcpy(S.log_term + s * e->L, terms + r->terms_offset, sizeof(int32_t) * (size_t)cnt);  /* :233 */
+    S.dummy_index[s] = r->dummy_index;
+    S.last_index[s] = r->last_index;
+    S.commit_index[s] = r->dummy_index;                               /* :79 */
+    S.last_applied[s] = r->dummy_index;                               /* :80 */
+    S.granted_votes[s] = 0;
+    for (int32_t j = 0; j < P; ++j) {                                 /* :64-65 */
+      S.match_index[s * P + j] = 0;
+      S.next_index[s * P + j] = 0;
+    }
+    if (S.persist_dirty) S.persist_dirty[s] = 0;
+  }
+  free(seen);
   return MRAFT_OK;
 }

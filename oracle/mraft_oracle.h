@@ -89,6 +89,12 @@ int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
 int ora_export_group_status(ora_engine *e, const int32_t *leader_peer,
                             int32_t *commit, int32_t *term_leader);
 
+int ora_collect_persist(ora_engine *e, int32_t *out_bits);
+int ora_read_persistent(ora_engine *e, const int32_t *slots, int64_t n, mraft_persistent *out,
+                        int32_t *out_terms, int64_t terms_cap);
+int ora_restore(ora_engine *e, const mraft_persistent *in, int64_t n, const int32_t *terms,
+                int64_t n_terms, int32_t *item_err);
+
 #ifdef __cplusplus
 }
 #endif

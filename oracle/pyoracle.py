@@ -150,6 +150,10 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
     nextIndex: List[int]
     matchIndex: List[int]
     grantedVotes: int = 0
+    persisted: int = 0  # persist() (1) / SaveStateAndSnapshot() (1|2) ran since the last collect
+
+    def persist(self, bits=1):  # raft.go:205-208; SaveStateAndSnapshot persister.go:58-63
+        self.persisted |= bits
 
     # ---- raft_append_entry.go ----
     def gatherArgs(self, peer):  # appendOneRound :20-54 (args part)
@@ -173,6 +177,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             self.currentTerm = reply.Term
             self.votedFor = -1
             self.state = FOLLOWER
+            self.persist()  # :72
             flags |= F_STEPPED_DOWN
         elif (reply.Term == self.currentTerm and self.state == LEADER and
               args.Term == self.currentTerm and args.PrevLogIndex == self.nextIndex[peer] - 1):
@@ -202,6 +207,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
         return False
 
     def HandleAppendEntries(self, args, reply):  # :108-162
+        self.persist()  # defer rf.persist(), :111
         if args.Term < self.currentTerm:
             reply.Term, reply.Success = self.currentTerm, False
             return
@@ -238,6 +244,15 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
         reply.Term, reply.Success = self.currentTerm, True
         return follower_commit
 
+    # ---- raft.go ----
+    def Start(self):  # raft.go:90-104 (the command stays with the caller)
+        if self.state != LEADER:
+            return -1, -1, 0
+        e = Entry(self.raftLog.lastIndex() + 1, self.currentTerm)
+        self.raftLog.append(e)
+        self.persist()  # :101
+        return e.Index, e.Term, 1
+
     # ---- raft_snapshot.go ----
     def Snapshot(self, index):  # :3-13
         if index <= self.raftLog.dummyIndex():
@@ -245,6 +260,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
         if index > self.raftLog.lastIndex():
             return PREV_BEYOND_LAST  # sliceFrom panics
         self.raftLog.setLogs(self.raftLog.sliceFrom(index))
+        self.persist(3)  # SaveStateAndSnapshot, :12
         return ITEM_OK
 
     def gatherInstallSnapshot(self):  # raft_append_entry.go:27-34
@@ -258,6 +274,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
                 return False
             if args.Term > self.currentTerm:
                 self.currentTerm, self.votedFor = args.Term, -1
+                self.persist()  # :26
             self.state = FOLLOWER
             if args.LastIncludedIndex <= self.commitIndex:
                 return False
@@ -269,6 +286,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             self.lastApplied = args.LastIncludedIndex
             self.raftLog.logs[0].Index = args.LastIncludedIndex
             self.raftLog.logs[0].Term = args.LastIncludedTerm
+            self.persist(3)  # SaveStateAndSnapshot, :47
             return True
         finally:
             reply.Term = self.currentTerm
@@ -278,6 +296,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             self.currentTerm = reply.Term
             self.votedFor = -1
             self.state = FOLLOWER
+            self.persist()  # :64
             return F_STEPPED_DOWN
         if self.state == LEADER and args.Term == self.currentTerm:
             self.matchIndex[peer] = args.LastIncludedIndex
@@ -293,6 +312,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
         args = RequestVoteArgs(Term=self.currentTerm, CandidateId=self.me,
                                LastLogIndex=lastLog.Index, LastLogTerm=lastLog.Term)
         self.votedFor = self.me
+        self.persist()  # :15
         self.grantedVotes = 1
         return args
 
@@ -310,10 +330,12 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             elif reply.Term > self.currentTerm:
                 self.state = FOLLOWER
                 self.currentTerm, self.votedFor = reply.Term, -1
+                self.persist()  # :45
                 flags |= F_STEPPED_DOWN
         return flags
 
     def HandleRequestVote(self, args, reply):  # :54-77
+        self.persist()  # defer rf.persist(), :57
         if args.Term < self.currentTerm:
             reply.Term, reply.VoteGranted = self.currentTerm, False
             return
@@ -334,7 +356,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
 # ---------------------------------------------------------------------------
 
 STATE_KEYS = ("current_term", "voted_for", "state", "commit_index", "last_applied",
-              "dummy_index", "last_index", "granted_votes", "log_term", "match_index", "next_index")
+              "dummy_index", "last_index", "granted_votes", "log_term", "match_index", "next_index", "persist_dirty")
 
 
 def from_soa(st: dict, G: int, P: int, L: int) -> List[Raft]:
@@ -349,7 +371,8 @@ def from_soa(st: dict, G: int, P: int, L: int) -> List[Raft]:
                           lastApplied=int(st["last_applied"][s]),
                           nextIndex=[int(x) for x in st["next_index"][s * P:(s + 1) * P]],
                           matchIndex=[int(x) for x in st["match_index"][s * P:(s + 1) * P]],
-                          grantedVotes=int(st["granted_votes"][s])))
+                          grantedVotes=int(st["granted_votes"][s]),
+                          persisted=int(st["persist_dirty"][s]) if "persist_dirty" in st else 0))
     return rafts
 
 
@@ -366,6 +389,9 @@ def to_soa(rafts: List[Raft], st: dict, G: int, P: int, L: int) -> dict:
         out["dummy_index"][s] = rf.raftLog.dummyIndex()
         out["last_index"][s] = rf.raftLog.lastIndex()
         out["granted_votes"][s] = rf.grantedVotes
+        if "persist_dirty" not in out:
+            out["persist_dirty"] = np.zeros(len(rafts), dtype=np.int32)
+        out["persist_dirty"][s] = rf.persisted
         if len(rf.raftLog.logs) > L:
             raise ValueError("log exceeds capacity")
         for k, e in enumerate(rf.raftLog.logs):

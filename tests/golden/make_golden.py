@@ -31,7 +31,7 @@ def one_group(P, L, slots):
     st = {k: np.zeros(n, dtype=np.int64) for k, n in {
         "current_term": P, "voted_for": P, "state": P, "commit_index": P, "last_applied": P,
         "dummy_index": P, "last_index": P, "granted_votes": P, "log_term": P * L,
-        "match_index": P * P, "next_index": P * P}.items()}
+        "match_index": P * P, "next_index": P * P, "persist_dirty": P}.items()}
     st["voted_for"][:] = -1
     st["state"][:] = FOLLOWER
     for p in range(P):
@@ -133,7 +133,84 @@ def build():
                      op="process_vote_replies", items=items,
                      expect={"flags": [0, 0, 8, 0], "slot0": dict(state=LEADER, granted_votes=4),
                              "next0": [3] * 7, "match0": [0] * 7}))
+    # Every handled AppendEntries / RequestVote persists (deferred
+    # rf.persist(), raft_append_entry.go:111, raft_election.go:57); a
+    # successful reply fold or a granted tally does not.
+    for k in kats:
+        k["expect"]["persist"] = ({"1": 1} if k["op"] in ("handle_append_entries", "handle_request_vote")
+                                  else {str(i): 0 for i in range(k["P"])})
+    kats += persist_kats()
     return kats
+
+
+def persist_kats():
+    """P1-P10: the persist() / SaveStateAndSnapshot() call sites (include/mraft.h
+    MRAFT_PERSIST_*: 1 = raft state, 2 = snapshot), hand-derived."""
+    ae, el, sn, rf = ("src/raft/raft_append_entry.go", "src/raft/raft_election.go",
+                      "src/raft/raft_snapshot.go", "src/raft/raft.go")
+    FL = [0, 1, 1, 2, 2, 3]  # follower log, indices 0..5
+    out = []
+    # P1: reply with a higher term -> step down + persist (:67-72)
+    st = one_group(3, 16, {0: dict(term=4, voted=0, state=LEADER, commit=1, terms=FL,
+                                   match=[0, 1, 1], next=[6, 2, 2])})
+    out.append(dict(name="P1", cite=f"{ae}:67-72", G=1, P=3, L=16, state=st, op="process_append_replies",
+                    items=[dict(slot=0, peer=1, args_term=4, args_prev_log_index=1, args_n_entries=4,
+                                reply_term=6, reply_success=0, reply_conflict_index=0)],
+                    expect={"flags": [4], "slot0": dict(current_term=6, voted_for=-1, state=FOLLOWER),
+                            "persist": {"0": 1}}))
+
+    def is_kat(name, cite, follower, args, reply_term, persist, extra=None):
+        st = one_group(3, 16, {1: follower})
+        a = dict(slot=1, term=args["term"], leader_id=0, last_included_index=args["lii"],
+                 last_included_term=args["lit"])
+        e = {"is_reply": reply_term, "persist": {"1": persist}}
+        if extra:
+            e["slot1"] = extra
+        return dict(name=name, cite=cite, G=1, P=3, L=16, state=st, op="handle_install_snapshot",
+                    args=[a], expect=e)
+    out.append(is_kat("P2", f"{sn}:20-22 (stale: no persist)", dict(term=5, commit=2, terms=FL),
+                      dict(term=4, lii=4, lit=2), 5, 0, dict(current_term=5, dummy_index=0)))
+    out.append(is_kat("P3", f"{sn}:31-33 (outdated, same term: no persist)",
+                      dict(term=5, commit=4, terms=FL), dict(term=5, lii=3, lit=2), 5, 0,
+                      dict(commit_index=4, dummy_index=0)))
+    out.append(is_kat("P4", f"{sn}:23-26 (term adopted: persist)", dict(term=5, commit=4, terms=FL),
+                      dict(term=7, lii=3, lit=2), 7, 1,
+                      dict(current_term=7, voted_for=-1, dummy_index=0, commit_index=4)))
+    out.append(is_kat("P5", f"{sn}:38-47 (installed: SaveStateAndSnapshot)",
+                      dict(term=5, commit=1, terms=FL), dict(term=5, lii=4, lit=2), 5, 3,
+                      dict(dummy_index=4, last_index=5, commit_index=4, last_applied=4, log=[2, 3])))
+    # P6: Snapshot below/at dummy is a no-op (:6-9); above it saves state + snapshot (:10-12)
+    st = one_group(3, 16, {0: dict(term=3, commit=5, terms=FL), 2: dict(term=3, commit=5, terms=FL, dummy=0)})
+    out.append(dict(name="P6", cite=f"{sn}:3-13", G=1, P=3, L=16, state=st, op="snapshot",
+                    slots=[0, 2], index=[0, 3],
+                    expect={"persist": {"0": 0, "2": 3}, "slot0": dict(dummy_index=0),
+                            "slot2": dict(dummy_index=3, log=[2, 2, 3])}))
+    # P7: Start on a follower returns early (:93-95); on the leader it persists (:96-101)
+    st = one_group(3, 16, {0: dict(term=3, terms=FL), 1: dict(term=3, state=LEADER, voted=1, terms=FL)})
+    out.append(dict(name="P7", cite=f"{rf}:90-104", G=1, P=3, L=16, state=st, op="start",
+                    slots=[0, 1], expect={"start": [[-1, -1, 0], [6, 3, 1]],
+                                          "persist": {"0": 0, "1": 1}, "slot1": dict(last_index=6)}))
+    # P8: a denied vote with a higher term -> step down + persist (:42-45)
+    st = one_group(3, 16, {0: dict(term=5, voted=0, state=CANDIDATE, terms=[0, 1])})
+    st["granted_votes"][0] = 1
+    out.append(dict(name="P8", cite=f"{el}:42-45", G=1, P=3, L=16, state=st, op="process_vote_replies",
+                    items=[dict(slot=0, peer=1, args_term=5, reply_term=8, vote_granted=0)],
+                    expect={"flags": [4], "slot0": dict(state=FOLLOWER, current_term=8, voted_for=-1),
+                            "persist": {"0": 1}}))
+    # P9: processInstallSnapshotReply with a higher term -> step down + persist (:59-64)
+    st = one_group(3, 16, {0: dict(term=4, voted=0, state=LEADER, commit=4, dummy=3, terms=[2, 2, 3],
+                                   match=[0, 0, 0], next=[6, 1, 6])})
+    out.append(dict(name="P9", cite=f"{sn}:56-69", G=1, P=3, L=16, state=st,
+                    op="process_install_snapshot_replies",
+                    items=[dict(slot=0, peer=1, args_term=4, args_last_included_index=3, reply_term=9),
+                           dict(slot=0, peer=2, args_term=4, args_last_included_index=3, reply_term=4)],
+                    expect={"flags": [4, 0], "slot0": dict(current_term=9, state=FOLLOWER),
+                            "persist": {"0": 1}}))
+    # P10: a stale RequestVote still persists (deferred, :57)
+    out.append(rv_kat("P10", dict(term=6, voted=2, terms=[0, 1]), dict(term=4, last_term=9, last_idx=9),
+                      f"{el}:57-62", dict(term=6, vote_granted=0), dict(voted_for=2, current_term=6)))
+    out[-1]["expect"]["persist"] = {"1": 1}
+    return out
 
 
 def run_py(k):
@@ -182,6 +259,28 @@ def run_py(k):
                                   po.RequestVoteReply(Term=it["reply_term"],
                                                       VoteGranted=bool(it["vote_granted"]))))
         out["flags"] = flags
+    elif k["op"] == "handle_install_snapshot":
+        a = k["args"][0]
+        rep = po.InstallSnapshotReply()
+        rafts[a["slot"]].HandleInstallSnapshot(po.InstallSnapshotArgs(
+            Term=a["term"], LeaderId=a["leader_id"], LastIncludedIndex=a["last_included_index"],
+            LastIncludedTerm=a["last_included_term"]), rep)
+        out["is_reply"] = rep.Term
+    elif k["op"] == "snapshot":
+        for s_, x in zip(k["slots"], k["index"]):
+            rafts[s_].Snapshot(x)
+    elif k["op"] == "start":
+        out["start"] = [list(rafts[s_].Start()) for s_ in k["slots"]]
+    elif k["op"] == "process_install_snapshot_replies":
+        flags = []
+        for it in k["items"]:
+            rf = rafts[it["slot"]]
+            flags.append(rf.processInstallSnapshotReply(
+                it["peer"], po.InstallSnapshotArgs(Term=it["args_term"], LeaderId=rf.me,
+                                                   LastIncludedIndex=it["args_last_included_index"],
+                                                   LastIncludedTerm=0),
+                po.InstallSnapshotReply(Term=it["reply_term"])))
+        out["flags"] = flags
     out["state"] = po.to_soa(rafts, st, G, P, L)
     return out
 
@@ -197,7 +296,14 @@ def check_kat(k, out):
     if "reply" in e:
         for f, v in e["reply"].items():
             assert out["reply"][f] == v, (k["name"], f, out["reply"][f], v)
-    for key, slot in (("slot1", 1), ("slot0", 0)):
+    if "is_reply" in e:
+        assert out["is_reply"] == e["is_reply"], (k["name"], out["is_reply"], e["is_reply"])
+    if "start" in e:
+        assert [list(x) for x in out["start"]] == e["start"], (k["name"], out["start"], e["start"])
+    for s_, v in e.get("persist", {}).items():
+        assert st["persist_dirty"][int(s_)] == v, (k["name"], "persist_dirty", s_,
+                                                   st["persist_dirty"][int(s_)], v)
+    for key, slot in (("slot1", 1), ("slot0", 0), ("slot2", 2)):
         for f, v in e.get(key, {}).items():
             if f == "log":
                 got = list(st["log_term"][slot * L: slot * L + len(v)])

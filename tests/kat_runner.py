@@ -7,7 +7,7 @@ import os
 
 import numpy as np
 
-from multiraft_amd._abi import AE_ARGS, AE_RESULT, RV_ARGS, RV_RESULT
+from multiraft_amd._abi import AE_ARGS, AE_RESULT, IS_ARGS, IS_RESULT, RV_ARGS, RV_RESULT
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -18,7 +18,9 @@ def load_kats():
 
 
 def kat_state(k):
-    return {kk: np.array(v, dtype=np.int32) for kk, v in k["state"].items()}
+    st = {kk: np.array(v, dtype=np.int32) for kk, v in k["state"].items()}
+    st.setdefault("persist_dirty", np.zeros(k["G"] * k["P"], np.int32))
+    return st
 
 
 def _rec(dtype, rows):
@@ -50,6 +52,22 @@ def run_kat(k, eng, store):
     elif k["op"] == "process_vote_replies":
         flags, err = eng.process_vote_replies(_rec(RV_RESULT, k["items"]),
                                               np.array([0, len(k["items"])], dtype=np.int64))
+        assert not err.any(), err
+        out["flags"] = flags.tolist()
+    elif k["op"] == "handle_install_snapshot":
+        rep, _, err = eng.handle_install_snapshot(_rec(IS_ARGS, k["args"]))
+        assert not err.any(), err
+        out["is_reply"] = int(rep["term"][0])
+    elif k["op"] == "snapshot":
+        err = eng.snapshot(np.array(k["slots"], np.int32), np.array(k["index"], np.int32))
+        assert not err.any(), err
+    elif k["op"] == "start":
+        idx, term, isl, err = eng.start(np.array(k["slots"], np.int32))
+        assert not err.any(), err
+        out["start"] = [[int(a), int(b), int(c)] for a, b, c in zip(idx, term, isl)]
+    elif k["op"] == "process_install_snapshot_replies":
+        flags, err = eng.process_install_snapshot_replies(
+            _rec(IS_RESULT, k["items"]), np.array([0, len(k["items"])], dtype=np.int64))
         assert not err.any(), err
         out["flags"] = flags.tolist()
     out["state"] = store()

@@ -8,7 +8,7 @@ import os
 import numpy as np
 
 from multiraft_amd._abi import (AE_ARGS, AE_REPLY, AE_RESULT, IS_ARGS, IS_REPLY, IS_RESULT,
-                                RV_ARGS, RV_REPLY, RV_RESULT, MraftSoa, ptr, soa_of)
+                                PERSISTENT, RV_ARGS, RV_REPLY, RV_RESULT, MraftSoa, ptr, soa_of)
 from multiraft_amd.engine import copy_state
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -47,6 +47,9 @@ def lib():
             "ora_gather_install_snapshot_args": [E, vp, vp, i64, vp, vp],
             "ora_handle_install_snapshot": [E, vp, i64, vp, vp, vp],
             "ora_process_install_snapshot_replies": [E, vp, i64, vp, i64, vp, vp],
+            "ora_collect_persist": [E, vp],
+            "ora_read_persistent": [E, vp, i64, vp, vp, i64],
+            "ora_restore": [E, vp, i64, vp, i64, vp],
         }
         for n, a in sigs.items():
             f = getattr(l, n)
@@ -204,6 +207,30 @@ class Oracle:
         gf = np.zeros(self.G, np.int32)
         lib().ora_election_rounds(ctypes.byref(self._e), ptr(m), m.shape[0], ptr(gf))
         return gf
+
+    # ---- persistence ---------------------------------------------------------
+    def collect_persist(self):
+        out = np.zeros(self.G * self.P, np.int32)
+        lib().ora_collect_persist(ctypes.byref(self._e), ptr(out))
+        return out
+
+    def read_persistent(self, slots):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        n = len(slots)
+        hdr = np.zeros(n, dtype=PERSISTENT)
+        cap = max(1, n * self.L)
+        terms = np.zeros(cap, np.int32)
+        rc = lib().ora_read_persistent(ctypes.byref(self._e), ptr(slots), n, ptr(hdr), ptr(terms), cap)
+        assert rc == 0
+        used = int((hdr["last_index"] - hdr["dummy_index"] + 1).sum()) if n else 0
+        return hdr, terms[:used].copy()
+
+    def restore(self, hdr, terms):
+        hdr = np.ascontiguousarray(hdr, dtype=PERSISTENT)
+        terms = np.ascontiguousarray(terms, dtype=np.int32)
+        err = np.zeros(len(hdr), np.int32)
+        lib().ora_restore(ctypes.byref(self._e), ptr(hdr), len(hdr), ptr(terms), len(terms), ptr(err))
+        return err
 
     def export_group_status(self, leader_peer=None):
         commit = np.zeros(self.G, dtype=np.int32)

@@ -19,7 +19,13 @@ Mapping to the reference:
   * the applier (raft.go:153-203) feeds cfg.logs with the same checks as
     config.go:144-163 (same index => same command; in-order apply);
   * one(), checkOneLeader(), nCommitted() follow config.go:569-622, 438-468,
-    502-524.
+    502-524;
+  * persistence (2C): after every batch of engine calls the replicas the
+    engine marked persist_dirty are saved to a per-server Persister
+    (multiraft_amd.persister, persister.go); crash1 / start1
+    (config.go:112-142, 283-340) kill a server and restart it with Make +
+    readPersist from its last persisted bytes (mraft_restore). A replica
+    whose state changed without a persist mark would lose that change here.
 Commands never enter the engine: the harness keeps each server's commands
 index-aligned with its log (the host side of the boundary, include/mraft.h).
 """
@@ -30,6 +36,7 @@ import numpy as np
 from multiraft_amd._abi import (AE_RESULT, F_BECAME_LEADER, F_NEED_MORE, F_STEPPED_DOWN, FOLLOWER,
                                 LEADER, RV_ARGS, RV_RESULT)
 from multiraft_amd.engine import new_state
+from multiraft_amd.persister import Persister, flush_persist, restart
 
 TICK_MS = 10
 HEARTBEAT = 9          # ticks
@@ -57,6 +64,9 @@ class Cluster:
         self.logs = [dict() for _ in range(P)]      # cfg.logs: applied index -> cmd
         self.max_index = 0
         self.rpcs = 0
+        self.alive = [True] * P                     # cfg.rafts[i] != nil
+        self.persister = Persister(P)               # cfg.saved
+        self.saved_cmds = [dict() for _ in range(P)]  # commands persisted beside the raft state
         self.st = self.eng.store_state()
 
     # ---- helpers ---------------------------------------------------------
@@ -73,7 +83,29 @@ class Cluster:
         return int(self.st["current_term"][p])
 
     def _link(self, a, b):
-        return self.connected[a] and self.connected[b]
+        return self.connected[a] and self.connected[b] and self.alive[a] and self.alive[b]
+
+    def _flush(self):
+        """The persist() call sites of the last batch, saved (persister.go)."""
+        for p in flush_persist(self.eng, self.persister):
+            self.saved_cmds[int(p)] = dict(self.cmds[int(p)])
+
+    def crash1(self, p):
+        """config.go:112-142: disconnect, kill; the persisted bytes survive."""
+        self.disconnect(p)
+        self.alive[p] = False
+
+    def start1(self, p):
+        """config.go:283-340: crash1, then Make + readPersist from the saved
+        state; the server stays disconnected until connect()."""
+        self.crash1(p)
+        err = restart(self.eng, self.persister, [p])
+        assert not err.any(), err
+        self.cmds[p] = dict(self.saved_cmds[p])
+        self.alive[p] = True
+        self.elec[p] = self._etimeout()
+        self.hb[p] = 0
+        self._refresh()
 
     def connect(self, p):
         self.connected[p] = True
@@ -84,13 +116,17 @@ class Cluster:
     # ---- Raft API mirror --------------------------------------------------
     def start(self, p, cmd):
         """Raft.Start (raft.go:90-104) on server p."""
+        if not self.alive[p]:
+            return -1, -1, False
         idx, term, isl, err = self.eng.start(np.array([p], np.int32))
         assert not err.any(), err
         if not isl[0]:
             return -1, -1, False
         self.cmds[p][int(idx[0])] = cmd
+        self._flush()
         self._refresh()
         self._replicate([p])  # BroadcastAppend(Append)
+        self._flush()
         return int(idx[0]), int(term[0]), True
 
     def get_state(self, p):
@@ -103,16 +139,18 @@ class Cluster:
         self._refresh()
         cands = []
         for p in range(self.P):
-            if self.now >= self.elec[p]:
+            if self.alive[p] and self.now >= self.elec[p]:
                 self.elec[p] = self._etimeout()
                 if self.role(p) != LEADER:
                     cands.append(p)
         if cands:
             self._election(cands)
         self._refresh()
-        leaders = [p for p in range(self.P) if self.role(p) == LEADER and self.now >= self.hb[p]]
+        leaders = [p for p in range(self.P)
+                   if self.alive[p] and self.role(p) == LEADER and self.now >= self.hb[p]]
         if leaders:
             self._replicate(leaders)
+        self._flush()
         self._apply()
 
     def advance(self, ticks):
@@ -227,6 +265,8 @@ class Cluster:
     def _apply(self):
         fr, to = self.eng.collect_apply()
         for p in range(self.P):
+            if not self.alive[p]:
+                continue
             for i in range(int(fr[p]), int(to[p]) + 1):
                 cmd = self.cmds[p].get(i)
                 for q in range(self.P):
@@ -254,7 +294,7 @@ class Cluster:
             self._refresh()
             leaders = {}
             for p in range(self.P):
-                if self.connected[p] and self.role(p) == LEADER:
+                if self.connected[p] and self.alive[p] and self.role(p) == LEADER:
                     leaders.setdefault(self.term(p), []).append(p)
             last = -1
             for t, ls in leaders.items():
@@ -283,7 +323,7 @@ class Cluster:
             index = -1
             for _ in range(self.P):
                 starts = (starts + 1) % self.P
-                if self.connected[starts]:
+                if self.connected[starts] and self.alive[starts]:
                     idx, _, ok = self.start(starts, cmd)
                     if ok:
                         index = idx
@@ -435,6 +475,133 @@ def backup_2b(mk, seed=7):                           # test_test.go:503-573
     cfg.one(cmd(), 5, True)
 
 
+def wait(cfg, index, n, start_term):               # config.go:535-566
+    to = 1
+    for _ in range(30):
+        nd, _ = cfg.n_committed(index)
+        if nd >= n:
+            break
+        cfg.advance(to)
+        to = min(to * 2, 100)
+        if start_term > -1:
+            for p in range(cfg.P):
+                t, _ = cfg.get_state(p)
+                if t > start_term:
+                    return -1
+    nd, cmd = cfg.n_committed(index)
+    if nd < n:
+        raise HarnessFailure(f"only {nd} decided for index {index}; wanted {n}")
+    return cmd
+
+
+def persist1_2c(mk, seed=8):                         # test_test.go:685-729
+    servers = 3
+    cfg = Cluster(mk, servers, seed=seed)
+    cfg.one(11, servers, True)
+    for i in range(servers):                         # crash and re-start all
+        cfg.start1(i)
+    for i in range(servers):
+        cfg.disconnect(i)
+        cfg.connect(i)
+    cfg.one(12, servers, True)
+    leader1 = cfg.check_one_leader()
+    cfg.disconnect(leader1)
+    cfg.start1(leader1)
+    cfg.connect(leader1)
+    cfg.one(13, servers, True)
+    leader2 = cfg.check_one_leader()
+    cfg.disconnect(leader2)
+    cfg.one(14, servers - 1, True)
+    cfg.start1(leader2)
+    cfg.connect(leader2)
+    wait(cfg, 4, servers, -1)                        # leader2 joins before i3 is killed
+    i3 = (cfg.check_one_leader() + 1) % servers
+    cfg.disconnect(i3)
+    cfg.one(15, servers - 1, True)
+    cfg.start1(i3)
+    cfg.connect(i3)
+    cfg.one(16, servers, True)
+
+
+def persist2_2c(mk, seed=9):                         # test_test.go:731-775
+    servers = 5
+    cfg = Cluster(mk, servers, seed=seed)
+    index = 1
+    for _ in range(5):
+        cfg.one(10 + index, servers, True)
+        index += 1
+        leader1 = cfg.check_one_leader()
+        cfg.disconnect((leader1 + 1) % servers)
+        cfg.disconnect((leader1 + 2) % servers)
+        cfg.one(10 + index, servers - 2, True)
+        index += 1
+        for k in (0, 3, 4):
+            cfg.disconnect((leader1 + k) % servers)
+        cfg.start1((leader1 + 1) % servers)
+        cfg.start1((leader1 + 2) % servers)
+        cfg.connect((leader1 + 1) % servers)
+        cfg.connect((leader1 + 2) % servers)
+        cfg.advance(RAFT_ELECTION_TIMEOUT)
+        cfg.start1((leader1 + 3) % servers)
+        cfg.connect((leader1 + 3) % servers)
+        cfg.one(10 + index, servers - 2, True)
+        index += 1
+        cfg.connect((leader1 + 4) % servers)
+        cfg.connect((leader1 + 0) % servers)
+    cfg.one(1000, servers, True)
+
+
+def persist3_2c(mk, seed=10):                        # test_test.go:777-806
+    servers = 3
+    cfg = Cluster(mk, servers, seed=seed)
+    cfg.one(101, 3, True)
+    leader = cfg.check_one_leader()
+    cfg.disconnect((leader + 2) % servers)
+    cfg.one(102, 2, True)
+    cfg.crash1((leader + 0) % servers)
+    cfg.crash1((leader + 1) % servers)
+    cfg.connect((leader + 2) % servers)
+    cfg.start1((leader + 0) % servers)
+    cfg.connect((leader + 0) % servers)
+    cfg.one(103, 2, True)
+    cfg.start1((leader + 1) % servers)
+    cfg.connect((leader + 1) % servers)
+    cfg.one(104, servers, True)
+
+
+def figure8_2c(mk, seed=11, iters=150):             # test_test.go:817-871 (1000 iterations there)
+    servers = 5
+    rng = np.random.default_rng(seed)
+    cfg = Cluster(mk, servers, seed=seed)
+    cfg.one(int(rng.integers(1, 1 << 30)), 1, True)
+    nup = servers
+    for _ in range(iters):
+        leader = -1
+        for i in range(servers):
+            if cfg.alive[i]:
+                _, _, ok = cfg.start(i, int(rng.integers(1, 1 << 30)))
+                if ok:
+                    leader = i
+        if rng.integers(0, 1000) < 100:
+            cfg.advance(int(rng.integers(0, RAFT_ELECTION_TIMEOUT // 2)) + 1)
+        else:
+            cfg.advance(int(rng.integers(0, 13)) // TICK_MS + 1)
+        if leader != -1:
+            cfg.crash1(leader)
+            nup -= 1
+        if nup < 3:
+            s_ = int(rng.integers(0, servers))
+            if not cfg.alive[s_]:
+                cfg.start1(s_)
+                cfg.connect(s_)
+                nup += 1
+    for i in range(servers):
+        if not cfg.alive[i]:
+            cfg.start1(i)
+            cfg.connect(i)
+    cfg.one(int(rng.integers(1, 1 << 30)), servers, True)
+
+
 SCENARIOS = {
     "InitialElection2A": initial_election_2a,
     "ReElection2A": re_election_2a,
@@ -443,4 +610,8 @@ SCENARIOS = {
     "FailNoAgree2B": fail_no_agree_2b,
     "Rejoin2B": rejoin_2b,
     "Backup2B": backup_2b,
+    "Persist12C": persist1_2c,
+    "Persist22C": persist2_2c,
+    "Persist32C": persist3_2c,
+    "Figure82C": figure8_2c,
 }

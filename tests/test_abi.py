@@ -32,11 +32,12 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_struct_sizes():
     lib = _abi.lib()
-    assert lib.mraft_abi_version() == 1
+    assert lib.mraft_abi_version() == _abi.ABI_VERSION == 2
     assert _abi.AE_ARGS.itemsize == 40
     assert _abi.AE_REPLY.itemsize == 16
     assert _abi.RV_RESULT.itemsize == 20
-    assert ctypes.sizeof(_abi.MraftSoa) == 11 * 8
+    assert ctypes.sizeof(_abi.MraftSoa) == 12 * 8
+    assert _abi.PERSISTENT.itemsize == 32
 
 
 def test_create_rejects_bad_dims_without_gpu():
@@ -45,3 +46,25 @@ def test_create_rejects_bad_dims_without_gpu():
     assert lib.mraft_create(0, 5, 16, 0, 0, ctypes.byref(h)) == _abi.E_INVAL
     assert lib.mraft_create(4, 9, 16, 0, 0, ctypes.byref(h)) == _abi.E_INVAL
     assert b"bad dims" in lib.mraft_last_error_string()
+
+
+def test_persistent_codec_round_trip_host_only():
+    """mraft_encode_persistent / mraft_decode_persistent are host code: they
+    run without a GPU. Round trip, exact size, and malformed-buffer rejection."""
+    import numpy as np
+    from multiraft_amd import decode_persistent, encode_persistent
+    from multiraft_amd.engine import MraftError
+    rec = {"current_term": 7, "voted_for": -1, "dummy_index": 40, "last_index": 44}
+    terms = np.array([3, 3, 5, 7, 7], np.int32)
+    b = encode_persistent(rec, terms)
+    assert len(b) == 36 + 8 * 5 and b[:4] == b"MRPS"
+    r, t = decode_persistent(b)
+    assert (int(r["current_term"]), int(r["voted_for"]), int(r["dummy_index"]),
+            int(r["last_index"])) == (7, -1, 40, 44)
+    assert t.tolist() == terms.tolist()
+    for bad in (b[:-1], b"XRPS" + b[4:], b[:32] + (6).to_bytes(4, "little") + b[36:]):
+        try:
+            decode_persistent(bad)
+        except MraftError:
+            continue
+        raise AssertionError("malformed buffer accepted")

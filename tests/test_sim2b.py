@@ -32,3 +32,14 @@ def test_scenario_oracle(name, seed):
 @pytest.mark.parametrize("name", list(SCENARIOS))
 def test_scenario_gpu(name):
     SCENARIOS[name](_gpu)
+
+
+def test_persistence_is_load_bearing(monkeypatch):
+    """Without the persist_dirty flushes, a crash of every server loses
+    committed entries and Persist12C must fail the reference's agreement
+    check (config.go:144-163): the 2C scenarios above really restart from
+    the persisted state."""
+    import sim2b
+    monkeypatch.setattr(sim2b.Cluster, "_flush", lambda self: None)
+    with pytest.raises(AssertionError):
+        sim2b.persist1_2c(_oracle, seed=1)
