@@ -1,8 +1,8 @@
 // mraft_elect.hip — the election storm (SURVEY.md §8a rows a5-a6, §8d
-// config #5) for gfx950: one lane per group; the P replicas' election state
-// (term, votedFor, role, grantedVotes, last index/term) lives in registers for
-// all R rounds of one launch, so HBM is touched once on entry and once on
-// exit. Per round: timeouts -> StartElection (raft_election.go:4-15) in peer
+// config #5) for gfx950: one lane per replica, eight lanes per group (eight
+// groups per wave); each replica's election state (term, votedFor, role,
+// grantedVotes, last index/term) lives in registers for all R rounds of one
+// launch, so HBM is touched once on entry and once on exit. Per round: timeouts -> StartElection (raft_election.go:4-15) in peer
 // order, every RequestVote delivered voter by voter in candidate order
 // (HandleRequestVote :54-77 with isLogUpToDate, raft_log.go:99-104), every
 // candidate's tally in voter order (closure :22-47).
@@ -13,112 +13,152 @@ namespace mraft {
 
 namespace {
 
+#ifndef MRAFT_EL_CX_LDS
+#define MRAFT_EL_CX_LDS 1  // candidate broadcast through LDS (else __shfl)
+#endif
+#ifndef MRAFT_EL_GM_LDS
+#define MRAFT_EL_GM_LDS 0  // grant-mask transpose through LDS (else __shfl; measured faster)
+#endif
+
 template <int P>
 __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *__restrict__ cand,
                                                          int R, int32_t *__restrict__ gflags) {
-  const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (g >= s.G) return;
-  const long long b = (long long)g * P;
-  int term[P], voted[P], role[P], votes[P], last[P], lterm[P], became[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    term[p] = s.term[b + p];
-    voted[p] = s.voted[b + p];
-    role[p] = s.role[b + p];
-    votes[p] = s.votes[b + p];
-    last[p] = s.last[b + p];
-    became[p] = 0;
+  // Lane p of an 8-lane segment holds replica p of group g (P <= 8): voters
+  // and candidates work in parallel, candidate data is broadcast inside the
+  // segment (__shfl width 8).
+  const int tid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int g = tid >> 3, p = tid & 7;
+  const bool grp = g < s.G;  // uniform over the segment
+  const bool act = grp && p < P;
+  const long long sl = (long long)g * P + p;
+  int term = 0, voted = -1, role = kFollower, votes = 0, last = 0, lterm = 0;
+  if (act) {
+    term = s.term[sl];
+    voted = s.voted[sl];
+    role = s.role[sl];
+    votes = s.votes[sl];
+    last = s.last[sl];
+    lterm = s.log[sl * s.L + (last - s.dummy[sl])];                    // lastEntry, raft_log.go:50-53
   }
+  // The logs do not change during an election storm, so isLogUpToDate of
+  // every candidate's (lastTerm, lastIndex) against this voter's
+  // (raft_log.go:99-104) is fixed for the launch: bit c of upm.
+  int upm = 0;
 #pragma unroll
-  for (int p = 0; p < P; ++p) lterm[p] = s.log[(b + p) * s.L + (last[p] - s.dummy[b + p])];  // lastEntry
-  int fl = 0, pdm = 0;  // pdm: replicas that ran persist() (StartElection :15, HandleRequestVote :57)
+  for (int c = 0; c < P; ++c) {
+    const int clt = __shfl(lterm, c, 8), clast = __shfl(last, c, 8);
+    upm |= (int)(clt > lterm || (clt == lterm && clast >= last)) << c;
+  }
+  __shared__ int lds_cx[256];
+  __shared__ __attribute__((aligned(8))) uint8_t lds_gm[256];
+  int fl = 0, became = 0, pd = 0;  // pd: persist() ran (StartElection :15, HandleRequestVote :57, :45)
+  int mnext = (grp && R > 0) ? (int)cand[g] : 0;  // round masks are fetched one round ahead
   for (int r = 0; r < R; ++r) {
-    const int m = cand[(long long)r * s.G + g];
-    int isc[P], at[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p) {                                      // StartElection :6-17
-      isc[p] = ((m >> p) & 1) && role[p] != kLeader;
-      if (isc[p]) {
-        pdm |= 1 << p;
-        role[p] = kCandidate;
-        term[p] += 1;
-        voted[p] = p;
-        votes[p] = 1;
-      }
-      at[p] = term[p];
+    const int m = mnext;
+    if (grp && r + 1 < R) mnext = (int)cand[(long long)(r + 1) * s.G + g];
+    const int isc = act && ((m >> p) & 1) && role != kLeader;
+    if (isc) {                                                         // StartElection :6-17
+      role = kCandidate;
+      term += 1;
+      voted = p;
+      votes = 1;
+      pd = 1;
     }
-    int rt[P][P], rg[P][P];  // reply of voter v to candidate c
+    const int at = term;  // args.Term of this lane's RequestVote (when isc); voter's term before RVs
+    // One broadcast per replica per round, through this wave's LDS words: its
+    // term with the candidate bit on top.
+    int cx[8];
+    const int mycx = (int)((unsigned)at | ((unsigned)isc << 31));
+    if (MRAFT_EL_CX_LDS) {
+      lds_cx[threadIdx.x] = mycx;
+      __builtin_amdgcn_wave_barrier();
+      const int4 a = *reinterpret_cast<const int4 *>(&lds_cx[threadIdx.x & ~7u]);
+      const int4 b = *reinterpret_cast<const int4 *>(&lds_cx[(threadIdx.x & ~7u) + 4]);
+      cx[0] = a.x; cx[1] = a.y; cx[2] = a.z; cx[3] = a.w;
+      cx[4] = b.x; cx[5] = b.y; cx[6] = b.z; cx[7] = b.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) cx[c] = c < P ? __shfl(mycx, c, 8) : 0;
+    }
+    // RequestVote deliveries: voter p handles the candidates in peer order
+    // (HandleRequestVote :54-77). pmx = max args.Term over candidates c <= p,
+    // which with the voter's own pre-delivery term gives every reply.Term the
+    // tally below needs (a voter's term after handling c is the max of the
+    // two, the stale branch included).
+    int gm = 0, pmx = INT32_MIN;
+#pragma unroll
+    for (int c = 0; c < P; ++c) {  // branch-free: every step is a select
+      const bool cisc = cx[c] < 0;
+      const int cat = cx[c] & 0x7fffffff;
+      pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
+      const bool h = act && cisc && c != p;                            // this voter handles c's RV
+      pd |= (int)h;
+      const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
+      const bool gt = h && cat > term;                                 // :63-66
+      term = gt ? cat : term;
+      role = gt ? kFollower : role;
+      voted = gt ? -1 : voted;
+      const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
+      voted = grant ? c : voted;
+      gm |= (int)grant << c;
+    }
+    // Grants transposed through LDS: byte v of the segment's word = voter v's
+    // grant mask; bit v of mine = voter v granted this lane.
+    int mine = 0;
+    if (MRAFT_EL_GM_LDS) {
+      lds_gm[threadIdx.x] = (uint8_t)gm;
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long gw = *reinterpret_cast<const unsigned long long *>(&lds_gm[threadIdx.x & ~7u]);
+      mine = (int)((((gw >> p) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (int v = 0; v < P; ++v) mine |= ((__shfl(gm, v, 8) >> p) & 1) << v;
+    }
+    // Tally (closure :22-47): candidate p folds its replies in voter order.
 #pragma unroll
     for (int v = 0; v < P; ++v) {
-#pragma unroll
-      for (int c = 0; c < P; ++c) {
-        rt[c][v] = 0;
-        rg[c][v] = 0;
-        if (!isc[c] || c == v) continue;
-        pdm |= 1 << v;
-        if (at[c] < term[v]) {                                         // :59-62
-          rt[c][v] = term[v];
-          continue;
-        }
-        if (at[c] > term[v]) {                                         // :63-66
-          role[v] = kFollower;
-          term[v] = at[c];
-          voted[v] = -1;
-        }
-        rt[c][v] = term[v];                                            // :67
-        const bool up = lterm[c] > lterm[v] || (lterm[v] == lterm[c] && last[c] >= last[v]);
-        if ((voted[v] == -1 || voted[v] == c) && up) {                 // :69-74
-          voted[v] = c;
-          rg[c][v] = 1;
-        }
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < P; ++c) {                                      // tally :24-47
-      if (!isc[c]) continue;
-#pragma unroll
-      for (int v = 0; v < P; ++v) {
-        if (v == c) continue;
-        if (term[c] == at[c] && role[c] == kCandidate) {               // :29
-          if (rg[c][v]) {
-            votes[c] += 1;                                             // :31
-            if (votes[c] > P / 2) {                                    // :32-38
-              role[c] = kLeader;
-              became[c] = 1;
-              fl |= MRAFT_G_ELECTED;
-            }
-          } else if (rt[c][v] > term[c]) {                             // :42-45
-            role[c] = kFollower;
-            term[c] = rt[c][v];
-            voted[c] = -1;
-            fl |= MRAFT_G_STEPPED_DOWN;
-          }
-        }
-      }
+      const bool ok = isc && v != p && term == at && role == kCandidate;  // :29
+      const bool gr = ok && ((mine >> v) & 1);                         // :30
+      votes += (int)gr;                                                // :31
+      const bool lead = gr && votes > P / 2;                           // :32-38
+      role = lead ? kLeader : role;
+      became |= (int)lead;
+      fl |= lead ? MRAFT_G_ELECTED : 0;
+      const int rt = max(cx[v] & 0x7fffffff, pmx);                     // voter v's reply.Term
+      const bool sd = ok && !gr && rt > term;                          // :42-45
+      role = sd ? kFollower : role;
+      term = sd ? rt : term;
+      voted = sd ? -1 : voted;
+      fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
     }
   }
+  const unsigned long long el = __ballot(fl & MRAFT_G_ELECTED), sd = __ballot(fl & MRAFT_G_STEPPED_DOWN);
+  const int seg = (int)(threadIdx.x & 63) & ~7;
+  if (grp && p == 0 && gflags) {
+    gflags[g] = (((el >> seg) & 0xffull) ? MRAFT_G_ELECTED : 0) |
+                (((sd >> seg) & 0xffull) ? MRAFT_G_STEPPED_DOWN : 0);
+  }
+  if (!act) return;
+  s.term[sl] = term;
+  s.voted[sl] = voted;
+  s.role[sl] = role;
+  s.votes[sl] = votes;
+  if (pd) mark_persist(s, sl, MRAFT_PERSIST_STATE);
+  if (became) {
 #pragma unroll
-  for (int p = 0; p < P; ++p) {
-    s.term[b + p] = term[p];
-    s.voted[b + p] = voted[p];
-    s.role[b + p] = role[p];
-    s.votes[b + p] = votes[p];
-    if ((pdm >> p) & 1) mark_persist(s, b + p, MRAFT_PERSIST_STATE);
-    if (became[p]) {
-      for (int j = 0; j < P; ++j) {
-        s.match[(b + p) * P + j] = 0;
-        s.next[(b + p) * P + j] = last[p] + 1;
-      }
+    for (int j = 0; j < P; ++j) {
+      s.match[sl * P + j] = 0;
+      s.next[sl * P + j] = last + 1;
     }
   }
-  if (gflags) gflags[g] = fl;
 }
 
 }  // namespace
 
 void launch_election_rounds(const Dev &s, const uint8_t *cand, int R, int32_t *gflags,
                             hipStream_t st) {
-  const dim3 gr((s.G + 255) / 256), bl(256);
+  const dim3 gr((unsigned)(((long long)s.G * 8 + 255) / 256)), bl(256);
   switch (s.P) {
 #define MRAFT_EL_CASE(PP) \
   case PP: hipLaunchKernelGGL(k_election_rounds<PP>, gr, bl, 0, st, s, cand, R, gflags); break;
