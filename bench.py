@@ -68,14 +68,21 @@ def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gs)
     threads = max(1, min(16, os.cpu_count() or 1))
 
+    o = Oracle(Gs, P, L, st)
+
     def run(nt, budget):
-        done, spent = 0, 0.0
-        while spent < budget:
-            o = Oracle(Gs, P, L, st)  # fresh copy, untimed
+        done, spent, w0, last = 0, 0.0, time.perf_counter(), time.perf_counter()
+        # bounded in tick time AND in wall time (the untimed restores count there)
+        while spent < budget and time.perf_counter() - w0 < 3 * budget + 10:
+            for k, v in st.items():  # restore the pristine state in place, untimed
+                np.copyto(o.st[k], v)
             t = time.perf_counter()
             o.replicate_tick(lp, nthreads=nt)
             spent += time.perf_counter() - t
             done += Gs
+            if time.perf_counter() - last > 20:
+                last = time.perf_counter()
+                log(rank, f"cpu baseline ({nt} threads): {done} decisions in {spent:.1f} s so far")
         return done / spent, done, spent
 
     v1, d1, s1 = run(1, min(3.0, budget_s / 4))

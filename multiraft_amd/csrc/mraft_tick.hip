@@ -1,6 +1,8 @@
 // mraft_tick.hip — the fused co-resident replication tick (SURVEY.md §8a rows
-// a1-a4) for gfx950: one 64-lane wave per Raft group, four groups per
-// 256-thread workgroup.
+// a1-a4) for gfx950: one 64-lane wave per Raft group, one group per 64-thread
+// workgroup (a wave's slot is released the moment its group is done; with
+// 4-wave workgroups a finished wave held its slot until its siblings ended,
+// idling ~18 % of the slots — tools/trace_tick.py).
 //
 // Per group (wave):
 //   header   wave-uniform scalar loads of the leader replica (role, term,
@@ -420,12 +422,27 @@ struct Fold {
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
 #endif
+#ifndef MRAFT_TICK_TRACE
+#define MRAFT_TICK_TRACE 0  // diagnostic build: s_memrealtime stamps per group (tools/trace_tick.py)
+#endif
+#if MRAFT_TICK_TRACE
+__device__ unsigned long long g_tick_trace[65536 * 4];
+#define TICK_STAMP(k)                                                                        \
+  do {                                                                                       \
+    if (!COUNT && g < 65536 && lane == 0) g_tick_trace[g * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define TICK_STAMP(k) do {} while (0)
+#endif
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
+#ifndef MRAFT_TICK_WPB
+#define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
+#endif
 
 template <int P, bool COUNT>
-__global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
+__global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
                                                     int32_t *__restrict__ gflags,
                                                     unsigned long long *__restrict__ counts) {
   constexpr int NI = P - 1;
@@ -440,9 +457,10 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
     const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
     gb = x * per + min(x, rem) + (gb >> 3);
   }
-  const int g = uni(gb * 4 + (int)(threadIdx.x >> 6));
+  const int g = uni(gb * MRAFT_TICK_WPB + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
   const int L = s.L;
+  TICK_STAMP(0);
 
   // ------------------------------------------------------------ header
   const int lp = uni(leader_peer[g]);
@@ -618,6 +636,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
     }
   }
   int fullmask = 0, found = -1;
+  TICK_STAMP(1);
   if (MRAFT_TICK_EXP == 0 && (merge_m || slo <= shi)) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
@@ -646,6 +665,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
       copy_loop<NI, VC, false, COUNT>(s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
     }
   }
+  TICK_STAMP(2);
   int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
@@ -762,6 +782,7 @@ __global__ __launch_bounds__(256, MRAFT_TICK_MINW) void k_tick_group(Dev s, cons
       if (commit != c0) s.commit[ld] = commit;
       if (gflags) gflags[g] = flags;
     }
+    TICK_STAMP(3);
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       const int pq = q < lp ? q : q + 1;
@@ -839,8 +860,8 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
 template <int P, bool COUNT>
 void launch_tick_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
                    hipStream_t st) {
-  const int blocks = (s.G + 3) / 4;
-  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(256), 0, st, s, lpeer, gflags,
+  const int blocks = (s.G + MRAFT_TICK_WPB - 1) / MRAFT_TICK_WPB;
+  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), 0, st, s, lpeer, gflags,
                      counts);
 }
 
@@ -864,6 +885,14 @@ void launch_tick_c(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned
 }
 
 }  // namespace
+
+#if MRAFT_TICK_TRACE
+extern "C" int mraft_debug_tick_trace(void *dst, long long nbytes) {
+  if (nbytes > (long long)sizeof(g_tick_trace)) nbytes = sizeof(g_tick_trace);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_tick_trace), (size_t)nbytes, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -3;
+}
+#endif
 
 void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, hipStream_t st) {
   launch_tick_c<false>(s, lpeer, gflags, nullptr, st);
