@@ -459,6 +459,20 @@ int64_t mraft_encode_persistent(const mraft_persistent *in, const int32_t *terms
 int mraft_decode_persistent(const uint8_t *buf, int64_t len, mraft_persistent *out,
                             int32_t *terms, int64_t terms_cap);
 
+/* ---- shard router (host-only) ---------------------------- */
+
+/* key2shard (src/shardkv/client.go:22-29): first byte of the key modulo
+ * nshards (0 for an empty key). Returns the shard, or MRAFT_E_INVAL. */
+int mraft_key2shard(const char *key, int64_t len, int32_t nshards);
+
+/* Config.ReAllocGID (src/shardctrler/common.go:87-132) in place: shards[s] is
+ * the gid serving shard s, gids the configured groups (Config.Groups keys).
+ * Shards of departed groups go to the least-loaded group, then shards move
+ * from the most- to the least-loaded group until the loads differ by at most
+ * one; ties break to the smallest gid (the reference sorts the keys), gid 0
+ * is the invalid group. Deterministic. */
+int mraft_realloc_gid(int32_t *shards, int32_t nshards, const int32_t *gids, int32_t ngroups);
+
 /* ---- read-out (GetState, raft.go:237-246) -------------------------------- */
 
 /* For each group g and its replica leader_peer[g] (or, with leader_peer NULL,

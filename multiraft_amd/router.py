@@ -1,4 +1,4 @@
-"""Host-side shard router view.
+"""Host-side shard router.
 
 Each rank owns a contiguous range of groups; once per tick the GetState words
 of every group (commitIndex, currentTerm<<1 | isLeader — mraft_export_group_status)
@@ -7,18 +7,81 @@ replacement for polling GetState()/commit progress
 (src/kvraft/server.go:114, src/shardkv/client.go:68-100). The collective is
 torch.distributed's all_gather_into_tensor: RCCL over xGMI for device tensors
 (backend "nccl"), gloo for host tensors (tests).
+
+The shard -> group assignment is the shard controller's Config
+(src/shardctrler/common.go:27-132), applied as its state machine does
+(server.go:124-162: Join / Leave / Move), with ReAllocGID and key2shard in
+the library's host code (mraft_realloc_gid, mraft_key2shard).
 """
 from __future__ import annotations
 
+import ctypes
+from dataclasses import dataclass, field
+
 import numpy as np
+
+from . import _abi
 
 NSHARDS = 10  # src/shardctrler/common.go:23
 
 
-def key2shard(key: str, nshards: int = NSHARDS) -> int:
+def key2shard(key, nshards: int = NSHARDS) -> int:
     """src/shardkv/client.go:22-29: first byte of the key modulo NShards."""
-    shard = ord(key[0]) if key else 0
-    return shard % nshards
+    b = key.encode() if isinstance(key, str) else bytes(key)
+    r = _abi.lib().mraft_key2shard(b, len(b), nshards)
+    if r < 0:
+        raise ValueError("nshards must be positive")
+    return r
+
+
+def realloc_gid(shards, gids):
+    """Config.ReAllocGID (common.go:87-132) on a copy: the new shard -> gid array."""
+    sh = np.ascontiguousarray(shards, dtype=np.int32).copy()
+    g = np.ascontiguousarray(sorted(gids), dtype=np.int32)
+    rc = _abi.lib().mraft_realloc_gid(sh.ctypes.data, len(sh), g.ctypes.data if len(g) else None, len(g))
+    if rc != _abi.OK:
+        raise ValueError("ReAllocGID has no valid group to assign (only gid 0 configured)")
+    return sh
+
+
+@dataclass
+class Config:
+    """shardctrler.Config (common.go:27-31)."""
+    num: int = 0
+    shards: np.ndarray = field(default_factory=lambda: np.zeros(NSHARDS, np.int32))
+    groups: dict = field(default_factory=dict)
+
+    def copy_next(self) -> "Config":                  # CopyConfig, common.go:33-44
+        return Config(self.num + 1, self.shards.copy(), dict(self.groups))
+
+
+class ShardCtrlerState:
+    """The shard controller's applied state machine (server.go:124-162,
+    StartServer :166-171): configs[0] has no groups, every shard on gid 0."""
+
+    def __init__(self, nshards: int = NSHARDS):
+        self.configs = [Config(0, np.zeros(nshards, np.int32), {})]
+
+    def join(self, servers: dict):                     # server.go:130-136
+        c = self.configs[-1].copy_next()
+        c.groups.update(servers)
+        c.shards = realloc_gid(c.shards, c.groups.keys())
+        self.configs.append(c)
+
+    def leave(self, gids):                             # :137-143
+        c = self.configs[-1].copy_next()
+        for g in gids:
+            c.groups.pop(g, None)
+        c.shards = realloc_gid(c.shards, c.groups.keys())
+        self.configs.append(c)
+
+    def move(self, shard: int, gid: int):              # :144-147
+        c = self.configs[-1].copy_next()
+        c.shards[shard] = gid
+        self.configs.append(c)
+
+    def query(self, num: int = -1) -> Config:          # Query(-1) = latest
+        return self.configs[-1] if num < 0 or num >= len(self.configs) else self.configs[num]
 
 
 def allgather_status(commit_local, term_leader_local):

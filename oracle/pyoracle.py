@@ -495,3 +495,49 @@ def _would_overflow(fr: Raft, args: AppendEntriesArgs, L: int) -> bool:
         if lg.convertIndex(e.Index) >= lg.len() or lg.getEntry(e.Index).Term != e.Term:
             return args.PrevLogIndex + len(args.Entries) - lg.dummyIndex() > L - 1
     return False
+
+
+# ---------------------------------------------------------------------------
+# Shard controller (src/shardctrler/common.go:53-132), for the router tests
+# ---------------------------------------------------------------------------
+
+def realloc_gid(shards, gids, nshards=10):
+    """Config.ReAllocGID restated on Python lists (g2s ordered by sorted gid,
+    as GetGIDWith{Minimum,Maximum}Shards iterate)."""
+    shards = list(shards)
+    if not gids:
+        return [0] * nshards
+    g2s = {g: [] for g in sorted(gids)}
+    for s, g in enumerate(shards):
+        if g != 0 and g in g2s:
+            g2s[g].append(s)
+
+    def gmin():
+        idx, mn = -1, nshards + 1
+        for g in sorted(g2s):
+            if g != 0 and len(g2s[g]) < mn:
+                idx, mn = g, len(g2s[g])
+        return idx
+
+    def gmax():
+        idx, mx = -1, -1
+        for g in sorted(g2s):
+            if len(g2s[g]) > mx:
+                idx, mx = g, len(g2s[g])
+        return idx
+
+    for i in range(nshards):
+        if shards[i] not in g2s:
+            g = gmin()
+            shards[i] = g
+            g2s[g].append(i)
+    while True:
+        src, tgt = gmax(), gmin()
+        if src != 0 and len(g2s[src]) - len(g2s[tgt]) <= 1:
+            break
+        g2s[tgt].append(g2s[src].pop(0))
+    out = [0] * nshards
+    for g, ss in g2s.items():
+        for s in ss:
+            out[s] = g
+    return out

@@ -15,6 +15,7 @@ for spec in "$@"; do
       $defs -c $f.hip -o build_$tag/$f.o 2>/dev/null &
   done
   g++ -O3 -std=c++17 -fPIC -c mraft_persist.cpp -o build_$tag/mraft_persist.o &
+  g++ -O3 -std=c++17 -fPIC -c mraft_router.cpp -o build_$tag/mraft_router.o &
   wait
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o
   rm -rf build_$tag
