@@ -417,7 +417,8 @@ struct Fold {
 #define MRAFT_TICK_VC 1    // dwordx4 vectors per lane in the copy-only loop
 #endif
 #ifndef MRAFT_TICK_EXP
-#define MRAFT_TICK_EXP 0   // traffic experiments only (wrong results): 1 = no pass, 2 = no pass, no scans
+#define MRAFT_TICK_EXP 0   // traffic experiments only (wrong results): 1 = no pass, 2 = no pass, no scans,
+                           // 3 = as 2 and no log[prev] / log[last] header loads
 #endif
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
@@ -513,9 +514,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     return;
   }
   int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = uni(s.log[lrow + (last - ldummy)]);             // speculative a1 probe
+  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + (last - ldummy)]);  // speculative a1 probe
   int prev_term = 0, ft = 0;
-  if (icls == IC_GO) {
+  if (icls == IC_GO && MRAFT_TICK_EXP != 3) {
     prev_term = s.log[lrow + (prev - ldummy)];                           // :49
     if (prev >= fdummy && prev <= flast) ft = s.log[f * L + (prev - fdummy)];
   }
@@ -566,7 +567,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   int scan_extra = 0;
   {
     unsigned long long m = __ballot(icls == IC_SCAN);
-    if (MRAFT_TICK_EXP == 2) m = 0;
+    if (MRAFT_TICK_EXP >= 2) m = 0;
     while (m) {
       const int src = first_lane(m);
       m &= m - 1;
