@@ -126,7 +126,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
+    ap.add_argument("--global-groups", type=int, default=0,
+                    help="fixed total split over the ranks instead (strong scaling; config #4 = 262144)")
     ap.add_argument("--peers", type=int, default=5)
     ap.add_argument("--log", type=int, default=4096, help="log capacity L")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -155,10 +157,13 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
-    from multiraft_amd.engine import export_group_status_into
     from multiraft_amd.router import allgather_status
 
     G, P, L, K, W = args.groups, args.peers, args.log, args.steps, args.warmup
+    if args.global_groups:
+        if args.global_groups % world:
+            raise SystemExit("--global-groups must be a multiple of the world size")
+        G = args.global_groups // world
     G_total = G * world
     seed = synth_seed(3)
     t = time.perf_counter()
@@ -213,10 +218,10 @@ def main():
         eng.bind(c)
         if timed:
             ev[i][0].record(stream)
-        eng.replicate_tick(lp_d, gf_d, where=DEVICE)
+        # the tick with the GetState export fused in (one launch per step)
+        eng.replicate_tick_export(lp_d, gf_d, commit_d, tl_d, where=DEVICE)
         if timed:
             ev[i][1].record(stream)
-        export_group_status_into(eng, lp_d, commit_d, tl_d)
         if world > 1:  # the shard router's fan-in
             if on_host:
                 allgather_status(commit_d.cpu(), tl_d.cpu())
@@ -266,11 +271,11 @@ def main():
         "warmup": W,
         "ms_per_step": dt / K * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_groups else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic: seeded config-#3 generator (include/mraft_synth.h), fresh HBM-resident copy per step",
-        "config": {"workload": "config #3 fused replication tick (a3+a4+a2+a1) + GetState export"
+        "config": {"workload": "config #3 fused replication tick (a3+a4+a2+a1) with the GetState export fused in"
                                + (" + RCCL all-gather of commit/term words" if world > 1 else ""),
                    "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
                    "committed_groups_last_step": int(((flags & 2) != 0).sum()),

@@ -326,6 +326,15 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items,
 int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer,
                          int32_t *group_flags, int32_t where);
 
+/* mraft_replicate_tick followed by mraft_export_group_status for the same
+ * leader_peer, fused into the one launch (the words the shard router
+ * all-gathers come out of the tick itself): commit[g] / term_leader[g] are
+ * the post-tick GetState words of replica leader_peer[g] (replica 0 when
+ * leader_peer[g] is out of range). */
+int mraft_replicate_tick_export(mraft_engine *h, const int32_t *leader_peer,
+                                int32_t *group_flags, int32_t *commit,
+                                int32_t *term_leader, int32_t where);
+
 /* Algorithmic word count of one mraft_replicate_tick on the current state
  * (DESIGN.md §4 definition; does not modify state): out_words[0] = words
  * read, out_words[1] = words written, out_words[2] = active groups. */

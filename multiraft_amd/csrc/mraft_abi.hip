@@ -311,7 +311,24 @@ int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer, int32_t *g
   void *lp, *gf;
   TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
   TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
-  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, h->stream);
+  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, nullptr, nullptr,
+                               h->stream);
+  return sg.finish();
+}
+
+int mraft_replicate_tick_export(mraft_engine *h, const int32_t *leader_peer, int32_t *group_flags,
+                                int32_t *commit, int32_t *term_leader, int32_t where) {
+  TRY(check(h));
+  if (!leader_peer || !commit || !term_leader) return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *lp, *gf, *c, *t;
+  TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
+  TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
+  TRY(sg.map(commit, sizeof(int32_t) * h->G, false, true, &c));
+  TRY(sg.map(term_leader, sizeof(int32_t) * h->G, false, true, &t));
+  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, (int32_t *)c,
+                               (int32_t *)t, h->stream);
   return sg.finish();
 }
 

@@ -9,7 +9,8 @@
 
 namespace mraft {
 
-void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, hipStream_t st);
+void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
+                           int32_t *exp_term_leader, hipStream_t st);
 void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,
                                  hipStream_t st);
 

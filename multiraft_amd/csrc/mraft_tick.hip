@@ -442,10 +442,23 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
 #endif
 
+// GetState (raft.go:237-246) of the group's exported replica, fused into the
+// tick (mraft_replicate_tick_export): commit and currentTerm<<1 | isLeader.
+struct Export {
+  int32_t *commit, *term_leader;
+  __device__ __forceinline__ void put(int g, int c, int t, int role) const {
+    if (commit) {
+      commit[g] = c;
+      term_leader[g] = (int32_t)(((uint32_t)t << 1) | (role == kLeader ? 1u : 0u));
+    }
+  }
+};
+
 template <int P, bool COUNT>
 __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
                                                     int32_t *__restrict__ gflags,
-                                                    unsigned long long *__restrict__ counts) {
+                                                    unsigned long long *__restrict__ counts,
+                                                    Export ex) {
   constexpr int NI = P - 1;
   constexpr int V = MRAFT_TICK_V;
   const int lane = lane_id();
@@ -466,7 +479,13 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // ------------------------------------------------------------ header
   const int lp = uni(leader_peer[g]);
   if (lp < 0 || lp >= P) {
-    if (!COUNT && lane == 0 && gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
+    if (!COUNT && lane == 0) {
+      if (gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
+      if (ex.commit) {
+        const long long s0 = (long long)g * P;  // mraft_export_group_status: replica 0
+        ex.put(g, s.commit[s0], s.term[s0], s.role[s0]);
+      }
+    }
     return;
   }
   const long long ld = (long long)g * P + lp;
@@ -493,8 +512,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     // the reachable states (include/mraft.h MRAFT_ITEM_BAD_STATE).
     if (COUNT) {
       if (lane == 0) atomicAdd(&counts[0], (unsigned long long)(role != kLeader ? 1 : 5));
-    } else if (lane == 0 && gflags) {
-      gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
+    } else if (lane == 0) {
+      if (gflags) gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
+      ex.put(g, c0, T, role);
     }
     return;
   }
@@ -508,8 +528,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   if (__ballot(icls == IC_PANIC)) {  // a3 would panic: the whole group is skipped
     if (COUNT) {
       if (lane == 0) atomicAdd(&counts[0], (unsigned long long)hR);
-    } else if (lane == 0 && gflags) {
-      gflags[g] = MRAFT_G_ERROR | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
+    } else if (lane == 0) {
+      if (gflags) gflags[g] = MRAFT_G_ERROR | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
+      ex.put(g, c0, T, role);
     }
     return;
   }
@@ -782,6 +803,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       }
       if (commit != c0) s.commit[ld] = commit;
       if (gflags) gflags[g] = flags;
+      ex.put(g, commit, fd.stepped ? fd.term : T, fd.stepped ? kFollower : kLeader);
     }
     TICK_STAMP(3);
 #pragma unroll
@@ -834,7 +856,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 // P == 1: no peers, so no AppendEntries and no reply ever reaches a1.
 __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
                           int32_t *__restrict__ gflags, unsigned long long *__restrict__ counts,
-                          int count) {
+                          int count, Export ex) {
   const int g = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   if (g >= s.G) return;
   const int lp = leader_peer[g];
@@ -853,34 +875,35 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
   if (count) {
     atomicAdd(&counts[0], R);
     atomicAdd(&counts[2], A);
-  } else if (gflags) {
-    gflags[g] = fl;
+  } else {
+    if (gflags) gflags[g] = fl;
+    ex.put(g, s.commit[g], s.term[g], s.role[g]);
   }
 }
 
 template <int P, bool COUNT>
 void launch_tick_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
-                   hipStream_t st) {
+                   Export ex, hipStream_t st) {
   const int blocks = (s.G + MRAFT_TICK_WPB - 1) / MRAFT_TICK_WPB;
   hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), 0, st, s, lpeer, gflags,
-                     counts);
+                     counts, ex);
 }
 
 template <bool COUNT>
 void launch_tick_c(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
-                   hipStream_t st) {
+                   Export ex, hipStream_t st) {
   switch (s.P) {
-    case 2: launch_tick_p<2, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 3: launch_tick_p<3, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 4: launch_tick_p<4, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 5: launch_tick_p<5, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 6: launch_tick_p<6, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 7: launch_tick_p<7, COUNT>(s, lpeer, gflags, counts, st); break;
-    case 8: launch_tick_p<8, COUNT>(s, lpeer, gflags, counts, st); break;
+    case 2: launch_tick_p<2, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 3: launch_tick_p<3, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 4: launch_tick_p<4, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 5: launch_tick_p<5, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 6: launch_tick_p<6, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 7: launch_tick_p<7, COUNT>(s, lpeer, gflags, counts, ex, st); break;
+    case 8: launch_tick_p<8, COUNT>(s, lpeer, gflags, counts, ex, st); break;
     default: {
       const int blocks = (s.G + 255) / 256;
       hipLaunchKernelGGL(k_tick_p1, dim3(blocks), dim3(256), 0, st, s, lpeer, gflags, counts,
-                         COUNT ? 1 : 0);
+                         COUNT ? 1 : 0, ex);
     }
   }
 }
@@ -895,13 +918,14 @@ extern "C" int mraft_debug_tick_trace(void *dst, long long nbytes) {
 }
 #endif
 
-void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, hipStream_t st) {
-  launch_tick_c<false>(s, lpeer, gflags, nullptr, st);
+void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
+                           int32_t *exp_term_leader, hipStream_t st) {
+  launch_tick_c<false>(s, lpeer, gflags, nullptr, Export{exp_commit, exp_term_leader}, st);
 }
 
 void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,
                                  hipStream_t st) {
-  launch_tick_c<true>(s, lpeer, nullptr, counts, st);
+  launch_tick_c<true>(s, lpeer, nullptr, counts, Export{nullptr, nullptr}, st);
 }
 
 }  // namespace mraft

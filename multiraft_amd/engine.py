@@ -157,6 +157,22 @@ class Engine:
             "mraft_replicate_tick")
         return group_flags
 
+    def replicate_tick_export(self, leader_peer, group_flags=None, commit=None, term_leader=None,
+                              where: int = HOST):
+        """The tick with the GetState export fused in: (flags, commit, term<<1|leader)."""
+        if where == HOST:
+            leader_peer = np.ascontiguousarray(leader_peer, dtype=np.int32)
+            if group_flags is None:
+                group_flags = np.zeros(self.G, dtype=np.int32)
+            if commit is None:
+                commit = np.zeros(self.G, dtype=np.int32)
+            if term_leader is None:
+                term_leader = np.zeros(self.G, dtype=np.int32)
+        _ck(self._lib.mraft_replicate_tick_export(self._h, ptr(leader_peer), ptr(group_flags),
+                                                  ptr(commit), ptr(term_leader), where),
+            "mraft_replicate_tick_export")
+        return group_flags, commit, term_leader
+
     def replicate_tick_count(self, leader_peer, where: int = HOST):
         if where == HOST:
             leader_peer = np.ascontiguousarray(leader_peer, dtype=np.int32)

@@ -228,3 +228,20 @@ def test_snapshot_install_gpu(P, L):
         for k in oo:
             assert np.array_equal(go[k], oo[k]), k
         assert_states_equal(e.store_state(), o.state(), G, P, L, "snapshot scenario")
+
+
+@pytest.mark.parametrize("G,P,L,seed", [(96, 5, 64, 61), (40, 3, 32, 62), (16, 1, 16, 63)])
+def test_tick_export_fused_gpu(G, P, L, seed):
+    """mraft_replicate_tick_export == the tick followed by GetState export,
+    idle (-1) and out-of-range leader indices included."""
+    st, lp, _ = synth_tick_state(G, P, L, seed=seed)
+    lp = lp.copy()
+    lp[::5] = -1
+    lp[3] = P
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        gf, c, tl = e.replicate_tick_export(lp)
+        assert np.array_equal(gf, o.replicate_tick(lp))
+        oc, otl = o.export_group_status(lp)
+        assert np.array_equal(c, oc) and np.array_equal(tl, otl)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "tick+export")
