@@ -69,10 +69,12 @@ def main():
            "config": {"workload": "config #5 election storm", "groups": G, "peers": P, "rounds": R,
                       "requestvotes_per_launch_upper_bound": rv_upper,
                       "groups_with_new_leader": int(((flags & 128) != 0).sum())},
-           "roofline": {"bound": "hbm", "achieved": bytes_launch / ker / 1e9, "peak": 8000.0,
+           "roofline": {"bound": "valu", "achieved": bytes_launch / ker / 1e9, "peak": 8000.0,
                         "unit": "GB/s", "frac": bytes_launch / ker / 8e12, "traffic": None,
                         "kernel": f"k_election_rounds<{P}>", "kernel_ms_mean": ker * 1e3,
-                        "note": "latency-bound: state stays in registers for all R rounds"},
+                        "note": ("VALU/issue-bound, not HBM: every replica's election state stays in "
+                                 "registers for all R rounds (HBM touched once in, once out); the GB/s "
+                                 "here are only the state bytes per launch")},
            "requestvotes_per_sec": rv_upper * K / dt,
            "cpu_baseline": None}
     if not a.no_cpu_baseline:
