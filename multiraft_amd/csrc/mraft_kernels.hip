@@ -195,15 +195,22 @@ __device__ __forceinline__ int quorum_rt(const int (&m)[8], int me) {
   return best;
 }
 
-// Lane per segment: the segment's replies folded in order, a1 evaluated after
-// each successful reply exactly as raft_append_entry.go:78 calls it.
+// Wave per segment: the segment's replies folded in order (wave-uniform), a1
+// evaluated after each successful reply exactly as raft_append_entry.go:78
+// calls it. a1's downward scan for the current-term gate (:90-103) is
+// wave-cooperative and incremental: the term is fixed while the replica stays
+// leader, and an evaluation that scanned (commit, top] leaves no entry of that
+// term above the new commit index up to top, so a later evaluation only scans
+// (H, top'] with H the highest index scanned so far — the same result as
+// rescanning from the top every time, with each log word read at most once.
 template <int P>
-__global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t n,
-                       const int64_t *__restrict__ seg_begin, int64_t n_seg,
-                       const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
-                       int32_t *__restrict__ item_err) {
-  const int64_t sg = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t n,
+                                              const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                                              const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
+                                              int32_t *__restrict__ item_err) {
+  const int64_t sg = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   if (sg >= n_seg) return;
+  const bool l0 = lane_id() == 0;
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   if (b >= e) return;
   const int L = s.L;
@@ -218,7 +225,8 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
   }
   if (!bad && s.commit[slot] < s.dummy[slot]) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {
-    for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
+    if (l0)
+      for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
     return;
   }
   const int me = slot % P;
@@ -234,6 +242,7 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
   const int c0 = commit, t0 = term, r0 = role;
   const int32_t *lrow = s.log + (int64_t)slot * L;
   bool touched_mn = false;
+  int H = commit;  // every index in (commit, H] is known not to hold the current term
   for (int64_t i = b; i < e; ++i) {
     const mraft_ae_result it = items[i];
     int fl = 0;
@@ -254,11 +263,13 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
 #pragma unroll
         for (int j = 0; j < P; ++j) if (j == pr) m[j] = mv;
         // a1 (:89-105): the count holds exactly for i <= M (quorum order
-        // statistic), so scan down from min(M, last) for the term gate.
-        const int M = quorum_rt<P>(m, me);
-        const int top = min(M, last);
-        for (int x = top; x > commit; --x) {
-          if (lrow[x - dummy] == term) { commit = x; fl |= MRAFT_F_COMMITTED; break; }
+        // statistic), so the gate is the highest index in (commit, min(M, last)]
+        // whose term is currentTerm.
+        const int top = min(quorum_rt<P>(m, me), last);
+        if (top > H) {
+          const int x = wave_scan_down_eq(lrow, dummy, H + 1, top, term);  // H if none
+          if (x > H) { commit = x; fl |= MRAFT_F_COMMITTED; }
+          H = top;
         }
       } else {
         nxp = it.reply_conflict_index;                                 // :82
@@ -267,9 +278,12 @@ __global__ void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t
       for (int j = 0; j < P; ++j) if (j == pr) nx[j] = nxp;
       if (nxp < last + 1) fl |= MRAFT_F_NEED_MORE;                     // :84-86
     }
-    flags[i] = fl;
-    item_err[i] = 0;
+    if (l0) {
+      flags[i] = fl;
+      item_err[i] = 0;
+    }
   }
+  if (!l0) return;
   if (term != t0 || role != r0) {
     s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
     mark_persist(s, slot, MRAFT_PERSIST_STATE);                        // :72
@@ -691,7 +705,7 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
                  hipStream_t st) {
   (void)n;
   if (n_seg <= 0) return;
-  const dim3 gr(blocks_for(n_seg, 64)), bl(64);
+  const dim3 gr(blocks_for(n_seg * 64)), bl(kBlock);
   switch (s.P) {
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
