@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--log-pad", type=int, default=0,
+                    help="experiment: pad every log row by this many entries (capacity L + pad, "
+                         "same logs and algorithmic words; only the row stride changes)")
     ap.add_argument("--group-order", default="natural", choices=["natural", "lpt-xcd", "random"],
                     help="experiment: permute the groups (same work, different dispatch order)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -172,6 +175,10 @@ def main():
     log(rank, f"generated {G}x{P}x{L} state in {time.perf_counter() - t:.1f}s")
     if args.group_order != "natural":
         st, lp = permute_groups(st, lp, G, P, L, args.group_order)
+    if args.log_pad:
+        st["log_term"] = np.ascontiguousarray(
+            np.pad(st["log_term"].reshape(G * P, L), ((0, 0), (0, args.log_pad))).reshape(-1))
+        L = L + args.log_pad
 
     # Ranks allocate in turn (a CPU rehearsal may put several ranks on one GPU).
     for r in range(world):

@@ -438,6 +438,9 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
+#ifndef MRAFT_TICK_HDR1
+#define MRAFT_TICK_HDR1 0  // 1: header scalars loaded by group index with leader_peer (one round trip fewer; measured no gain: HBM-bound)
+#endif
 #ifndef MRAFT_TICK_WPB
 #define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
 #endif
@@ -477,6 +480,51 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   TICK_STAMP(0);
 
   // ------------------------------------------------------------ header
+#if MRAFT_TICK_HDR1
+  // Every scalar the header needs is indexed by the group alone (the P
+  // replicas' scalars, the P matchIndex / nextIndex rows: the same lines the
+  // leader's own words sit on), so it is issued together with leader_peer[g]
+  // and the leader's and followers' words are then picked out of registers:
+  // one dependent round trip fewer than loading by leader slot.
+  const long long gs = (long long)g * P;
+  int r_term = 0, r_dummy = 0, r_last = 0, r_commit = 0, r_role = 0, r_match = 0, r_next = 0;
+  if (lane < P) {
+    r_term = s.term[gs + lane];
+    r_dummy = s.dummy[gs + lane];
+    r_last = s.last[gs + lane];
+    r_commit = s.commit[gs + lane];
+    r_role = s.role[gs + lane];
+  }
+  if (lane < P * P) {
+    r_match = s.match[gs * P + lane];
+    r_next = s.next[gs * P + lane];
+  }
+  const int lp = uni(leader_peer[g]);
+  if (lp < 0 || lp >= P) {
+    const int e_c = __builtin_amdgcn_readlane(r_commit, 0), e_t = __builtin_amdgcn_readlane(r_term, 0),
+              e_r = __builtin_amdgcn_readlane(r_role, 0);  // mraft_export_group_status: replica 0
+    if (!COUNT && lane == 0) {
+      if (gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
+      ex.put(g, e_c, e_t, e_r);
+    }
+    return;
+  }
+  const long long ld = gs + lp;
+  const long long lrow = ld * L;
+  const int role = __builtin_amdgcn_readlane(r_role, lp), T = __builtin_amdgcn_readlane(r_term, lp),
+            c0 = __builtin_amdgcn_readlane(r_commit, lp), last = __builtin_amdgcn_readlane(r_last, lp),
+            ldummy = __builtin_amdgcn_readlane(r_dummy, lp);
+  int mm[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) mm[j] = __builtin_amdgcn_readlane(r_match, lp * P + j);
+  const int p = lane < lp ? lane : lane + 1;
+  const long long f = gs + p;
+  const int fp = lane < NI ? p : 0;
+  int nxt = __shfl(r_next, lp * P + fp, 64), fterm = __shfl(r_term, fp, 64),
+      fdummy = __shfl(r_dummy, fp, 64), flast = __shfl(r_last, fp, 64),
+      fcommit = __shfl(r_commit, fp, 64);
+  if (lane >= NI) nxt = fterm = fdummy = flast = fcommit = 0;
+#else
   const int lp = uni(leader_peer[g]);
   if (lp < 0 || lp >= P) {
     if (!COUNT && lane == 0) {
@@ -506,6 +554,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     flast = s.last[f];
     fcommit = s.commit[f];
   }
+#endif
   long long hR = 1;  // algorithmic words of the header (wave-uniform)
   if (role != kLeader || c0 < ldummy) {
     // not a leader: appendOneRound returns (:22-25); commit < dummy: outside
