@@ -245,3 +245,46 @@ def test_tick_export_fused_gpu(G, P, L, seed):
         oc, otl = o.export_group_status(lp)
         assert np.array_equal(c, oc) and np.array_equal(tl, otl)
         assert_states_equal(e.store_state(), o.state(), G, P, L, "tick+export")
+
+
+def _assert_big_states_equal(a, b, G, P, L, ctx, rows=8192):
+    """assert_states_equal in row blocks (the full config-#3 image is 5 GiB)."""
+    for k in a:
+        if k != "log_term":
+            assert np.array_equal(a[k], b[k]), f"{ctx}: {k}"
+    la, lb = a["log_term"].reshape(G * P, L), b["log_term"].reshape(G * P, L)
+    live = a["last_index"] - a["dummy_index"]
+    col = np.arange(L)[None, :]
+    for r0 in range(0, G * P, rows):
+        m = col <= live[r0:r0 + rows, None]
+        assert np.array_equal(np.where(m, la[r0:r0 + rows], 0), np.where(m, lb[r0:r0 + rows], 0)), \
+            f"{ctx}: log rows {r0}..{r0 + rows}"
+
+
+def test_tick_full_config3_gpu():
+    """BASELINE config #3 at full size (65,536 groups x 5 peers x 4,096-entry
+    logs, the bench workload): two ticks bit-exact against the oracle (state,
+    persist bits, group flags, fused GetState words) and the algorithmic word
+    count of the roofline equal to the oracle's instrumented count."""
+    G, P, L = 65536, 5, 4096
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        assert e.replicate_tick_count(lp) == o.replicate_tick_count(lp)
+        for k in range(2):
+            gf, c, tl = e.replicate_tick_export(lp)
+            assert np.array_equal(gf, o.replicate_tick(lp, nthreads=16)), f"tick {k} flags"
+            oc, otl = o.export_group_status(lp)
+            assert np.array_equal(c, oc) and np.array_equal(tl, otl)
+            _assert_big_states_equal(e.store_state(), o.state(), G, P, L, f"full tick {k}")
+
+
+def test_election_storm_full_config5_gpu():
+    """BASELINE config #5 at full size: 65,536 groups x 7 peers, 64 rounds."""
+    from multiraft_amd import synth_election_state
+    G, P, L, R = 65536, 7, 8, 64
+    st, mask = synth_election_state(G, P, L, seed=synth_seed(5), rounds=R)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        assert np.array_equal(e.election_rounds(mask), o.election_rounds(mask))
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "full storm")
