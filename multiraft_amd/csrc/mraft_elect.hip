@@ -16,6 +16,9 @@ namespace {
 #ifndef MRAFT_EL_CX_LDS
 #define MRAFT_EL_CX_LDS 1  // candidate broadcast through LDS (else __shfl)
 #endif
+#ifndef MRAFT_EL_SPARSE
+#define MRAFT_EL_SPARSE 1  // voter loop over the round's candidates only (else all P peers)
+#endif
 #ifndef MRAFT_EL_GM_LDS
 #define MRAFT_EL_GM_LDS 0  // grant-mask transpose through LDS (else __shfl; measured faster)
 #endif
@@ -51,6 +54,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
   __shared__ int lds_cx[256];
   __shared__ __attribute__((aligned(8))) uint8_t lds_gm[256];
+  const int seg = (int)(threadIdx.x & 63) & ~7;
   int fl = 0, became = 0, pd = 0;  // pd: persist() ran (StartElection :15, HandleRequestVote :57, :45)
   int mnext = (grp && R > 0) ? (int)cand[g] : 0;  // round masks are fetched one round ahead
   for (int r = 0; r < R; ++r) {
@@ -86,6 +90,35 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // tally below needs (a voter's term after handling c is the max of the
     // two, the stale branch included).
     int gm = 0, pmx = INT32_MIN;
+#if MRAFT_EL_SPARSE
+    // Only the candidates: the k-th set bit of the group's candidate mask, for
+    // k below the wave's largest candidate count (ascending peer order kept).
+    const unsigned long long cb = __ballot(isc);
+    int cm = (int)((cb >> seg) & 0xffull);
+    int kmax = __builtin_popcount(cm);
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
+    kmax = __builtin_amdgcn_readfirstlane(kmax);
+    for (int k = 0; k < kmax; ++k) {
+      const bool any = cm != 0;
+      const int c = any ? __builtin_ctz(cm) : 0;
+      cm &= cm - 1;
+      const int cxc = __shfl(mycx, c, 8);
+      const bool cisc = any;
+      const int cat = cxc & 0x7fffffff;
+      pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
+      const bool h = act && cisc && c != p;                            // this voter handles c's RV
+      pd |= (int)h;
+      const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
+      const bool gt = h && cat > term;                                 // :63-66
+      term = gt ? cat : term;
+      role = gt ? kFollower : role;
+      voted = gt ? -1 : voted;
+      const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
+      voted = grant ? c : voted;
+      gm |= (int)grant << c;
+    }
+#else
 #pragma unroll
     for (int c = 0; c < P; ++c) {  // branch-free: every step is a select
       const bool cisc = cx[c] < 0;
@@ -102,6 +135,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       voted = grant ? c : voted;
       gm |= (int)grant << c;
     }
+#endif
     // Grants transposed through LDS: byte v of the segment's word = voter v's
     // grant mask; bit v of mine = voter v granted this lane.
     int mine = 0;
@@ -134,7 +168,6 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     }
   }
   const unsigned long long el = __ballot(fl & MRAFT_G_ELECTED), sd = __ballot(fl & MRAFT_G_STEPPED_DOWN);
-  const int seg = (int)(threadIdx.x & 63) & ~7;
   if (grp && p == 0 && gflags) {
     gflags[g] = (((el >> seg) & 0xffull) ? MRAFT_G_ELECTED : 0) |
                 (((sd >> seg) & 0xffull) ? MRAFT_G_STEPPED_DOWN : 0);
