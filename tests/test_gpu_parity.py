@@ -288,3 +288,29 @@ def test_election_storm_full_config5_gpu():
     with _engine(G, P, L, st) as e:
         assert np.array_equal(e.election_rounds(mask), o.election_rounds(mask))
         assert_states_equal(e.store_state(), o.state(), G, P, L, "full storm")
+
+
+def test_start_and_applier_gpu():
+    """Start (raft.go:90-104) on random slots — leaders and non-leaders,
+    duplicate slots, multi-entry counts, appends past the capacity — then the
+    applier's ranges (raft.go:153-203) after a tick, against the oracle."""
+    G, P, L = 128, 5, 64
+    rng = np.random.default_rng(71)
+    st, lp, _ = synth_tick_state(G, P, L, seed=72)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        for _ in range(3):
+            slots = rng.integers(0, G * P, 200).astype(np.int32)
+            counts = rng.integers(1, 24, 200).astype(np.int32)
+            counts[::17] = 0                                   # rejected: BAD_SLOT
+            got = e.start(slots, counts)
+            exp = o.start(slots, counts)
+            for a, b in zip(got, exp):
+                assert np.array_equal(a, b)
+            assert_states_equal(e.store_state(), o.state(), G, P, L, "start")
+        assert np.array_equal(e.replicate_tick(lp), o.replicate_tick(lp))
+        for _ in range(2):
+            fr, to = e.collect_apply()
+            ofr, oto = o.collect_apply()
+            assert np.array_equal(fr, ofr) and np.array_equal(to, oto)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "applier")
