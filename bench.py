@@ -57,46 +57,79 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(G_total, P, L, seed, budget_s, rank):
-    """The CPU oracle (C restatement of the Go control flow, incl. the
-    per-message entries copy of raft_append_entry.go:50-54 and a1's downward
-    loop) timed on a bounded sample of the same workload on this host."""
+    """The reference's tick timed on this host's cores, two restatements:
+    the Go-shaped one (oracle/mraft_goshape.c: int64 Raft structs, 40-byte
+    Entry slices, a fresh entries copy per message as appendOneRound makes,
+    trunc + append, advanceCommitIndexForLeader's O((last-commit)*P) count) is
+    the reported value; the engine-layout one (oracle/mraft_oracle.c, SoA
+    int32, same control flow) is reported beside it. Both on bounded samples
+    of the same seeded workload, fresh state per pass (restores untimed)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_lib import Oracle  # test infrastructure: the checker / CPU baseline only
+    from oracle_lib import GoShaped, Oracle  # test infrastructure: CPU baseline only
 
     from multiraft_amd import synth_tick_state
-    Gs = min(8192, G_total)
-    st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gs)
     threads = max(1, min(16, os.cpu_count() or 1))
 
-    o = Oracle(Gs, P, L, st)
-
-    def run(nt, budget):
+    def timed(make, tick, budget, nt, groups):
         done, spent, w0, last = 0, 0.0, time.perf_counter(), time.perf_counter()
-        # bounded in tick time AND in wall time (the untimed restores count there)
         while spent < budget and time.perf_counter() - w0 < 3 * budget + 10:
-            for k, v in st.items():  # restore the pristine state in place, untimed
-                np.copyto(o.st[k], v)
+            obj = make()  # untimed restore of the pristine state
             t = time.perf_counter()
-            o.replicate_tick(lp, nthreads=nt)
+            tick(obj, nt)
             spent += time.perf_counter() - t
-            done += Gs
+            done += groups
             if time.perf_counter() - last > 20:
                 last = time.perf_counter()
                 log(rank, f"cpu baseline ({nt} threads): {done} decisions in {spent:.1f} s so far")
         return done / spent, done, spent
 
-    v1, d1, s1 = run(1, min(3.0, budget_s / 4))
-    vt, dt, stt = run(threads, budget_s)
-    log(rank, f"cpu baseline: {vt:.4g} decisions/s on {threads} threads, {v1:.4g} on 1 thread")
-    return {"value": vt, "unit": "decisions/s", "cores": threads, "kind": "port",
+    # Go-shaped restatement (the value)
+    Gg = min(2048, G_total)
+    stg, lpg, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gg)
+    holder = {}
+
+    def make_go():
+        if "g" in holder:
+            holder["g"].close()
+        holder["g"] = GoShaped(Gg, P, L, stg)
+        return holder["g"]
+
+    def tick_go(g, nt):
+        assert g.replicate_tick(lpg, nthreads=nt) == 0
+
+    g1, _, _ = timed(make_go, tick_go, min(1.0, budget_s / 8), 1, Gg)
+    gt, gdone, gspent = timed(make_go, tick_go, budget_s / 2, threads, Gg)
+    holder["g"].close()
+    # engine-layout (SoA int32) restatement
+    Gs = min(8192, G_total)
+    st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gs)
+    o = Oracle(Gs, P, L, st)
+
+    def make_soa():
+        for k, v in st.items():
+            np.copyto(o.st[k], v)
+        return o
+
+    def tick_soa(obj, nt):
+        obj.replicate_tick(lp, nthreads=nt)
+
+    s1, _, _ = timed(make_soa, tick_soa, min(2.0, budget_s / 6), 1, Gs)
+    stt, sdone, sspent = timed(make_soa, tick_soa, budget_s / 3, threads, Gs)
+    log(rank, f"cpu baseline: go-shaped {gt:.4g} decisions/s on {threads} threads ({g1:.4g} on 1); "
+              f"SoA {stt:.4g} ({s1:.4g} on 1)")
+    return {"value": gt, "unit": "decisions/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "compiler": "gcc -O3 -march=x86-64-v3 (oracle/Makefile)",
-            "sample": (f"oracle/mraft_oracle.c replicate_tick over groups 0..{Gs - 1} of the same "
-                       f"seeded config-#3 workload ({P} peers, L={L}), fresh state per pass, "
-                       f"{d1 // Gs + dt // Gs} passes; {threads} threads: {dt} decisions in {stt:.2f} s; "
-                       f"1 thread: {v1:.4g} decisions/s; excludes gob persist()/labrpc encoding "
-                       f"the Go reference also pays per handler"),
-            "single_thread_value": v1}
+            "sample": (f"oracle/mraft_goshape.c: the tick on the reference's data shapes (int64 Raft "
+                       f"structs, 40-byte Entry slices, per-message entries copies, a1's "
+                       f"O((last-commit)*P) loop) over groups 0..{Gg - 1} of the same seeded config-#3 "
+                       f"workload ({P} peers, L={L}), fresh state per pass; {threads} threads: "
+                       f"{gdone} decisions in {gspent:.2f} s; 1 thread: {g1:.4g} decisions/s; excludes "
+                       f"the gob persist()/labrpc encoding the Go reference also pays per handler"),
+            "single_thread_value": g1,
+            "soa_int32": {"value": stt, "single_thread_value": s1, "cores": threads,
+                          "sample": (f"oracle/mraft_oracle.c (engine layout, same control flow) over "
+                                     f"groups 0..{Gs - 1}: {sdone} decisions in {sspent:.2f} s")}}
 
 
 def permute_groups(st, lp, G, P, L, how):

@@ -95,6 +95,14 @@ int ora_read_persistent(ora_engine *e, const int32_t *slots, int64_t n, mraft_pe
 int ora_restore(ora_engine *e, const mraft_persistent *in, int64_t n, const int32_t *terms,
                 int64_t n_terms, int32_t *item_err);
 
+/* Go-shaped restatement of the tick (mraft_goshape.c): int64 Raft structs,
+ * 40-byte Entry slices, per-message entry copies. CPU baseline only. */
+typedef struct go_cluster go_cluster;
+go_cluster *goshape_build(int32_t G, int32_t P, int32_t L, const mraft_soa *s);
+void goshape_store(const go_cluster *c, const mraft_soa *s);
+void goshape_free(go_cluster *c);
+int64_t goshape_tick(go_cluster *c, const int32_t *leader_peer, int32_t nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,11 +50,18 @@ def lib():
             "ora_collect_persist": [E, vp],
             "ora_read_persistent": [E, vp, i64, vp, vp, i64],
             "ora_restore": [E, vp, i64, vp, i64, vp],
+            "goshape_build": [i32, i32, i32, ctypes.POINTER(MraftSoa)],
+            "goshape_store": [vp, ctypes.POINTER(MraftSoa)],
+            "goshape_free": [vp],
+            "goshape_tick": [vp, vp, i32],
         }
         for n, a in sigs.items():
             f = getattr(l, n)
             f.argtypes = a
-            f.restype = None if n in ("ora_count_disable", "ora_count_result") else ctypes.c_int
+            f.restype = None if n in ("ora_count_disable", "ora_count_result", "goshape_store",
+                                      "goshape_free") else ctypes.c_int
+        l.goshape_build.restype = ctypes.c_void_p
+        l.goshape_tick.restype = ctypes.c_int64
         _lib = l
     return _lib
 
@@ -257,3 +264,32 @@ def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = "")
     if not np.array_equal(np.where(mask, la, 0), np.where(mask, lb, 0)):
         rows = np.nonzero((np.where(mask, la, 0) != np.where(mask, lb, 0)).any(axis=1))[0][:8]
         raise AssertionError(f"{ctx}: log_term differs in replicas {rows}")
+
+
+class GoShaped:
+    """The tick on the reference's own data shapes (oracle/mraft_goshape.c):
+    the CPU baseline's Go-shaped variant. Built from a SoA image (untimed)."""
+
+    def __init__(self, G: int, P: int, L: int, st: dict):
+        self.G, self.P, self.L = G, P, L
+        self._st = st
+        self._soa = soa_of(st)
+        self._c = lib().goshape_build(G, P, L, ctypes.byref(self._soa))
+
+    def replicate_tick(self, leader_peer, nthreads: int = 1) -> int:
+        lp = np.ascontiguousarray(leader_peer, dtype=np.int32)
+        return int(lib().goshape_tick(self._c, ptr(lp), nthreads))
+
+    def state(self) -> dict:
+        out = copy_state(self._st)
+        soa = soa_of(out)
+        lib().goshape_store(self._c, ctypes.byref(soa))
+        return out
+
+    def close(self):
+        if self._c:
+            lib().goshape_free(self._c)
+            self._c = None
+
+    def __del__(self):
+        self.close()

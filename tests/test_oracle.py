@@ -343,3 +343,23 @@ def test_snapshot_install_c_vs_py(P, L):
     assert out["pr_fl"].tolist() == prfl
     assert_states_equal(o.state(), pst, G, P, L, "snapshot scenario")
     assert (out["is_fl"] == 32).any() and (snap_err == 1).any()
+
+
+def test_goshaped_tick_equals_oracle():
+    """The CPU baseline's Go-shaped restatement (int64 structs, 40-B Entry
+    slices, per-message copies) computes the same tick as the SoA oracle."""
+    from oracle_lib import GoShaped
+    for (G, P, L, seed) in [(256, 5, 256, 3), (128, 3, 512, 4), (64, 7, 128, 5)]:
+        st, lp, _ = synth_tick_state(G, P, L, seed=seed)
+        o = Oracle(G, P, L, st)
+        o.replicate_tick(lp)
+        gsh = GoShaped(G, P, L, st)
+        assert gsh.replicate_tick(lp, nthreads=4) == 0
+        got = gsh.state()
+        exp = o.state()
+        for k in exp:
+            if k in ("persist_dirty", "log_term"):
+                continue
+            assert np.array_equal(got[k], exp[k]), k
+        assert_states_equal({k: v for k, v in got.items() if k != "persist_dirty"},
+                            {k: v for k, v in exp.items() if k != "persist_dirty"}, G, P, L, "go-shaped")
