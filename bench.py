@@ -86,20 +86,18 @@ def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     # Go-shaped restatement (the value)
     Gg = min(2048, G_total)
     stg, lpg, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gg)
-    holder = {}
+    gsh = GoShaped(Gg, P, L, stg)
 
     def make_go():
-        if "g" in holder:
-            holder["g"].close()
-        holder["g"] = GoShaped(Gg, P, L, stg)
-        return holder["g"]
+        gsh.reset(threads)
+        return gsh
 
     def tick_go(g, nt):
         assert g.replicate_tick(lpg, nthreads=nt) == 0
 
     g1, _, _ = timed(make_go, tick_go, min(1.0, budget_s / 8), 1, Gg)
     gt, gdone, gspent = timed(make_go, tick_go, budget_s / 2, threads, Gg)
-    holder["g"].close()
+    gsh.close()
     # engine-layout (SoA int32) restatement
     Gs = min(8192, G_total)
     st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=0, g_end=Gs)

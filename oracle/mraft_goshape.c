@@ -80,8 +80,13 @@ go_cluster *goshape_build(int32_t G, int32_t P, int32_t L, const mraft_soa *s) {
     r->currentTerm = s->current_term[i]; r->votedFor = s->voted_for[i]; r->state = s->state[i];
     r->commitIndex = s->commit_index[i]; r->lastApplied = s->last_applied[i];
     const int64_t d = s->dummy_index[i], n = (int64_t)s->last_index[i] - d + 1;
-    r->caplogs = n; r->nlogs = n;
-    r->logs = (go_entry *)calloc((size_t)n, sizeof(go_entry));
+    /* capacity L, like a slice that has already grown: the timed tick then
+     * copies entries but never reallocates (a realloc of a large block is an
+     * mremap syscall that serialises threads on the address-space lock, a
+     * cost Go's heap does not have) */
+    r->caplogs = n > L ? n : L; r->nlogs = n;
+    r->logs = (go_entry *)malloc(sizeof(go_entry) * (size_t)r->caplogs);
+    memset(r->logs, 0, sizeof(go_entry) * (size_t)r->caplogs);  /* pre-fault (Go's heap is warm) */
     for (int64_t k = 0; k < n; ++k) {
       r->logs[k].Index = d + k;
       r->logs[k].Term = s->log_term[i * L + k];
@@ -277,4 +282,50 @@ int64_t goshape_tick(go_cluster *c, const int32_t *leader_peer, int32_t nthreads
     skipped += jobs[t].skipped;
   }
   return skipped;
+}
+
+/* Restores the pristine SoA state into the already-built cluster in place
+ * (slices keep their capacity), groups split over nthreads. Untimed helper of
+ * the CPU baseline. */
+typedef struct {
+  go_cluster *c;
+  const mraft_soa *s;
+  int64_t b, e;
+} go_reset_job;
+
+static void *go_reset_worker(void *arg) {
+  go_reset_job *j = (go_reset_job *)arg;
+  const int32_t P = j->c->P, L = j->c->L;
+  const mraft_soa *s = j->s;
+  for (int64_t i = j->b; i < j->e; ++i) {
+    go_raft *r = &j->c->r[i];
+    r->currentTerm = s->current_term[i]; r->votedFor = s->voted_for[i]; r->state = s->state[i];
+    r->commitIndex = s->commit_index[i]; r->lastApplied = s->last_applied[i];
+    const int64_t d = s->dummy_index[i], n = (int64_t)s->last_index[i] - d + 1;
+    r->nlogs = n;
+    for (int64_t k = 0; k < n; ++k) {
+      r->logs[k].Index = d + k;
+      r->logs[k].Term = s->log_term[i * L + k];
+    }
+    for (int32_t q = 0; q < P; ++q) {
+      r->nextIndex[q] = s->next_index[i * P + q];
+      r->matchIndex[q] = s->match_index[i * P + q];
+    }
+  }
+  return NULL;
+}
+
+void goshape_reset(go_cluster *c, const mraft_soa *s, int32_t nthreads) {
+  const int64_t n = (int64_t)c->G * c->P;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  go_reset_job jobs[256];
+  for (int32_t t = 0; t < nthreads; ++t) {
+    jobs[t].c = c; jobs[t].s = s;
+    jobs[t].b = n * t / nthreads;
+    jobs[t].e = n * (t + 1) / nthreads;
+    pthread_create(&th[t], NULL, go_reset_worker, &jobs[t]);
+  }
+  for (int32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }

@@ -101,6 +101,7 @@ typedef struct go_cluster go_cluster;
 go_cluster *goshape_build(int32_t G, int32_t P, int32_t L, const mraft_soa *s);
 void goshape_store(const go_cluster *c, const mraft_soa *s);
 void goshape_free(go_cluster *c);
+void goshape_reset(go_cluster *c, const mraft_soa *s, int32_t nthreads);
 int64_t goshape_tick(go_cluster *c, const int32_t *leader_peer, int32_t nthreads);
 
 #ifdef __cplusplus

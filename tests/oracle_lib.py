@@ -54,12 +54,13 @@ def lib():
             "goshape_store": [vp, ctypes.POINTER(MraftSoa)],
             "goshape_free": [vp],
             "goshape_tick": [vp, vp, i32],
+            "goshape_reset": [vp, ctypes.POINTER(MraftSoa), i32],
         }
         for n, a in sigs.items():
             f = getattr(l, n)
             f.argtypes = a
             f.restype = None if n in ("ora_count_disable", "ora_count_result", "goshape_store",
-                                      "goshape_free") else ctypes.c_int
+                                      "goshape_free", "goshape_reset") else ctypes.c_int
         l.goshape_build.restype = ctypes.c_void_p
         l.goshape_tick.restype = ctypes.c_int64
         _lib = l
@@ -279,6 +280,10 @@ class GoShaped:
     def replicate_tick(self, leader_peer, nthreads: int = 1) -> int:
         lp = np.ascontiguousarray(leader_peer, dtype=np.int32)
         return int(lib().goshape_tick(self._c, ptr(lp), nthreads))
+
+    def reset(self, nthreads: int = 1):
+        """Back to the state it was built from (slices keep their capacity)."""
+        lib().goshape_reset(self._c, ctypes.byref(self._soa), nthreads)
 
     def state(self) -> dict:
         out = copy_state(self._st)

@@ -363,3 +363,17 @@ def test_goshaped_tick_equals_oracle():
             assert np.array_equal(got[k], exp[k]), k
         assert_states_equal({k: v for k, v in got.items() if k != "persist_dirty"},
                             {k: v for k, v in exp.items() if k != "persist_dirty"}, G, P, L, "go-shaped")
+
+
+def test_goshaped_reset_restores():
+    from oracle_lib import GoShaped
+    G, P, L = 64, 5, 128
+    st, lp, _ = synth_tick_state(G, P, L, seed=9)
+    g = GoShaped(G, P, L, st)
+    g.replicate_tick(lp, nthreads=2)
+    first = g.state()
+    g.reset(nthreads=3)
+    assert_states_equal({k: v for k, v in g.state().items() if k != "persist_dirty"},
+                        {k: v for k, v in st.items() if k != "persist_dirty"}, G, P, L, "reset")
+    g.replicate_tick(lp, nthreads=1)
+    assert_states_equal(g.state(), first, G, P, L, "re-run")
