@@ -438,6 +438,9 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
+#ifndef MRAFT_TICK_XCD_CHUNK
+#define MRAFT_TICK_XCD_CHUNK 0  // 0: one contiguous range of groups per XCD; else chunks of this many
+#endif
 #ifndef MRAFT_TICK_HDR1
 #define MRAFT_TICK_HDR1 0  // 1: header scalars loaded by group index with leader_peer (one round trip fewer; measured no gain: HBM-bound)
 #endif
@@ -470,7 +473,17 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // scalar SoA lines neighbouring groups share stay in one XCD's L2. Speed
   // only; any placement gives the same results.
   int gb = (int)blockIdx.x;
-  if (MRAFT_TICK_XCD) {
+  if (MRAFT_TICK_XCD && MRAFT_TICK_XCD_CHUNK > 0) {
+    // XCD x takes chunks x, x+8, x+16, ... of MRAFT_TICK_XCD_CHUNK consecutive
+    // groups: neighbours still share an L2, and every XCD's work is spread
+    // over the whole image. The tail that does not fill 8 chunks keeps its order.
+    constexpr int C = MRAFT_TICK_XCD_CHUNK > 0 ? MRAFT_TICK_XCD_CHUNK : 1;
+    const int full = ((int)gridDim.x / (8 * C)) * (8 * C);
+    if (gb < full) {
+      const int x = gb & 7, k = gb >> 3;
+      gb = ((k / C) * 8 + x) * C + (k % C);
+    }
+  } else if (MRAFT_TICK_XCD) {
     const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
     gb = x * per + min(x, rem) + (gb >> 3);
   }
