@@ -4,6 +4,7 @@
 // opposed to the fused co-resident tick of mraft_tick.hip.
 #include "mraft_device.h"
 #include "mraft_internal.h"
+#include "mraft_pass.h"
 
 namespace mraft {
 
@@ -144,21 +145,40 @@ __global__ __launch_bounds__(256) void k_handle_ae(Dev s, const mraft_ae_args *_
         r.conflict_index = wave_conflict_scan(frow, fdummy, prev, frow[prev - fdummy]);  // :136-142
       else r.conflict_index = prev;
     } else {
-      const int32_t *E = ent + a.entries_offset;
-      int32_t *F = s.log + (int64_t)f * L + (prev + 1 - fdummy);
-      const int kc = min(nn, flast - prev);
-      int k = wave_merge_compare(E, F, kc);                            // :149-155
-      if (k < 0 && kc < nn) k = kc;
+      // :146-155 through the streaming pass the tick uses (mraft_pass.h):
+      // compare entries with the follower's terms, truncate-and-append from
+      // the first mismatch; dwordx4 when entries and row are 16-B aligned
+      // alike and every vector read stays inside its buffer.
+      const long long eo = a.entries_offset - (long long)(prev + 1);    // entry Index x -> ent[eo + x]
+      const long long fo[1] = {(long long)f * L - fdummy};               // follower Index x -> log[fo + x]
+      const int plo = prev + 1, phi = prev + nn, nend = prev + nn + 1;
+      const int start[1] = {plo}, cend[1] = {min(phi, flast) + 1};
+      const int capok[1] = {(int64_t)prev + nn - fdummy <= (int64_t)L - 1};
+      int mode[1] = {M_CMP}, cfrom[1] = {0}, fullmask = 0, found = -1;
+      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)(s.log + fo[0] + plo);
+      const bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0 && ((ea ^ fa) & 15) == 0 &&
+                       (ea & ~(uintptr_t)15) >= (uintptr_t)ent &&
+                       ((uintptr_t)(ent + eo + phi) | 15) < (uintptr_t)(ent + n_ent);
+      if (vec) {
+        int c = plo - (int)((ea >> 2) & 31);                           // 128-B aligned chunks
+        for (; c <= phi && mode[0] == M_CMP; c += 256)
+          pass_chunk<1, 1, true, false>(ent, s.log, eo, fo, start, cend, nend, mode, cfrom, capok,
+                                        fullmask, 1, 0, 0, found, c, plo, phi);
+        copy_loop<1, 1, true, false>(ent, s.log, eo, fo, mode, c, nend, phi, 1, 0, 0, found);
+      } else {
+        int c = plo;
+        for (; c <= phi && mode[0] == M_CMP; c += 256)
+          pass_chunk<1, 1, false, false>(ent, s.log, eo, fo, start, cend, nend, mode, cfrom, capok,
+                                         fullmask, 1, 0, 0, found, c, plo, phi);
+        copy_loop<1, 1, false, false>(ent, s.log, eo, fo, mode, c, nend, phi, 1, 0, 0, found);
+      }
       int last_after = flast;
-      if (k >= 0) {
-        if ((int64_t)prev + nn - fdummy > (int64_t)L - 1) {
-          write_state = false;                                         // engine capacity
-          if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_LOG_FULL; }
-        } else {
-          wave_copy(E + k, F + k, nn - k);
-          newlast = prev + nn;
-          last_after = newlast;
-        }
+      if (fullmask) {
+        write_state = false;                                           // engine capacity
+        if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_LOG_FULL; }
+      } else if (cfrom[0] > 0) {                                       // truncated and appended
+        newlast = prev + nn;
+        last_after = newlast;
       }
       if (write_state) {
         const int fc = s.commit[f];

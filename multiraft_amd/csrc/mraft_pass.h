@@ -1,0 +1,280 @@
+// mraft_pass.h — the streaming entry-merge pass shared by the fused tick
+// (mraft_tick.hip) and the message-level HandleAppendEntries
+// (mraft_kernels.hip): raft_append_entry.go:146-155's compare-then-truncate-
+// and-append over one source of entries (`src`: the leader's log row, or a
+// network batch) into up to NI follower rows of `log`, 256 entries per wave
+// iteration, first mismatch by ballot, and — for the tick — the exact a1
+// commit scan riding on the same loads.
+#pragma once
+#include "mraft_device.h"
+
+namespace mraft {
+namespace {
+
+enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the pass
+
+#ifndef MRAFT_TICK_NT
+#define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
+#endif
+
+// Streaming (read-once / write-once) log accesses of the pass.
+__device__ __forceinline__ int4 ld4(const int32_t *p) {
+  if (MRAFT_TICK_NT & 2) {
+    const int4 *q = reinterpret_cast<const int4 *>(p);
+    return make_int4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
+                     __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
+  }
+  return *reinterpret_cast<const int4 *>(p);
+}
+__device__ __forceinline__ int ld1(const int32_t *p) {
+  if (MRAFT_TICK_NT & 2) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ __forceinline__ void st4(int32_t *p, int a, int b, int c, int d) {
+  if (MRAFT_TICK_NT & 1) {
+    int4 *q = reinterpret_cast<int4 *>(p);
+    __builtin_nontemporal_store(a, &q->x);
+    __builtin_nontemporal_store(b, &q->y);
+    __builtin_nontemporal_store(c, &q->z);
+    __builtin_nontemporal_store(d, &q->w);
+  } else {
+    *reinterpret_cast<int4 *>(p) = make_int4(a, b, c, d);
+  }
+}
+__device__ __forceinline__ void st1(int32_t *p, int a) {
+  if (MRAFT_TICK_NT & 1) __builtin_nontemporal_store(a, p);
+  else *p = a;
+}
+
+// One chunk of the streaming pass over the leader's log. The pass serves
+// (1) every follower q's entry merge: compare entries [start_q, cend_q) with
+// the follower's log, then (from the first mismatch) copy entries up to `hi`
+// into it; and (2) the exact commit scan: the largest index in [slo, shi]
+// whose term equals T (kept in `found`, the pass ascends).
+// VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
+// otherwise lane j owns c+64(4v+u)+j. Leader entry idx is log[eo + idx],
+// follower q's is log[fo[q] + idx].
+template <int NI, int V, bool VEC, bool COUNT>
+__device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int32_t *__restrict__ log,
+                                           long long eo,
+                                           const long long (&fo)[NI], const int (&start)[NI],
+                                           const int (&cend)[NI], int nend, int (&mode)[NI],
+                                           int (&cfrom)[NI], const int (&capok)[NI],
+                                           int &fullmask, int slo, int shi, int T, int &found,
+                                           int c, int plo, int phi) {
+  constexpr int CW = 256 * V;
+  const int lane = lane_id();
+  int idx[V][4], e[V][4];
+#pragma unroll
+  for (int v = 0; v < V; ++v)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
+  // Leader entries, then every comparing follower's terms: all loads in flight
+  // before the first compare.
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if (VEC) {
+      int4 x = make_int4(0, 0, 0, 0);
+      if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(src + eo + idx[v][0]);
+      e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src + eo + idx[v][u]) : 0;
+    }
+  }
+  int f[NI][V][4];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f[q][v][u] = 0;
+    if (mode[q] != M_CMP || start[q] > c + CW - 1 || cend[q] <= c) continue;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if (VEC) {
+        if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
+          const int4 x = ld4(log + fo[q] + idx[v][0]);
+          f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(log + fo[q] + idx[v][u]);
+      }
+    }
+  }
+  // Commit scan: highest index of this chunk in [slo, shi] with term T.
+  if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+    int hit = -1;
+#pragma unroll
+    for (int v = V - 1; v >= 0; --v) {
+      if (hit >= 0) break;
+      if (VEC) {
+        int lu = -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
+        const unsigned long long m = __ballot(lu >= 0);
+        if (m) {
+          const int l = 63 - __clzll((long long)m);
+          hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
+        }
+      } else {
+#pragma unroll
+        for (int u = 3; u >= 0; --u) {
+          if (hit >= 0) break;
+          const unsigned long long m =
+              __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
+          if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
+        }
+      }
+    }
+    if (hit >= 0) found = hit;
+  }
+#pragma unroll
+  for (int q = 0; q < NI; ++q) {
+    if (mode[q] == M_DONE || start[q] > c + CW - 1) continue;
+    if (mode[q] == M_CMP) {
+      int im = -1;  // first mismatching entry index in this chunk
+      if (cend[q] > c) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          if (im >= 0) break;
+          if (VEC) {
+            int first = 4;
+#pragma unroll
+            for (int u = 3; u >= 0; --u)
+              if (idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]) first = u;
+            const unsigned long long m = __ballot(first < 4);
+            if (m) {
+              const int l = first_lane(m);
+              im = c + 256 * v + 4 * l + __shfl(first, l, 64);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const unsigned long long m =
+                  __ballot(idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]);
+              if (m && im < 0) im = c + 64 * (4 * v + u) + first_lane(m);
+            }
+          }
+        }
+      }
+      if (im < 0 && cend[q] <= c + CW - 1) {
+        // Compared region ends in this chunk without a mismatch: either every
+        // entry matched (no truncation: the non-FIFO guard, :146-155) or the
+        // follower's log ends before the entries do ("beyond the end").
+        if (cend[q] < nend) im = cend[q];
+        else mode[q] = M_DONE;
+      }
+      if (im >= 0) {
+        cfrom[q] = im;
+        if (capok[q]) {
+          mode[q] = M_COPY;
+        } else {
+          mode[q] = M_DONE;  // MRAFT_ITEM_LOG_FULL: no state change
+          fullmask |= 1 << q;
+        }
+      }
+    }
+    if (mode[q] == M_COPY) {
+      if (!COUNT) {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
+            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
+          }
+        }
+      }
+      if (c + CW >= nend) mode[q] = M_DONE;
+    }
+  }
+}
+
+// Copy-only tail of the pass, once no follower is still comparing: every
+// follower in M_COPY receives the leader's entries [c, nend) (its copy start
+// is already behind c), VC dwordx4 loads per lane in flight per iteration,
+// and the commit scan [slo, shi] continues on the same loads.
+template <int NI, int VC, bool VEC, bool COUNT>
+__device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32_t *__restrict__ log,
+                                          long long eo,
+                                          const long long (&fo)[NI], const int (&mode)[NI], int c,
+                                          int nend, int phi, int slo, int shi, int T, int &found) {
+  constexpr int CW = 256 * VC;
+  const int lane = lane_id();
+  int cmask = 0;
+#pragma unroll
+  for (int q = 0; q < NI; ++q) cmask |= (mode[q] == M_COPY) ? (1 << q) : 0;
+  for (; c <= phi; c += CW) {
+    const bool scan = slo <= shi && c <= shi && c + CW - 1 >= slo;
+    if (!cmask && !(slo <= shi && c <= shi)) break;
+    int idx[VC][4], e[VC][4];
+#pragma unroll
+    for (int v = 0; v < VC; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
+#pragma unroll
+    for (int v = 0; v < VC; ++v) {
+      if (VEC) {
+        int4 x = make_int4(0, 0, 0, 0);
+        if (idx[v][0] <= phi) x = ld4(src + eo + idx[v][0]);
+        e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? ld1(src + eo + idx[v][u]) : 0;
+      }
+    }
+    if (scan) {
+      int hit = -1;
+#pragma unroll
+      for (int v = VC - 1; v >= 0; --v) {
+        if (hit >= 0) break;
+        if (VEC) {
+          int lu = -1;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
+          const unsigned long long m = __ballot(lu >= 0);
+          if (m) {
+            const int l = 63 - __clzll((long long)m);
+            hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
+          }
+        } else {
+#pragma unroll
+          for (int u = 3; u >= 0; --u) {
+            if (hit >= 0) break;
+            const unsigned long long m =
+                __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
+            if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
+          }
+        }
+      }
+      if (hit >= 0) found = hit;
+    }
+    if (!COUNT) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if (!((cmask >> q) & 1)) continue;
+#pragma unroll
+        for (int v = 0; v < VC; ++v) {
+          if (VEC && idx[v][3] < nend) {
+            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
+          }
+        }
+      }
+    }
+    if (c + CW >= nend) cmask = 0;
+  }
+}
+
+}  // namespace
+}  // namespace mraft

@@ -32,6 +32,7 @@
 // algorithmic word count of DESIGN.md §4 (reads, writes, active groups).
 #include "mraft_device.h"
 #include "mraft_internal.h"
+#include "mraft_pass.h"
 
 namespace mraft {
 
@@ -56,8 +57,6 @@ enum : int {
   IC_IS_PANIC   // InstallSnapshot whose sliceFrom would panic: dropped
 };
 
-enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };
-
 template <int P>
 __device__ __forceinline__ int quorum_match(const int (&m)[P], int lp) {
   // h-th largest (h = P/2) of matchIndex[j != me]: the largest i for which
@@ -80,267 +79,6 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 }
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-#ifndef MRAFT_TICK_NT
-#define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
-#endif
-
-// Streaming (read-once / write-once) log accesses of the pass.
-__device__ __forceinline__ int4 ld4(const int32_t *p) {
-  if (MRAFT_TICK_NT & 2) {
-    const int4 *q = reinterpret_cast<const int4 *>(p);
-    return make_int4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
-                     __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
-  }
-  return *reinterpret_cast<const int4 *>(p);
-}
-__device__ __forceinline__ int ld1(const int32_t *p) {
-  if (MRAFT_TICK_NT & 2) return __builtin_nontemporal_load(p);
-  return *p;
-}
-__device__ __forceinline__ void st4(int32_t *p, int a, int b, int c, int d) {
-  if (MRAFT_TICK_NT & 1) {
-    int4 *q = reinterpret_cast<int4 *>(p);
-    __builtin_nontemporal_store(a, &q->x);
-    __builtin_nontemporal_store(b, &q->y);
-    __builtin_nontemporal_store(c, &q->z);
-    __builtin_nontemporal_store(d, &q->w);
-  } else {
-    *reinterpret_cast<int4 *>(p) = make_int4(a, b, c, d);
-  }
-}
-__device__ __forceinline__ void st1(int32_t *p, int a) {
-  if (MRAFT_TICK_NT & 1) __builtin_nontemporal_store(a, p);
-  else *p = a;
-}
-
-// One chunk of the streaming pass over the leader's log. The pass serves
-// (1) every follower q's entry merge: compare entries [start_q, cend_q) with
-// the follower's log, then (from the first mismatch) copy entries up to `hi`
-// into it; and (2) the exact commit scan: the largest index in [slo, shi]
-// whose term equals T (kept in `found`, the pass ascends).
-// VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
-// otherwise lane j owns c+64(4v+u)+j. Leader entry idx is log[eo + idx],
-// follower q's is log[fo[q] + idx].
-template <int NI, int V, bool VEC, bool COUNT>
-__device__ __forceinline__ void pass_chunk(int32_t *__restrict__ log, long long eo,
-                                           const long long (&fo)[NI], const int (&start)[NI],
-                                           const int (&cend)[NI], int nend, int (&mode)[NI],
-                                           int (&cfrom)[NI], const int (&capok)[NI],
-                                           int &fullmask, int slo, int shi, int T, int &found,
-                                           int c, int plo, int phi) {
-  constexpr int CW = 256 * V;
-  const int lane = lane_id();
-  int idx[V][4], e[V][4];
-#pragma unroll
-  for (int v = 0; v < V; ++v)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
-  // Leader entries, then every comparing follower's terms: all loads in flight
-  // before the first compare.
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    if (VEC) {
-      int4 x = make_int4(0, 0, 0, 0);
-      if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(log + eo + idx[v][0]);
-      e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(log + eo + idx[v][u]) : 0;
-    }
-  }
-  int f[NI][V][4];
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {
-#pragma unroll
-    for (int v = 0; v < V; ++v)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) f[q][v][u] = 0;
-    if (mode[q] != M_CMP || start[q] > c + CW - 1 || cend[q] <= c) continue;
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      if (VEC) {
-        if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
-          const int4 x = ld4(log + fo[q] + idx[v][0]);
-          f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(log + fo[q] + idx[v][u]);
-      }
-    }
-  }
-  // Commit scan: highest index of this chunk in [slo, shi] with term T.
-  if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
-    int hit = -1;
-#pragma unroll
-    for (int v = V - 1; v >= 0; --v) {
-      if (hit >= 0) break;
-      if (VEC) {
-        int lu = -1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
-        const unsigned long long m = __ballot(lu >= 0);
-        if (m) {
-          const int l = 63 - __clzll((long long)m);
-          hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
-        }
-      } else {
-#pragma unroll
-        for (int u = 3; u >= 0; --u) {
-          if (hit >= 0) break;
-          const unsigned long long m =
-              __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
-          if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
-        }
-      }
-    }
-    if (hit >= 0) found = hit;
-  }
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {
-    if (mode[q] == M_DONE || start[q] > c + CW - 1) continue;
-    if (mode[q] == M_CMP) {
-      int im = -1;  // first mismatching entry index in this chunk
-      if (cend[q] > c) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          if (im >= 0) break;
-          if (VEC) {
-            int first = 4;
-#pragma unroll
-            for (int u = 3; u >= 0; --u)
-              if (idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]) first = u;
-            const unsigned long long m = __ballot(first < 4);
-            if (m) {
-              const int l = first_lane(m);
-              im = c + 256 * v + 4 * l + __shfl(first, l, 64);
-            }
-          } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const unsigned long long m =
-                  __ballot(idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]);
-              if (m && im < 0) im = c + 64 * (4 * v + u) + first_lane(m);
-            }
-          }
-        }
-      }
-      if (im < 0 && cend[q] <= c + CW - 1) {
-        // Compared region ends in this chunk without a mismatch: either every
-        // entry matched (no truncation: the non-FIFO guard, :146-155) or the
-        // follower's log ends before the entries do ("beyond the end").
-        if (cend[q] < nend) im = cend[q];
-        else mode[q] = M_DONE;
-      }
-      if (im >= 0) {
-        cfrom[q] = im;
-        if (capok[q]) {
-          mode[q] = M_COPY;
-        } else {
-          mode[q] = M_DONE;  // MRAFT_ITEM_LOG_FULL: no state change
-          fullmask |= 1 << q;
-        }
-      }
-    }
-    if (mode[q] == M_COPY) {
-      if (!COUNT) {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
-            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
-          }
-        }
-      }
-      if (c + CW >= nend) mode[q] = M_DONE;
-    }
-  }
-}
-
-// Copy-only tail of the pass, once no follower is still comparing: every
-// follower in M_COPY receives the leader's entries [c, nend) (its copy start
-// is already behind c), VC dwordx4 loads per lane in flight per iteration,
-// and the commit scan [slo, shi] continues on the same loads.
-template <int NI, int VC, bool VEC, bool COUNT>
-__device__ __forceinline__ void copy_loop(int32_t *__restrict__ log, long long eo,
-                                          const long long (&fo)[NI], const int (&mode)[NI], int c,
-                                          int nend, int phi, int slo, int shi, int T, int &found) {
-  constexpr int CW = 256 * VC;
-  const int lane = lane_id();
-  int cmask = 0;
-#pragma unroll
-  for (int q = 0; q < NI; ++q) cmask |= (mode[q] == M_COPY) ? (1 << q) : 0;
-  for (; c <= phi; c += CW) {
-    const bool scan = slo <= shi && c <= shi && c + CW - 1 >= slo;
-    if (!cmask && !(slo <= shi && c <= shi)) break;
-    int idx[VC][4], e[VC][4];
-#pragma unroll
-    for (int v = 0; v < VC; ++v)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
-#pragma unroll
-    for (int v = 0; v < VC; ++v) {
-      if (VEC) {
-        int4 x = make_int4(0, 0, 0, 0);
-        if (idx[v][0] <= phi) x = ld4(log + eo + idx[v][0]);
-        e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? ld1(log + eo + idx[v][u]) : 0;
-      }
-    }
-    if (scan) {
-      int hit = -1;
-#pragma unroll
-      for (int v = VC - 1; v >= 0; --v) {
-        if (hit >= 0) break;
-        if (VEC) {
-          int lu = -1;
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
-          const unsigned long long m = __ballot(lu >= 0);
-          if (m) {
-            const int l = 63 - __clzll((long long)m);
-            hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
-          }
-        } else {
-#pragma unroll
-          for (int u = 3; u >= 0; --u) {
-            if (hit >= 0) break;
-            const unsigned long long m =
-                __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
-            if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
-          }
-        }
-      }
-      if (hit >= 0) found = hit;
-    }
-    if (!COUNT) {
-#pragma unroll
-      for (int q = 0; q < NI; ++q) {
-        if (!((cmask >> q) & 1)) continue;
-#pragma unroll
-        for (int v = 0; v < VC; ++v) {
-          if (VEC && idx[v][3] < nend) {
-            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
-          }
-        }
-      }
-    }
-    if (c + CW >= nend) cmask = 0;
-  }
-}
 
 // Reply fold of one group (processAppendEntriesReply, :66-88, in peer order),
 // wave-uniform. Inputs per follower slot q come from lane q.
@@ -732,10 +470,10 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 #pragma unroll
         for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
         if (!cmp) break;
-        pass_chunk<NI, V, true, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
+        pass_chunk<NI, V, true, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
                                        fullmask, slo, shi, T, found, c, plo, phi);
       }
-      copy_loop<NI, VC, true, COUNT>(s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
+      copy_loop<NI, VC, true, COUNT>(s.log, s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
     } else {
       int c = plo;
       for (; c <= phi; c += 256 * V) {
@@ -743,10 +481,10 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 #pragma unroll
         for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
         if (!cmp) break;
-        pass_chunk<NI, V, false, COUNT>(s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
+        pass_chunk<NI, V, false, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
                                         fullmask, slo, shi, T, found, c, plo, phi);
       }
-      copy_loop<NI, VC, false, COUNT>(s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
+      copy_loop<NI, VC, false, COUNT>(s.log, s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
     }
   }
   TICK_STAMP(2);
