@@ -897,11 +897,11 @@ int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
 /* voter order.                                                              */
 /* ------------------------------------------------------------------------ */
 
-int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
-                        int32_t *group_flags) {
+static int election_rounds_range(ora_engine *e, const uint8_t *cand_mask, int32_t R,
+                                 int32_t *group_flags, int32_t g_begin, int32_t g_end) {
   const int32_t P = e->P, G = e->G;
   if (P > 8) return MRAFT_E_INVAL;
-  for (int32_t g = 0; g < G; ++g) {
+  for (int32_t g = g_begin; g < g_end; ++g) {
     int32_t fl = 0;
     for (int32_t r = 0; r < R; ++r) {
       const uint8_t m = cand_mask[(int64_t)r * G + g];
@@ -929,6 +929,41 @@ int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
     }
     if (group_flags) group_flags[g] = fl;
   }
+  return MRAFT_OK;
+}
+
+int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
+                        int32_t *group_flags) {
+  return election_rounds_range(e, cand_mask, R, group_flags, 0, e->G);
+}
+
+typedef struct {
+  ora_engine *e;
+  const uint8_t *m;
+  int32_t R, b, en;
+  int32_t *gf;
+} el_job;
+
+static void *el_worker(void *arg) {
+  el_job *j = (el_job *)arg;
+  election_rounds_range(j->e, j->m, j->R, j->gf, j->b, j->en);
+  return NULL;
+}
+
+/* Groups split contiguously over nthreads (CPU baseline of config #5). */
+int ora_election_rounds_mt(ora_engine *e, const uint8_t *cand_mask, int32_t R,
+                           int32_t *group_flags, int32_t nthreads) {
+  if (nthreads <= 1) return ora_election_rounds(e, cand_mask, R, group_flags);
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  el_job jobs[256];
+  for (int32_t t = 0; t < nthreads; ++t) {
+    jobs[t].e = e; jobs[t].m = cand_mask; jobs[t].R = R; jobs[t].gf = group_flags;
+    jobs[t].b = (int32_t)((int64_t)e->G * t / nthreads);
+    jobs[t].en = (int32_t)((int64_t)e->G * (t + 1) / nthreads);
+    pthread_create(&th[t], NULL, el_worker, &jobs[t]);
+  }
+  for (int32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   return MRAFT_OK;
 }
 

@@ -86,6 +86,8 @@ int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
                              int32_t *item_err);
 int ora_election_rounds(ora_engine *e, const uint8_t *cand_mask, int32_t R,
                         int32_t *group_flags);
+int ora_election_rounds_mt(ora_engine *e, const uint8_t *cand_mask, int32_t R,
+                           int32_t *group_flags, int32_t nthreads);
 int ora_export_group_status(ora_engine *e, const int32_t *leader_peer,
                             int32_t *commit, int32_t *term_leader);
 

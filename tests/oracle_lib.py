@@ -43,6 +43,7 @@ def lib():
             "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
             "ora_export_group_status": [E, vp, vp, vp],
             "ora_election_rounds": [E, vp, i32, vp],
+            "ora_election_rounds_mt": [E, vp, i32, vp, i32],
             "ora_snapshot": [E, vp, vp, i64, vp],
             "ora_gather_install_snapshot_args": [E, vp, vp, i64, vp, vp],
             "ora_handle_install_snapshot": [E, vp, i64, vp, vp, vp],
@@ -210,10 +211,10 @@ class Oracle:
                                        0 if sb is None else len(sb) - 1, ptr(flags), ptr(err))
         return flags, err
 
-    def election_rounds(self, cand_mask):
+    def election_rounds(self, cand_mask, nthreads: int = 1):
         m = np.ascontiguousarray(cand_mask, dtype=np.uint8)
         gf = np.zeros(self.G, np.int32)
-        lib().ora_election_rounds(ctypes.byref(self._e), ptr(m), m.shape[0], ptr(gf))
+        lib().ora_election_rounds_mt(ctypes.byref(self._e), ptr(m), m.shape[0], ptr(gf), nthreads)
         return gf
 
     # ---- persistence ---------------------------------------------------------

@@ -377,3 +377,12 @@ def test_goshaped_reset_restores():
                         {k: v for k, v in st.items() if k != "persist_dirty"}, G, P, L, "reset")
     g.replicate_tick(lp, nthreads=1)
     assert_states_equal(g.state(), first, G, P, L, "re-run")
+
+
+def test_election_rounds_mt_equals_st():
+    from multiraft_amd import synth_election_state
+    G, P, L, R = 512, 7, 16, 8
+    st, mask = synth_election_state(G, P, L, seed=13, rounds=R)
+    a, b = Oracle(G, P, L, st), Oracle(G, P, L, st)
+    assert np.array_equal(a.election_rounds(mask), b.election_rounds(mask, nthreads=6))
+    assert_states_equal(a.state(), b.state(), G, P, L, "election mt")
