@@ -359,6 +359,16 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts,
 int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to,
                         int32_t where);
 
+/* Applier, compacted: only the slots with commitIndex >
+ * lastApplied, in ascending slot order: out_slots[k], and their ApplyMsg
+ * range (out_from[k] - 1, out_to[k]] = (lastApplied, commitIndex]. *out_n =
+ * the number of such slots; the first min(*out_n, cap) are written and only
+ * those advance lastApplied to commitIndex (raft.go:200), so a caller with a
+ * small buffer calls again for the rest. */
+int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots,
+                                int32_t *out_from, int32_t *out_to,
+                                int64_t cap, int64_t *out_n, int32_t where);
+
 /* ---- snapshots --------------------------------------- */
 
 /* Snapshot (raft_snapshot.go:3-13) for n items: if index[i] > dummyIndex, the

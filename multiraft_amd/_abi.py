@@ -88,6 +88,7 @@ ABI_SYMBOLS = (
     "mraft_export_group_status", "mraft_collect_persist", "mraft_read_persistent",
     "mraft_restore", "mraft_encode_persistent", "mraft_decode_persistent",
     "mraft_key2shard", "mraft_realloc_gid", "mraft_replicate_tick_export",
+    "mraft_collect_apply_compact",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -128,6 +129,7 @@ _SIGS = {
     "mraft_decode_persistent": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64]),
     "mraft_key2shard": (ctypes.c_int, [ctypes.c_char_p, _i64, _i32]),
     "mraft_replicate_tick_export": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32]),
+    "mraft_collect_apply_compact": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i32]),
     "mraft_realloc_gid": (ctypes.c_int, [_vp, _i32, _vp, _i32]),
 }
 _SYNTH_SIGS = {

@@ -459,6 +459,24 @@ int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int
   return sg.finish();
 }
 
+int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *out_from,
+                                int32_t *out_to, int64_t cap, int64_t *out_n, int32_t where) {
+  TRY(check(h));
+  if (cap < 0 || !out_n || (cap > 0 && (!out_slots || !out_from || !out_to)))
+    return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *sl, *f, *t, *n, *bc;
+  TRY(sg.map(out_slots, sizeof(int32_t) * (size_t)cap, false, true, &sl));
+  TRY(sg.map(out_from, sizeof(int32_t) * (size_t)cap, false, true, &f));
+  TRY(sg.map(out_to, sizeof(int32_t) * (size_t)cap, false, true, &t));
+  TRY(sg.map(out_n, sizeof(int64_t), false, true, &n));
+  TRY(scratch(h, 6, sizeof(int32_t) * (size_t)((gp_of(h) + 255) / 256), &bc));
+  mraft::launch_collect_apply_compact(dev_of(h), (int32_t *)bc, cap, (int32_t *)sl, (int32_t *)f,
+                                      (int32_t *)t, (int64_t *)n, h->stream);
+  return sg.finish();
+}
+
 int mraft_snapshot(mraft_engine *h, const int32_t *slots, const int32_t *index, int64_t n,
                    int32_t *item_err, int32_t where) {
   TRY(check(h));

@@ -32,6 +32,8 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
                   int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st);
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t st);
+void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t cap, int32_t *oslot,
+                                  int32_t *ofrom, int32_t *oto, int64_t *total, hipStream_t st);
 void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,
                      int32_t *err, hipStream_t st);
 void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,

@@ -353,6 +353,66 @@ __global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__re
   }
 }
 
+// Compacted applier: slots with commitIndex > lastApplied, ascending, in
+// three launches (per-block counts, one-workgroup exclusive scan, emit).
+__global__ __launch_bounds__(256) void k_apply_count(Dev s, int32_t *__restrict__ bcnt) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool pend = i < gp && s.commit[i] > s.applied[i];
+  const unsigned long long m = __ballot(pend);
+  __shared__ int wc[4];
+  if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(1024) void k_apply_scan(int32_t *__restrict__ bcnt, int64_t nb,
+                                                     int64_t *__restrict__ total) {
+  __shared__ int64_t part[1024];
+  int64_t carry = 0;
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < nb ? bcnt[i] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+      const int64_t add = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < nb) bcnt[i] = (int32_t)(carry + part[threadIdx.x] - v);  // exclusive offset
+    const int64_t chunk = part[1023];
+    __syncthreads();
+    carry += chunk;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_apply_emit(Dev s, const int32_t *__restrict__ boff, int64_t cap,
+                                                    int32_t *__restrict__ oslot, int32_t *__restrict__ ofrom,
+                                                    int32_t *__restrict__ oto) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int la = 0, ci = 0;
+  if (i < gp) { la = s.applied[i]; ci = s.commit[i]; }
+  const bool pend = i < gp && ci > la;
+  const unsigned long long m = __ballot(pend);
+  __shared__ int wc[4];
+  if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  const int w = threadIdx.x >> 6;
+  int off = boff[blockIdx.x];
+  for (int k = 0; k < w; ++k) off += wc[k];
+  off += __popcll(m & ((1ull << lane_id()) - 1));
+  if (pend && off < cap) {
+    oslot[off] = (int32_t)i;
+    ofrom[off] = la + 1;                                               // raft.go:179-190
+    oto[off] = ci;
+    s.applied[i] = ci;                                                 // :200
+  }
+}
+
 // ---------------------------------------------------------------- snapshots
 // Snapshot (raft_snapshot.go:3-13): wave per item.
 __global__ __launch_bounds__(256) void k_snapshot(Dev s, const int32_t *__restrict__ slots,
@@ -750,6 +810,16 @@ void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t 
   int blocks = blocks_for((int64_t)s.G * s.P);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_collect_apply, dim3(blocks), dim3(kBlock), 0, st, s, from, to);
+}
+
+void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t cap, int32_t *oslot,
+                                  int32_t *ofrom, int32_t *oto, int64_t *total, hipStream_t st) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  const int64_t nb = (gp + 255) / 256;
+  hipLaunchKernelGGL(k_apply_count, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt);
+  hipLaunchKernelGGL(k_apply_scan, dim3(1), dim3(1024), 0, st, scratch_bcnt, nb, total);
+  hipLaunchKernelGGL(k_apply_emit, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt, cap, oslot,
+                     ofrom, oto);
 }
 
 void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,

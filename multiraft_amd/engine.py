@@ -235,6 +235,17 @@ class Engine:
         _ck(self._lib.mraft_collect_apply(self._h, ptr(fr), ptr(to), HOST), "mraft_collect_apply")
         return fr, to
 
+    def collect_apply_compact(self, cap: int | None = None):
+        """Applier, compacted: (slots, from, to, total) for the slots with
+        commitIndex > lastApplied, ascending; only the returned ones advance."""
+        cap = self.G * self.P if cap is None else cap
+        sl, fr, to = (np.zeros(max(cap, 1), np.int32) for _ in range(3))
+        n = np.zeros(1, np.int64)
+        _ck(self._lib.mraft_collect_apply_compact(self._h, ptr(sl), ptr(fr), ptr(to), cap, ptr(n), HOST),
+            "mraft_collect_apply_compact")
+        k = int(min(n[0], cap))
+        return sl[:k].copy(), fr[:k].copy(), to[:k].copy(), int(n[0])
+
     # ---- snapshots (raft_snapshot.go) -------------------------------------
     def snapshot(self, slots, index):
         slots = np.ascontiguousarray(slots, dtype=np.int32)

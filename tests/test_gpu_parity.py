@@ -314,3 +314,32 @@ def test_start_and_applier_gpu():
             ofr, oto = o.collect_apply()
             assert np.array_equal(fr, ofr) and np.array_equal(to, oto)
         assert_states_equal(e.store_state(), o.state(), G, P, L, "applier")
+
+
+@pytest.mark.parametrize("cap", [None, 37])
+def test_applier_compact_gpu(cap):
+    """The compacted applier lists exactly the slots whose range is non-empty,
+    ascending, with the dense applier's ranges; with a short buffer only the
+    listed slots advance, and a second call returns the rest."""
+    G, P, L = 700, 5, 64
+    st, lp, _ = synth_tick_state(G, P, L, seed=81)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        assert np.array_equal(e.replicate_tick(lp), o.replicate_tick(lp))
+        pre = e.store_state()
+        fr, to = o.collect_apply()
+        want = np.nonzero(to >= fr)[0]
+        sl, f, t, n = e.collect_apply_compact(cap)
+        assert n == len(want) and n > 40
+        k = len(sl)
+        assert k == (n if cap is None else min(cap, n))
+        assert np.array_equal(sl, want[:k]) and np.array_equal(f, fr[want[:k]]) and np.array_equal(t, to[want[:k]])
+        got = e.store_state()
+        exp_applied = pre["last_applied"].copy()
+        exp_applied[want[:k]] = pre["commit_index"][want[:k]]
+        assert np.array_equal(got["last_applied"], exp_applied)
+        if cap is not None:
+            sl2, f2, t2, n2 = e.collect_apply_compact()
+            assert n2 == n - k and np.array_equal(sl2, want[k:])
+        assert e.collect_apply_compact()[3] == 0
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "applier compact")
