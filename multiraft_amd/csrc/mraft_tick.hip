@@ -182,6 +182,13 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #ifndef MRAFT_TICK_HDR1
 #define MRAFT_TICK_HDR1 0  // 1: header scalars loaded by group index with leader_peer (one round trip fewer; measured no gain: HBM-bound)
 #endif
+#ifndef MRAFT_TICK_HNT
+#define MRAFT_TICK_HNT 0   // 1: the header's single-word log reads non-temporal too
+#endif
+__device__ __forceinline__ int hld(const int32_t *p) {
+  if (MRAFT_TICK_HNT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 #ifndef MRAFT_TICK_WPB
 #define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
 #endif
@@ -335,11 +342,11 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     return;
   }
   int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + (last - ldummy)]);  // speculative a1 probe
+  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(hld(s.log + lrow + (last - ldummy)));  // speculative a1 probe
   int prev_term = 0, ft = 0;
   if (icls == IC_GO && MRAFT_TICK_EXP != 3) {
-    prev_term = s.log[lrow + (prev - ldummy)];                           // :49
-    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + (prev - fdummy)];
+    prev_term = hld(s.log + lrow + (prev - ldummy));                     // :49
+    if (prev >= fdummy && prev <= flast) ft = hld(s.log + f * L + (prev - fdummy));
   }
   const int n = last - prev;                                             // :50
   int rterm = 0, rsucc = 0, rci = 0;
