@@ -176,6 +176,9 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
+#ifndef MRAFT_TICK_XCD_STAGGER
+#define MRAFT_TICK_XCD_STAGGER 0  // 1: stagger each XCD's start inside its range
+#endif
 #ifndef MRAFT_TICK_XCD_CHUNK
 #define MRAFT_TICK_XCD_CHUNK 0  // 0: one contiguous range of groups per XCD; else chunks of this many
 #endif
@@ -230,7 +233,14 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
   } else if (MRAFT_TICK_XCD) {
     const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
-    gb = x * per + min(x, rem) + (gb >> 3);
+    int k = gb >> 3;
+    if (MRAFT_TICK_XCD_STAGGER && rem == 0 && per > 0) {
+      // XCD x starts x/8 of the way into its range (and wraps): the eight
+      // XCDs never stream the same offset of their ranges at the same time.
+      k += (int)(((long long)x * per) >> 3);
+      if (k >= per) k -= per;
+    }
+    gb = x * per + min(x, rem) + k;
   }
   const int g = uni(gb * MRAFT_TICK_WPB + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
