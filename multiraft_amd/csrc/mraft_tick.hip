@@ -176,22 +176,6 @@ __device__ unsigned long long g_tick_trace[65536 * 4];
 #ifndef MRAFT_TICK_XCD
 #define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
 #endif
-#ifndef MRAFT_TICK_XCD_STAGGER
-#define MRAFT_TICK_XCD_STAGGER 0  // 1: stagger each XCD's start inside its range
-#endif
-#ifndef MRAFT_TICK_XCD_CHUNK
-#define MRAFT_TICK_XCD_CHUNK 0  // 0: one contiguous range of groups per XCD; else chunks of this many
-#endif
-#ifndef MRAFT_TICK_HDR1
-#define MRAFT_TICK_HDR1 0  // 1: header scalars loaded by group index with leader_peer (one round trip fewer; measured no gain: HBM-bound)
-#endif
-#ifndef MRAFT_TICK_HNT
-#define MRAFT_TICK_HNT 0   // 1: the header's single-word log reads non-temporal too
-#endif
-__device__ __forceinline__ int hld(const int32_t *p) {
-  if (MRAFT_TICK_HNT) return __builtin_nontemporal_load(p);
-  return *p;
-}
 #ifndef MRAFT_TICK_WPB
 #define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
 #endif
@@ -221,26 +205,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // scalar SoA lines neighbouring groups share stay in one XCD's L2. Speed
   // only; any placement gives the same results.
   int gb = (int)blockIdx.x;
-  if (MRAFT_TICK_XCD && MRAFT_TICK_XCD_CHUNK > 0) {
-    // XCD x takes chunks x, x+8, x+16, ... of MRAFT_TICK_XCD_CHUNK consecutive
-    // groups: neighbours still share an L2, and every XCD's work is spread
-    // over the whole image. The tail that does not fill 8 chunks keeps its order.
-    constexpr int C = MRAFT_TICK_XCD_CHUNK > 0 ? MRAFT_TICK_XCD_CHUNK : 1;
-    const int full = ((int)gridDim.x / (8 * C)) * (8 * C);
-    if (gb < full) {
-      const int x = gb & 7, k = gb >> 3;
-      gb = ((k / C) * 8 + x) * C + (k % C);
-    }
-  } else if (MRAFT_TICK_XCD) {
+  if (MRAFT_TICK_XCD) {
     const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
-    int k = gb >> 3;
-    if (MRAFT_TICK_XCD_STAGGER && rem == 0 && per > 0) {
-      // XCD x starts x/8 of the way into its range (and wraps): the eight
-      // XCDs never stream the same offset of their ranges at the same time.
-      k += (int)(((long long)x * per) >> 3);
-      if (k >= per) k -= per;
-    }
-    gb = x * per + min(x, rem) + k;
+    gb = x * per + min(x, rem) + (gb >> 3);
   }
   const int g = uni(gb * MRAFT_TICK_WPB + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
@@ -248,51 +215,6 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   TICK_STAMP(0);
 
   // ------------------------------------------------------------ header
-#if MRAFT_TICK_HDR1
-  // Every scalar the header needs is indexed by the group alone (the P
-  // replicas' scalars, the P matchIndex / nextIndex rows: the same lines the
-  // leader's own words sit on), so it is issued together with leader_peer[g]
-  // and the leader's and followers' words are then picked out of registers:
-  // one dependent round trip fewer than loading by leader slot.
-  const long long gs = (long long)g * P;
-  int r_term = 0, r_dummy = 0, r_last = 0, r_commit = 0, r_role = 0, r_match = 0, r_next = 0;
-  if (lane < P) {
-    r_term = s.term[gs + lane];
-    r_dummy = s.dummy[gs + lane];
-    r_last = s.last[gs + lane];
-    r_commit = s.commit[gs + lane];
-    r_role = s.role[gs + lane];
-  }
-  if (lane < P * P) {
-    r_match = s.match[gs * P + lane];
-    r_next = s.next[gs * P + lane];
-  }
-  const int lp = uni(leader_peer[g]);
-  if (lp < 0 || lp >= P) {
-    const int e_c = __builtin_amdgcn_readlane(r_commit, 0), e_t = __builtin_amdgcn_readlane(r_term, 0),
-              e_r = __builtin_amdgcn_readlane(r_role, 0);  // mraft_export_group_status: replica 0
-    if (!COUNT && lane == 0) {
-      if (gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
-      ex.put(g, e_c, e_t, e_r);
-    }
-    return;
-  }
-  const long long ld = gs + lp;
-  const long long lrow = ld * L;
-  const int role = __builtin_amdgcn_readlane(r_role, lp), T = __builtin_amdgcn_readlane(r_term, lp),
-            c0 = __builtin_amdgcn_readlane(r_commit, lp), last = __builtin_amdgcn_readlane(r_last, lp),
-            ldummy = __builtin_amdgcn_readlane(r_dummy, lp);
-  int mm[P];
-#pragma unroll
-  for (int j = 0; j < P; ++j) mm[j] = __builtin_amdgcn_readlane(r_match, lp * P + j);
-  const int p = lane < lp ? lane : lane + 1;
-  const long long f = gs + p;
-  const int fp = lane < NI ? p : 0;
-  int nxt = __shfl(r_next, lp * P + fp, 64), fterm = __shfl(r_term, fp, 64),
-      fdummy = __shfl(r_dummy, fp, 64), flast = __shfl(r_last, fp, 64),
-      fcommit = __shfl(r_commit, fp, 64);
-  if (lane >= NI) nxt = fterm = fdummy = flast = fcommit = 0;
-#else
   const int lp = uni(leader_peer[g]);
   if (lp < 0 || lp >= P) {
     if (!COUNT && lane == 0) {
@@ -322,7 +244,6 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     flast = s.last[f];
     fcommit = s.commit[f];
   }
-#endif
   long long hR = 1;  // algorithmic words of the header (wave-uniform)
   if (role != kLeader || c0 < ldummy) {
     // not a leader: appendOneRound returns (:22-25); commit < dummy: outside
@@ -352,11 +273,11 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     return;
   }
   int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(hld(s.log + lrow + (last - ldummy)));  // speculative a1 probe
+  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + (last - ldummy)]);  // speculative a1 probe
   int prev_term = 0, ft = 0;
   if (icls == IC_GO && MRAFT_TICK_EXP != 3) {
-    prev_term = hld(s.log + lrow + (prev - ldummy));                     // :49
-    if (prev >= fdummy && prev <= flast) ft = hld(s.log + f * L + (prev - fdummy));
+    prev_term = s.log[lrow + (prev - ldummy)];                           // :49
+    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + (prev - fdummy)];
   }
   const int n = last - prev;                                             // :50
   int rterm = 0, rsucc = 0, rci = 0;
