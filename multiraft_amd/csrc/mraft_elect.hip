@@ -19,8 +19,11 @@ namespace {
 #ifndef MRAFT_EL_SPARSE
 #define MRAFT_EL_SPARSE 1  // voter loop over the round's candidates only (else all P peers)
 #endif
+#ifndef MRAFT_EL_TALLY_CF
+#define MRAFT_EL_TALLY_CF 1  // closed-form vote tally (else the per-reply fold)
+#endif
 #ifndef MRAFT_EL_GM_LDS
-#define MRAFT_EL_GM_LDS 0  // grant-mask transpose through LDS (else __shfl; measured faster)
+#define MRAFT_EL_GM_LDS 2  // grant-mask transpose: 2 ballots (else 1 LDS bytes, 0 __shfl)
 #endif
 
 template <int P>
@@ -145,11 +148,52 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       const unsigned long long gw = *reinterpret_cast<const unsigned long long *>(&lds_gm[threadIdx.x & ~7u]);
       mine = (int)((((gw >> p) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
       __builtin_amdgcn_wave_barrier();
+    } else if (MRAFT_EL_GM_LDS == 2) {
+      // One ballot per candidate bit: bit seg+v of b_c = voter v granted c.
+      unsigned long long bs = 0;
+#pragma unroll
+      for (int c = 0; c < P; ++c) {
+        const unsigned long long b = __ballot((gm >> c) & 1);
+        bs = p == c ? b : bs;
+      }
+      mine = (int)((bs >> seg) & 0xffull);
     } else {
 #pragma unroll
       for (int v = 0; v < P; ++v) mine |= ((__shfl(gm, v, 8) >> p) & 1) << v;
     }
     // Tally (closure :22-47): candidate p folds its replies in voter order.
+    // The guard (:29) can only flip at the first event, becoming leader at the
+    // grant that makes a majority (:32-38) or stepping down at the first
+    // refusal whose reply.Term exceeds args.Term (:42-45), so the fold is
+    // closed-form: whichever of the two positions comes first in voter order.
+#if MRAFT_EL_TALLY_CF
+    {
+      const bool ok0 = isc && term == at && role == kCandidate;
+      const int om = ((1 << P) - 1) & ~(1 << p);
+      int gt = 0, tv = 0;
+#pragma unroll
+      for (int v = 0; v < P; ++v) gt |= (int)((cx[v] & 0x7fffffff) > at) << v;
+      // reply.Term = max(voter's own term, pmx) > at: every refusal when pmx > at.
+      const int smask = om & ~mine & (pmx > at ? om : gt);
+      int mm = mine & om;
+#pragma unroll
+      for (int k = 1; k < (P / 2 > 1 ? P / 2 : 1); ++k) mm &= mm - 1;  // the (P/2)-th grant
+      const int lpos = mm ? __builtin_ctz(mm) : 32;
+      const int spos = smask ? __builtin_ctz(smask) : 32;
+#pragma unroll
+      for (int v = 0; v < P; ++v) tv = spos == v ? (cx[v] & 0x7fffffff) : tv;
+      const bool lead = ok0 && lpos < spos;
+      const bool sd = ok0 && spos < lpos;
+      const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
+      votes += ok0 ? __builtin_popcount(mine & om & upto) : 0;                // :31
+      role = lead ? kLeader : sd ? kFollower : role;
+      became |= (int)lead;
+      fl |= lead ? MRAFT_G_ELECTED : 0;
+      term = sd ? max(tv, pmx) : term;
+      voted = sd ? -1 : voted;
+      fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
+    }
+#else
 #pragma unroll
     for (int v = 0; v < P; ++v) {
       const bool ok = isc && v != p && term == at && role == kCandidate;  // :29
@@ -166,6 +210,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       voted = sd ? -1 : voted;
       fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
     }
+#endif
   }
   const unsigned long long el = __ballot(fl & MRAFT_G_ELECTED), sd = __ballot(fl & MRAFT_G_STEPPED_DOWN);
   if (grp && p == 0 && gflags) {
