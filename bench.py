@@ -255,6 +255,10 @@ def main():
     chain = world == 1 and not restore
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
 
+    # The all-gather, timed on its own (reported beside the step).
+    ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if world > 1 else []
+    ag_ms = []
+
     def mark_start(i):
         return marks[i] if chain else marks[2 * i]
 
@@ -277,9 +281,16 @@ def main():
             mark_end(i).record(stream)
         if world > 1:  # the shard router's fan-in
             if on_host:
+                t1 = time.perf_counter()
                 allgather_status(commit_d.cpu(), tl_d.cpu())
+                if timed:
+                    ag_ms.append((time.perf_counter() - t1) * 1e3)
             else:
+                if timed:
+                    ag_marks[2 * i].record(stream)
                 allgather_status(commit_d, tl_d)
+                if timed:
+                    ag_marks[2 * i + 1].record(stream)
 
     for i in range(W):
         step(i, False)
@@ -296,6 +307,8 @@ def main():
     ker_ms = [mark_start(i).elapsed_time(mark_end(i)) for i in range(K)]
     log(rank, "tick kernel ms per step: " + " ".join(f"{x:.3f}" for x in ker_ms))
     flags = gf_d.cpu().numpy()
+    if world > 1 and not on_host:
+        ag_ms = [ag_marks[2 * i].elapsed_time(ag_marks[2 * i + 1]) for i in range(K)]
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if on_host else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -336,7 +349,9 @@ def main():
                                   if args.config == 2 else ""),
                    "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
                    "committed_groups_last_step": int(((flags & 2) != 0).sum()),
-                   "active_groups": active, "restore_in_timed_step": restore},
+                   "active_groups": active, "restore_in_timed_step": restore,
+                   "allgather_ms_mean": float(np.mean(ag_ms)) if ag_ms else None,
+                   "allgather_bytes_per_rank": 8 * G if world > 1 else 0},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,

@@ -40,7 +40,8 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 __device__ __forceinline__ int first_lane(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
 // Largest idx in [lo, hi] with row[idx - base] != a, scanning downward; returns
-// lo - 1 when every term in the range equals a. Wave-uniform arguments.
+// lo - 1 when every term in the range equals a. Wave-uniform arguments;
+// row[lo - base] must be readable when lo <= hi (lanes past lo re-read it).
 __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base,
                                                  int lo, int hi, int a) {
   const int lane = lane_id();
@@ -48,14 +49,19 @@ __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row
     int v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      int idx = top - lane - kWave * u;
-      v[u] = idx >= lo ? row[idx - base] : a;
+      const int idx = top - lane - kWave * u;
+      const int w = row[max(idx, lo) - base];  // unconditional: the loads issue back to back
+      v[u] = idx >= lo ? w : a;
     }
+    // Every ballot, no exit per vector (which lets the compiler sink each load
+    // behind the previous compare: one round trip per 64 terms).
+    int r = lo - 1;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      unsigned long long m = __ballot(v[u] != a);
-      if (m) return top - kWave * u - first_lane(m);
+    for (int u = kUnroll - 1; u >= 0; --u) {
+      const unsigned long long m = __ballot(v[u] != a);
+      r = m ? top - kWave * u - first_lane(m) : r;
     }
+    if (r >= lo) return r;
   }
   return lo - 1;
 }
@@ -68,14 +74,17 @@ __device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row
     int v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      int idx = top - lane - kWave * u;
-      v[u] = idx >= lo ? row[idx - base] : a + 1;
+      const int idx = top - lane - kWave * u;
+      const int w = row[max(idx, lo) - base];
+      v[u] = idx >= lo ? w : a + 1;
     }
+    int r = lo - 1;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      unsigned long long m = __ballot(v[u] == a);
-      if (m) return top - kWave * u - first_lane(m);
+    for (int u = kUnroll - 1; u >= 0; --u) {
+      const unsigned long long m = __ballot(v[u] == a);
+      r = m ? top - kWave * u - first_lane(m) : r;
     }
+    if (r >= lo) return r;
   }
   return lo - 1;
 }
@@ -104,15 +113,18 @@ __device__ __forceinline__ int wave_merge_compare(const int32_t *__restrict__ E,
     int e[kUnroll], f[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      int k = base + lane + kWave * u;
-      e[u] = k < kc ? E[k] : 0;
-      f[u] = k < kc ? F[k] : 0;
+      const int k = base + lane + kWave * u, kk = min(k, kc - 1);
+      const int x = E[kk], y = F[kk];
+      e[u] = k < kc ? x : 0;
+      f[u] = k < kc ? y : 0;
     }
+    int r = -1;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      unsigned long long m = __ballot(e[u] != f[u]);
-      if (m) return base + kWave * u + first_lane(m);
+    for (int u = kUnroll - 1; u >= 0; --u) {
+      const unsigned long long m = __ballot(e[u] != f[u]);
+      r = m ? base + kWave * u + first_lane(m) : r;
     }
+    if (r >= 0) return r;
   }
   return -1;
 }

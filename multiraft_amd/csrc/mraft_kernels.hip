@@ -12,6 +12,8 @@ namespace {
 
 constexpr int kBlock = 256;
 
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 inline int blocks_for(int64_t n, int per_block = kBlock) {
   int64_t b = (n + per_block - 1) / per_block;
   return (int)(b < 1 ? 1 : b);
@@ -102,11 +104,24 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
 
 // ---------------------------------------------------------------- a4
 // One wave per item: uniform prologue, wave-cooperative conflict scan / merge.
-__global__ __launch_bounds__(256) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
+#ifndef MRAFT_AE_WPB
+#define MRAFT_AE_WPB 1  // messages (waves) per workgroup of the AppendEntries handler (1: 6 % faster than 4)
+#endif
+#ifndef MRAFT_AE_XCD
+#define MRAFT_AE_XCD 1  // each XCD takes a contiguous range of workgroups: a group's consecutive
+                        // messages share one L2 for the leader entries (another 8 %)
+#endif
+
+__global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
                                                    int64_t n, const int32_t *__restrict__ ent,
                                                    int64_t n_ent, mraft_ae_reply *__restrict__ rep,
                                                    int32_t *__restrict__ err) {
-  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  int64_t gb = blockIdx.x;
+  if (MRAFT_AE_XCD) {
+    const int64_t nb = gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
+    gb = x * per + min(x, rem) + (gb >> 3);
+  }
+  const int64_t i = gb * MRAFT_AE_WPB + (threadIdx.x >> 6);
   if (i >= n) return;
   const int lane = lane_id();
   mraft_ae_reply r = {0, 0, 0, 0};
@@ -215,104 +230,221 @@ __device__ __forceinline__ int quorum_rt(const int (&m)[8], int me) {
   return best;
 }
 
-// Wave per segment: the segment's replies folded in order (wave-uniform), a1
-// evaluated after each successful reply exactly as raft_append_entry.go:78
-// calls it. a1's downward scan for the current-term gate (:90-103) is
-// wave-cooperative and incremental: the term is fixed while the replica stays
-// leader, and an evaluation that scanned (commit, top] leaves no entry of that
-// term above the new commit index up to top, so a later evaluation only scans
-// (H, top'] with H the highest index scanned so far — the same result as
-// rescanning from the top every time, with each log word read at most once.
+#ifndef MRAFT_FOLD_GRID
+#define MRAFT_FOLD_GRID (1 << 30)  // workgroups of the reply fold (segments beyond: grid-stride)
+#endif
+#ifndef MRAFT_FOLD_TRACE
+#define MRAFT_FOLD_TRACE 0  // diagnostic build: s_memrealtime stamps per segment (tools/trace_fold.py)
+#endif
+#if MRAFT_FOLD_TRACE
+__device__ unsigned long long g_fold_trace[65536 * 6];
+#define FOLD_STAMP(k, dep)                                                                         \
+  do {                                                                                             \
+    if (sg < 65536 && lane == 0) {                                                                 \
+      asm volatile("" ::"v"(dep));                                                                 \
+      g_fold_trace[sg * 6 + (k)] = __builtin_amdgcn_s_memrealtime();                               \
+    }                                                                                              \
+  } while (0)
+#else
+#define FOLD_STAMP(k, dep) do {} while (0)
+#endif
+#ifndef MRAFT_FOLD_XCD
+#define MRAFT_FOLD_XCD 0  // 1: XCD-contiguous segment ranges
+#endif
+#ifndef MRAFT_FOLD_MINW
+#define MRAFT_FOLD_MINW 8  // __launch_bounds__ minimum waves per SIMD of the reply fold (8: SGPRs spill to VGPR lanes, 13 % faster than 7 waves)
+#endif
+
+#ifndef MRAFT_FOLD_EXP
+#define MRAFT_FOLD_EXP 0  // timing experiments only (wrong results): 1 = no a1 log reads, 2 = probes only
+#endif
+#ifndef MRAFT_FOLD_SCANU
+#define MRAFT_FOLD_SCANU 4  // a1 scan: dword loads per lane in flight per iteration (64·U terms)
+#endif
+
+// Highest idx in [lo, hi] with row[idx - base] == a, or lo - 1: the a1 scan
+// of the reply fold, 64·U terms per round trip (wave-uniform arguments).
+template <int U>
+__device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row, int base, int lo, int hi,
+                                                 int a) {
+  const int lane = lane_id();
+  for (int top = hi; top >= lo; top -= kWave * U) {
+    int v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = top - lane - kWave * u;
+      const int w = row[max(idx, lo) - base];  // unconditional: the U loads issue back to back
+      v[u] = idx >= lo ? w : a + 1;
+    }
+    // Every ballot of the iteration (no early exit: an exit per vector lets
+    // the compiler sink each load behind the previous compare).
+    int r = lo - 1;
+#pragma unroll
+    for (int u = U - 1; u >= 0; --u) {
+      const unsigned long long m = __ballot(v[u] == a);
+      r = m ? top - kWave * u - first_lane(m) : r;
+    }
+    if (r >= lo) return r;
+  }
+  return lo - 1;
+}
+
+// Wave per segment (one 64-thread workgroup each). Lane k loads reply k of a
+// 64-reply batch, so a segment's replies arrive in one round trip; the fold
+// (a2, :66-88) then runs over them in array order on wave-uniform values.
+// a1 (:89-105) is evaluated after each successful reply exactly as :78 calls
+// it, but its log reads are deferred to the end of the batch: the fold never
+// reads commitIndex, and while the replica stays leader its term is the
+// segment's initial term, so every evaluation is "the highest index in
+// (H, top] whose term is currentTerm", with H the largest top evaluated so
+// far (an evaluation that scanned (commit, top] leaves no entry of that term
+// above the new commit up to top). The ranges of one batch are disjoint and
+// ascending: their top words are probed in parallel (one round trip; on a
+// log whose last entries carry the current term, every range ends there) and
+// only ranges whose top word differs are scanned, wave-cooperatively.
 template <int P>
-__global__ __launch_bounds__(256) void k_fold(Dev s, const mraft_ae_result *__restrict__ items, int64_t n,
-                                              const int64_t *__restrict__ seg_begin, int64_t n_seg,
-                                              const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
-                                              int32_t *__restrict__ item_err) {
-  const int64_t sg = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  if (sg >= n_seg) return;
-  const bool l0 = lane_id() == 0;
+__device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result *__restrict__ items,
+                                             const int64_t *__restrict__ seg_begin, int64_t sg,
+                                             const int32_t *__restrict__ seg_err,
+                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
+  const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   if (b >= e) return;
-  const int L = s.L;
-  const int slot = items[b].slot;
-  int bad = seg_err[sg];
-  if (!bad) {
-    for (int64_t i = b; i < e; ++i) {
-      const mraft_ae_result it = items[i];
-      if (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == slot % P)
-        bad = MRAFT_ITEM_BAD_SLOT;
-    }
-  }
-  if (!bad && s.commit[slot] < s.dummy[slot]) bad = MRAFT_ITEM_BAD_STATE;
-  if (bad) {
-    if (l0)
-      for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }
-    return;
-  }
+  const int64_t cnt = e - b;
+  FOLD_STAMP(0, (int)sg);
+  mraft_ae_result it{};
+  if (lane < cnt) it = items[b + lane];
+  const int slot = __builtin_amdgcn_readfirstlane(it.slot);
+  FOLD_STAMP(1, slot);
   const int me = slot % P;
   const int64_t mrow = (int64_t)slot * P;
+  // The replica's state in one round trip: one load per lane, lanes 0..P-1
+  // matchIndex, 8..8+P-1 nextIndex, 16..20 the scalars.
+  const int32_t *src = nullptr;
+  int64_t si = slot;
+  if (lane < P) { src = s.match; si = mrow + lane; }
+  else if (lane >= 8 && lane < 8 + P) { src = s.next; si = mrow + lane - 8; }
+  else if (lane == 16) src = s.term;
+  else if (lane == 17) src = s.role;
+  else if (lane == 18) src = s.commit;
+  else if (lane == 19) src = s.last;
+  else if (lane == 20) src = s.dummy;
+  const int vs = src ? src[si] : 0;
+  int term = __builtin_amdgcn_readlane(vs, 16), role = __builtin_amdgcn_readlane(vs, 17),
+      commit = __builtin_amdgcn_readlane(vs, 18);
+  const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20);
+  int bad = uni(seg_err[sg]);
+  FOLD_STAMP(2, term + role + commit + last + dummy);
+  for (int64_t base = 0; base < cnt; base += 64) {
+    const int64_t i = base + lane;
+    int sl = it.slot, pr = it.peer;
+    if (base > 0 && i < cnt) { sl = items[b + i].slot; pr = items[b + i].peer; }
+    if (__ballot(i < cnt && (sl != slot || pr < 0 || pr >= P || pr == me))) bad = MRAFT_ITEM_BAD_SLOT;
+  }
+  if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
+  if (bad) {
+    for (int64_t i = lane; i < cnt; i += 64) { item_err[b + i] = bad; flags[b + i] = 0; }
+    return;
+  }
   int m[8], nx[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    m[j] = j < P ? s.match[mrow + j] : 0;
-    nx[j] = j < P ? s.next[mrow + j] : 0;
+    m[j] = j < P ? __builtin_amdgcn_readlane(vs, j) : 0;
+    nx[j] = j < P ? __builtin_amdgcn_readlane(vs, 8 + j) : 0;
   }
-  int term = s.term[slot], role = s.role[slot], commit = s.commit[slot];
-  const int last = s.last[slot], dummy = s.dummy[slot];
   const int c0 = commit, t0 = term, r0 = role;
-  const int32_t *lrow = s.log + (int64_t)slot * L;
+  const int32_t *lrow = s.log + (int64_t)slot * s.L;
   bool touched_mn = false;
-  int H = commit;  // every index in (commit, H] is known not to hold the current term
-  for (int64_t i = b; i < e; ++i) {
-    const mraft_ae_result it = items[i];
-    int fl = 0;
-    const int pr = it.peer;
-    int nxp = 0;
+  int H = commit;
+  for (int64_t base = 0; base < cnt; base += 64) {
+    if (base > 0 && base + lane < cnt) it = items[b + base + lane];
+    const int nb = (int)min((int64_t)64, cnt - base);
+    int myfl = 0, plo = 1, phi = 0;  // this lane's reply: flags and a1 range
+    for (int k = 0; k < nb; ++k) {
+      const int pr = __builtin_amdgcn_readlane(it.peer, k);
+      const int rt = __builtin_amdgcn_readlane(it.reply_term, k);
+      const int at = __builtin_amdgcn_readlane(it.args_term, k);
+      const int ap = __builtin_amdgcn_readlane(it.args_prev_log_index, k);
+      int fl = 0, nxp = 0;
 #pragma unroll
-    for (int j = 0; j < P; ++j) if (j == pr) nxp = nx[j];
-    if (it.reply_term > term) {                                        // :67-72
-      term = it.reply_term; role = kFollower;
-      fl |= MRAFT_F_STEPPED_DOWN;
-    } else if (it.reply_term == term && role == kLeader && it.args_term == term &&
-               it.args_prev_log_index == nxp - 1) {                    // :73-74
-      fl |= MRAFT_F_APPLIED;
-      touched_mn = true;
-      if (it.reply_success) {
-        const int mv = it.args_n_entries + it.args_prev_log_index;     // :76
-        nxp = mv + 1;                                                  // :77
+      for (int j = 0; j < P; ++j) if (j == pr) nxp = nx[j];
+      if (rt > term) {                                                   // :67-72
+        term = rt; role = kFollower;
+        fl |= MRAFT_F_STEPPED_DOWN;
+      } else if (rt == term && role == kLeader && at == term && ap == nxp - 1) {  // :73-74
+        fl |= MRAFT_F_APPLIED;
+        touched_mn = true;
+        if (__builtin_amdgcn_readlane(it.reply_success, k)) {
+          const int mv = __builtin_amdgcn_readlane(it.args_n_entries, k) + ap;  // :76
+          nxp = mv + 1;                                                  // :77
 #pragma unroll
-        for (int j = 0; j < P; ++j) if (j == pr) m[j] = mv;
-        // a1 (:89-105): the count holds exactly for i <= M (quorum order
-        // statistic), so the gate is the highest index in (commit, min(M, last)]
-        // whose term is currentTerm.
-        const int top = min(quorum_rt<P>(m, me), last);
-        if (top > H) {
-          const int x = wave_scan_down_eq(lrow, dummy, H + 1, top, term);  // H if none
-          if (x > H) { commit = x; fl |= MRAFT_F_COMMITTED; }
-          H = top;
+          for (int j = 0; j < P; ++j) if (j == pr) m[j] = mv;
+          const int top = min(quorum_rt<P>(m, me), last);                // a1, :78
+          if (top > H) {
+            if (lane == k) { plo = H + 1; phi = top; }
+            H = top;
+          }
+        } else {
+          nxp = __builtin_amdgcn_readlane(it.reply_conflict_index, k);   // :82
         }
-      } else {
-        nxp = it.reply_conflict_index;                                 // :82
+#pragma unroll
+        for (int j = 0; j < P; ++j) if (j == pr) nx[j] = nxp;
+        if (nxp < last + 1) fl |= MRAFT_F_NEED_MORE;                     // :84-86
       }
-#pragma unroll
-      for (int j = 0; j < P; ++j) if (j == pr) nx[j] = nxp;
-      if (nxp < last + 1) fl |= MRAFT_F_NEED_MORE;                     // :84-86
+      if (lane == k) myfl = fl;
     }
-    if (l0) {
-      flags[i] = fl;
-      item_err[i] = 0;
+    // The batch's a1 ranges: probe every top word at once, scan the rest.
+    FOLD_STAMP(3, myfl + H);
+    int x = -1;
+    if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
+    if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
+    if (plo <= phi && lrow[phi - dummy] == t0) x = phi;                  // :98
+    unsigned long long pend = __ballot(plo < phi && x < 0);
+    while (pend) {
+      const int src = first_lane(pend);
+      pend &= pend - 1;
+      const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
+      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU>(lrow, dummy, lo, hi, t0);  // lo - 1 if none
+      if (lane == src && r >= lo) x = r;
+    }
+    FOLD_STAMP(4, x);
+    if (x >= 0) myfl |= MRAFT_F_COMMITTED;                               // :99-100
+    const unsigned long long fm = __ballot(x >= 0);
+    if (fm) commit = __shfl(x, 63 - __builtin_clzll(fm), 64);           // the latest range that found one
+    if (lane < nb) {
+      flags[b + base + lane] = myfl;
+      item_err[b + base + lane] = 0;
     }
   }
-  if (!l0) return;
   if (term != t0 || role != r0) {
-    s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
-    mark_persist(s, slot, MRAFT_PERSIST_STATE);                        // :72
+    if (lane == 0) {
+      s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
+      mark_persist(s, slot, MRAFT_PERSIST_STATE);                        // :72
+    }
   }
-  if (commit != c0) s.commit[slot] = commit;
+  if (commit != c0 && lane == 0) s.commit[slot] = commit;
   if (touched_mn) {
+    int om = 0, on = 0;
 #pragma unroll
-    for (int j = 0; j < P; ++j) { s.match[mrow + j] = m[j]; s.next[mrow + j] = nx[j]; }
+    for (int j = 0; j < P; ++j) if (lane == j) { om = m[j]; on = nx[j]; }
+    if (lane < P) { s.match[mrow + lane] = om; s.next[mrow + lane] = on; }
   }
+  FOLD_STAMP(5, commit);
+}
+
+template <int P>
+__global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft_ae_result *__restrict__ items,
+                                             const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                                             const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
+                                             int32_t *__restrict__ item_err) {
+  if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
+    const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
+    const int64_t sg = x * per + min(x, rem) + (b >> 3);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, flags, item_err);
+    return;
+  }
+  for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
+    fold_segment<P>(s, items, seg_begin, sg, seg_err, flags, item_err);
 }
 
 // ---------------------------------------------------------------- Start
@@ -776,20 +908,28 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
                       int64_t n_ent, mraft_ae_reply *rep, int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, args, n, ent,
-                     n_ent, rep, err);
+  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n * 64, 64 * MRAFT_AE_WPB)), dim3(64 * MRAFT_AE_WPB), 0, st,
+                     s, args, n, ent, n_ent, rep, err);
 }
+
+#if MRAFT_FOLD_TRACE
+extern "C" int mraft_debug_fold_trace(void *dst, long long nbytes) {
+  if (nbytes > (long long)sizeof(g_fold_trace)) nbytes = sizeof(g_fold_trace);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fold_trace), (size_t)nbytes, 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -3;
+}
+#endif
 
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
                  hipStream_t st) {
   (void)n;
   if (n_seg <= 0) return;
-  const dim3 gr(blocks_for(n_seg * 64)), bl(kBlock);
+  const dim3 gr((unsigned)min(n_seg, (int64_t)MRAFT_FOLD_GRID)), bl(64);
   switch (s.P) {
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
-    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, flags, \
+    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, seg_begin, n_seg, seg_err, flags,  \
                        item_err);                                                             \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)

@@ -327,15 +327,39 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   {
     unsigned long long m = __ballot(icls == IC_SCAN);
     if (MRAFT_TICK_EXP >= 2) m = 0;
-    while (m) {
-      const int src = first_lane(m);
-      m &= m - 1;
-      const long long sf = (long long)g * P + (src < lp ? src : src + 1);
-      const int sd = __shfl(fdummy, src, 64), sp = __shfl(prev, src, 64), sa = __shfl(ft, src, 64);
-      const int ci = wave_conflict_scan(s.log + sf * L, sd, sp, sa);
-      if (lane == src) {
-        rci = ci;
-        if (COUNT) scan_extra = sp - (ci > sd + 1 ? ci : sd + 2);
+    // ConflictIndex scans (:136-142): the first 64 terms below prev of every
+    // scanning follower in one round trip (most runs end there), then each
+    // longer run on its own, 256 terms per round trip.
+    int pv[NI];
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      pv[q] = 0;
+      if ((m >> q) & 1) {
+        const long long sf = (long long)g * P + (q < lp ? q : q + 1);
+        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64));
+        pv[q] = s.log[sf * L + (max(sp - 1 - lane, sd + 2) - sd)];  // prev >= dummy + 2: readable
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if ((m >> q) & 1) {
+        const long long sf = (long long)g * P + (q < lp ? q : q + 1);
+        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(ft, q, 64));
+        const int lo = sd + 2, hi = sp - 1;
+        const unsigned long long mm = __ballot(hi - lane >= lo && pv[q] != sa);
+        int ci;
+        if (mm) {
+          ci = hi - first_lane(mm);
+        } else if (hi - 64 < lo) {
+          ci = sd + 1;
+        } else {
+          const int r = wave_scan_down_ne(s.log + sf * L, sd, lo, hi - 64, sa);
+          ci = r < lo ? sd + 1 : r;
+        }
+        if (lane == q) {
+          rci = ci;
+          if (COUNT) scan_extra = sp - (ci > sd + 1 ? ci : sd + 2);
+        }
       }
     }
   }

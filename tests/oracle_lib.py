@@ -299,3 +299,46 @@ class GoShaped:
 
     def __del__(self):
         self.close()
+
+
+def random_reply_segments(st: dict, G: int, P: int, lp: np.ndarray, seed: int, max_len: int = 150):
+    """Reply batches for process_append_replies beyond what a3 produces: per
+    leader slot a segment of 0..max_len replies in arrival order (repeats of a
+    peer, stale and higher terms, failures, successes whose matchIndex moves
+    up and down), so a1 runs many times per segment, over logs whose tail may
+    not carry the current term (the Figure-8 scan). Returns items, seg_begin."""
+    rng = np.random.default_rng(seed)
+    L = st["log_term"].size // (G * P)
+    out = []
+    seg = [0]
+    for g in range(G):
+        if lp[g] < 0 or P < 2:
+            continue
+        s = g * P + int(lp[g])
+        k = int(rng.integers(0, max_len + 1)) if rng.random() < 0.9 else 0
+        T, last = int(st["current_term"][s]), int(st["last_index"][s])
+        nxt = st["next_index"][s * P:(s + 1) * P].astype(np.int64).copy()
+        for _ in range(k):
+            p = int(rng.integers(0, P - 1))
+            p = p if p < s % P else p + 1
+            r = np.zeros(1, dtype=AE_RESULT)[0]
+            r["slot"], r["peer"] = s, p
+            u = rng.random()
+            r["args_term"] = T if u < 0.9 else T - 1
+            prev = int(nxt[p]) - 1 if rng.random() < 0.8 else int(rng.integers(0, last + 1))
+            r["args_prev_log_index"] = prev
+            n = int(rng.integers(0, max(1, last - prev + 1))) if prev <= last else 0
+            r["args_n_entries"] = n
+            v = rng.random()
+            r["reply_term"] = T if v < 0.995 else (T + 1 if v < 0.997 else T - 1)
+            ok = rng.random() < 0.7
+            r["reply_success"] = int(ok)
+            r["reply_conflict_index"] = int(rng.integers(1, max(2, prev + 2)))
+            if ok and prev == nxt[p] - 1:
+                nxt[p] = prev + n + 1
+            elif prev == nxt[p] - 1:
+                nxt[p] = r["reply_conflict_index"]
+            out.append(r)
+        seg.append(len(out))
+    items = np.array(out, dtype=AE_RESULT) if out else np.zeros(0, dtype=AE_RESULT)
+    return items, np.array(seg, dtype=np.int64)

@@ -78,6 +78,22 @@ def test_fold_batch_config2():
         assert_states_equal(e.store_state(), o.state(), G, P, L, "fold")
 
 
+@pytest.mark.parametrize("P,seed", [(5, 24), (3, 25), (8, 26), (2, 27)])
+def test_fold_long_segments_gpu(P, seed):
+    """Segments longer than one 64-reply batch, repeated peers, many a1
+    evaluations per segment (ranges probed in parallel, Figure-8 scans)."""
+    from oracle_lib import random_reply_segments
+    G, L = 64, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=seed)
+    items, seg = random_reply_segments(st, G, P, lp, seed=seed)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        f, err = e.process_append_replies(items, seg)
+        of, oerr = o.process_append_replies(items, seg)
+        assert np.array_equal(err, oerr) and np.array_equal(f, of)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "fold long")
+
+
 def test_item_path_gpu():
     G, P, L = 256, 5, 256
     st, lp, _ = synth_tick_state(G, P, L, seed=61)

@@ -115,6 +115,34 @@ def test_fold_batch_c_vs_py():
     assert_states_equal(o.state(), po.to_soa(rafts, st, G, P, L), G, P, L, "fold")
 
 
+def test_fold_long_segments_c_vs_py():
+    """Segments of up to 150 replies in arrival order (repeated peers, stale
+    and higher terms, a1 evaluated many times per segment): C oracle ==
+    Python restatement, flags and state."""
+    from oracle_lib import random_reply_segments
+    G, P, L = 48, 5, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=23)
+    items, seg = random_reply_segments(st, G, P, lp, seed=24)
+    assert (np.diff(seg) > 64).any()
+    o = Oracle(G, P, L, st)
+    flags, err = o.process_append_replies(items, seg)
+    assert not err.any()
+    rafts = po.from_soa(st, G, P, L)
+    pflags = []
+    for it in items:
+        rf = rafts[it["slot"]]
+        args = po.AppendEntriesArgs(Term=int(it["args_term"]), LeaderId=rf.me,
+                                    Entries=[None] * int(it["args_n_entries"]),
+                                    PrevLogIndex=int(it["args_prev_log_index"]), PrevLogTerm=0,
+                                    LeaderCommit=0)
+        rep = po.AppendEntriesReply(Term=int(it["reply_term"]), Success=bool(it["reply_success"]),
+                                    ConflictIndex=int(it["reply_conflict_index"]))
+        pflags.append(rf.processAppendEntriesReply(int(it["peer"]), args, rep))
+    assert flags.tolist() == pflags
+    assert ((flags & 2) != 0).sum() > 10  # COMMITTED on many replies
+    assert_states_equal(o.state(), po.to_soa(rafts, st, G, P, L), G, P, L, "fold long")
+
+
 def test_item_path_equals_tick():
     """gather (a3) -> handle (a4) -> process (a2+a1) through the item-level
     oracle entry points equals the fused tick."""
