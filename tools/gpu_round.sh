@@ -14,4 +14,6 @@ echo "== microbench" && { timeout -k 5 120 ./tools/mb_segcopy > gpurun_out/mb_se
 echo "== election storm (config #5)" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/el -o el -- python3 bench_election.py --no-cpu-baseline > gpurun_out/prof/el_bench.json 2> gpurun_out/prof/el_bench.err &&
 cp "$(find gpurun_out/prof/el -name 'el_kernel_stats.csv' | head -1)" gpurun_out/${TAG}_election_kernel_stats.csv &&
-timeout -k 10 300 python bench_election.py > gpurun_out/${TAG}_election_bench.json 2> gpurun_out/election_bench.err && cat gpurun_out/${TAG}_election_bench.json
+timeout -k 10 300 python bench_election.py > gpurun_out/${TAG}_election_bench.json 2> gpurun_out/election_bench.err && cat gpurun_out/${TAG}_election_bench.json &&
+echo "== message path" &&
+timeout -k 10 300 python tools/bench_items.py > gpurun_out/${TAG}_message_path.json 2> gpurun_out/items.err && cat gpurun_out/${TAG}_message_path.json
