@@ -344,7 +344,9 @@ def main():
                 "HBM-resident copy per step",
         "config": {"workload": f"config #{args.config} fused replication tick (a3+a4+a2+a1) with the GetState "
                                "export fused in"
-                               + (" + RCCL all-gather of commit/term words" if world > 1 else "")
+                               + ((" + RCCL all-gather of commit/term words" if not on_host else
+                                   f" + {args.dist_backend} all-gather of commit/term words (rehearsal)")
+                                  if world > 1 else "")
                                + (" [cache-resident working set: not an HBM measurement]"
                                   if args.config == 2 else ""),
                    "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
