@@ -140,6 +140,19 @@ def permute_groups(st, lp, G, P, L, how):
     work = np.clip(last[:, None] + 1 - nxt, 0, None).sum(axis=1)
     if how == "random":
         perm = np.random.default_rng(0).permutation(G)
+    elif how.startswith("taillight"):
+        # natural order, except that each XCD range ends with its lightest
+        # groups (the last `frac` of its dispatch order): a lighter tail
+        frac = float(how[len("taillight"):] or 0.12)
+        per = G // 8
+        parts = []
+        for x in range(8):
+            idx = np.arange(x * per, (x + 1) * per)
+            k = int(per * frac)
+            light = idx[np.argsort(work[idx], kind="stable")[:k]]
+            rest = np.setdiff1d(idx, light, assume_unique=True)
+            parts.append(np.concatenate([rest, light[::-1]]))
+        perm = np.concatenate(parts + [np.arange(8 * per, G)])
     else:
         per = G // 8
         perm = np.concatenate([x * per + np.argsort(-work[x * per:(x + 1) * per], kind="stable")
@@ -171,8 +184,9 @@ def main():
     ap.add_argument("--log-pad", type=int, default=0,
                     help="experiment: pad every log row by this many entries (capacity L + pad, "
                          "same logs and algorithmic words; only the row stride changes)")
-    ap.add_argument("--group-order", default="natural", choices=["natural", "lpt-xcd", "random"],
-                    help="experiment: permute the groups (same work, different dispatch order)")
+    ap.add_argument("--group-order", default="natural",
+                    help="experiment: permute the groups (same work, different dispatch order): "
+                         "natural, lpt-xcd, random, taillight[FRAC]")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (CPU rehearsal)")
     args = ap.parse_args()
