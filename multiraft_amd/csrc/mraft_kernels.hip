@@ -125,12 +125,18 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
   if (i >= n) return;
   const int lane = lane_id();
   mraft_ae_reply r = {0, 0, 0, 0};
-  int e = err[i];
+  // Three round trips before the merge: the item (error word and args
+  // together), the follower's scalars (one load per lane), log[prev].
+  const int e = err[i];
+  const mraft_ae_args a = args[i];
+  // Both loads in flight before the branch (else the compiler sinks the args
+  // load behind the error check: one more round trip).
+  asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
+               "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset));
   if (e) {
     if (lane == 0) rep[i] = r;
     return;
   }
-  const mraft_ae_args a = args[i];
   const int L = s.L;
   if (a.n_entries < 0 || a.entries_offset < 0 ||
       (a.n_entries > 0 && a.entries_offset + a.n_entries > n_ent)) {
@@ -138,26 +144,28 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
     return;
   }
   const int f = a.slot, prev = a.prev_log_index, nn = a.n_entries;
-  const int fterm = s.term[f];
+  const int32_t *sa = lane == 0 ? s.term : lane == 1 ? s.dummy : lane == 2 ? s.last : s.commit;
+  const int sv = lane < 4 ? sa[f] : 0;
+  const int fterm = __builtin_amdgcn_readlane(sv, 0), fdummy = __builtin_amdgcn_readlane(sv, 1),
+            flast = __builtin_amdgcn_readlane(sv, 2), fc = __builtin_amdgcn_readlane(sv, 3);
   if (a.term < fterm) {                                                // :112-115
     r.term = fterm;
     if (lane == 0) { rep[i] = r; mark_persist(s, f, MRAFT_PERSIST_STATE); }  // deferred :111
     return;
   }
   const bool adopt = a.term > fterm;                                   // :116-118
-  const int fdummy = s.dummy[f];
   const int32_t *frow = s.log + (int64_t)f * L;
   bool write_state = true;
   int newlast = -1, fcommit_new = -1;
   if (prev < fdummy) {                                                 // :123-127
     r.term = 0; r.conflict_index = fdummy + 1;
   } else {
-    const int flast = s.last[f];
-    if (prev > flast || frow[prev - fdummy] != a.prev_log_term) {      // matchLog, raft_log.go:92-96
+    const int ftp = prev > flast ? 0 : frow[prev - fdummy];
+    if (prev > flast || ftp != a.prev_log_term) {                      // matchLog, raft_log.go:92-96
       r.term = a.term;
       if (prev > flast) r.conflict_index = flast + 1;                  // :131-133
       else if (prev > fdummy + 1)
-        r.conflict_index = wave_conflict_scan(frow, fdummy, prev, frow[prev - fdummy]);  // :136-142
+        r.conflict_index = wave_conflict_scan(frow, fdummy, prev, ftp);  // :136-142
       else r.conflict_index = prev;
     } else {
       // :146-155 through the streaming pass the tick uses (mraft_pass.h):
@@ -196,7 +204,6 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
         last_after = newlast;
       }
       if (write_state) {
-        const int fc = s.commit[f];
         if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160
         r.term = a.term; r.success = 1;                                // :161
       }
