@@ -187,13 +187,25 @@ def main():
     ap.add_argument("--group-order", default="natural",
                     help="experiment: permute the groups (same work, different dispatch order): "
                          "natural, lpt-xcd, random, taillight[FRAC]")
+    ap.add_argument("--fanin-at-1", action="store_true",
+                    help="rehearsal: set up the process group and run the per-tick fan-in even with "
+                         "one rank (exercises the RCCL + overlap path on a single GPU)")
+    ap.add_argument("--fanin", default="overlap", choices=["overlap", "inline"],
+                    help="RCCL fan-in placement: overlap = on its own stream beside the next tick; "
+                         "inline = on the tick's stream")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (CPU rehearsal)")
     args = ap.parse_args()
+    # The result line is the only thing on stdout: libraries that print there
+    # (RCCL's version banner at communicator init) are sent to stderr.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    dist_on = world > 1 or args.fanin_at_1
     import torch
     import torch.distributed as dist
 
@@ -201,14 +213,18 @@ def main():
     local_dev = local % max(ndev, 1)  # gloo rehearsals may share one GPU
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    if dist_on:
+        if world == 1:  # --fanin-at-1 without a launcher
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29561"), ("RANK", "0"),
+                         ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
 
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
-    from multiraft_amd.router import allgather_status
+    from multiraft_amd.router import allgather_status_packed
 
     if args.config == 2:
         args.groups, args.peers, args.log = 1024, 3, 256
@@ -239,7 +255,7 @@ def main():
             pool = max(1, min(K + 1, int(free * 0.9 // clone_bytes)))
             clones = [{k: v.clone() for k, v in master.items()} for _ in range(pool)]
             torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             dist.barrier()
     del st
     restore = pool < K + 1
@@ -254,9 +270,21 @@ def main():
     eng.set_stream(stream.cuda_stream)
     lp_d = torch.from_numpy(lp).to(dev)
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    commit_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    tl_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    on_host = world > 1 and args.dist_backend != "nccl"
+    on_host = dist_on and args.dist_backend != "nccl"
+    # Per-step GetState export blocks (commitIndex | term<<1|leader, one buffer
+    # so the router's fan-in is ONE collective per tick) and their gathers:
+    # never reused within a run, so a step's all-gather can overlap the next
+    # step's tick on its own stream with no buffer hazard.
+    nbuf = W + K
+    status = torch.zeros((nbuf, 2 * G), dtype=torch.int32, device=dev)
+    comm = None
+    if dist_on and not on_host:
+        # (a high-priority stream measured no better: the all-gather still waits
+        # for CU slots behind the next tick)
+        comm = stream if args.fanin == "inline" else torch.cuda.Stream(dev)
+    gathered = (torch.empty((nbuf, world * 2 * G), dtype=torch.int32, device=dev)
+                if comm is not None else None)
+    tick_done = [torch.cuda.Event() for _ in range(nbuf)] if comm is not None else []
 
     # Algorithmic words of one tick on the pristine state.
     eng.bind(master)
@@ -266,11 +294,11 @@ def main():
     # Per-launch kernel timing on the engine's stream. With nothing else on the
     # stream between ticks (one rank, no restores) one marker between
     # consecutive ticks serves as the end of one and the start of the next.
-    chain = world == 1 and not restore
+    chain = not dist_on and not restore
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
 
     # The all-gather, timed on its own (reported beside the step).
-    ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if world > 1 else []
+    ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if dist_on else []
     ag_ms = []
 
     def mark_start(i):
@@ -290,40 +318,47 @@ def main():
         if timed and (i == 0 or not chain):
             mark_start(i).record(stream)
         # the tick with the GetState export fused in (one launch per step)
-        eng.replicate_tick_export(lp_d, gf_d, commit_d, tl_d, where=DEVICE)
+        j = i if timed else K + i  # timed steps use blocks 0..K-1, warmup K..K+W-1
+        eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
         if timed:
             mark_end(i).record(stream)
-        if world > 1:  # the shard router's fan-in
+        if dist_on:  # the shard router's fan-in
             if on_host:
                 t1 = time.perf_counter()
-                allgather_status(commit_d.cpu(), tl_d.cpu())
+                allgather_status_packed(status[j].cpu())
                 if timed:
                     ag_ms.append((time.perf_counter() - t1) * 1e3)
             else:
-                if timed:
-                    ag_marks[2 * i].record(stream)
-                allgather_status(commit_d, tl_d)
-                if timed:
-                    ag_marks[2 * i + 1].record(stream)
+                # RCCL all-gather of this tick's words on the comm stream, after
+                # the tick and overlapped with the next tick (which writes
+                # another block): the next batch never waits for the fan-in.
+                tick_done[j].record(stream)
+                comm.wait_event(tick_done[j])
+                with torch.cuda.stream(comm):
+                    if timed:
+                        ag_marks[2 * i].record(comm)
+                    allgather_status_packed(status[j], out=gathered[j])
+                    if timed:
+                        ag_marks[2 * i + 1].record(comm)
 
     for i in range(W):
         step(i, False)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(K):
         step(i, True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
     ker_ms = [mark_start(i).elapsed_time(mark_end(i)) for i in range(K)]
     log(rank, "tick kernel ms per step: " + " ".join(f"{x:.3f}" for x in ker_ms))
     flags = gf_d.cpu().numpy()
-    if world > 1 and not on_host:
+    if dist_on and not on_host:
         ag_ms = [ag_marks[2 * i].elapsed_time(ag_marks[2 * i + 1]) for i in range(K)]
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if on_host else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -360,14 +395,15 @@ def main():
                                "export fused in"
                                + ((" + RCCL all-gather of commit/term words" if not on_host else
                                    f" + {args.dist_backend} all-gather of commit/term words (rehearsal)")
-                                  if world > 1 else "")
+                                  if dist_on else "")
                                + (" [cache-resident working set: not an HBM measurement]"
                                   if args.config == 2 else ""),
                    "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
                    "committed_groups_last_step": int(((flags & 2) != 0).sum()),
                    "active_groups": active, "restore_in_timed_step": restore,
                    "allgather_ms_mean": float(np.mean(ag_ms)) if ag_ms else None,
-                   "allgather_bytes_per_rank": 8 * G if world > 1 else 0},
+                   "allgather_bytes_per_rank": 8 * G if dist_on else 0,
+                   "allgather_placement": args.fanin if comm is not None else None},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
@@ -380,12 +416,12 @@ def main():
                      "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dist_on and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, args.cpu_seconds, rank)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     eng.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

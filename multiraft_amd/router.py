@@ -98,6 +98,27 @@ def allgather_status(commit_local, term_leader_local):
     return all_c, all_t
 
 
+def allgather_status_packed(status_local, out=None):
+    """One collective for both words: `status_local` is this rank's [2 * n]
+    block (commitIndex[0:n] then term<<1|leader[n:2n], the layout the fused
+    tick exports into when handed two halves of one buffer); returns the
+    [world * 2 * n] gather, rank-major. unpack_status() splits it."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    if out is None:
+        out = torch.empty(world * status_local.numel(), dtype=status_local.dtype,
+                          device=status_local.device)
+    dist.all_gather_into_tensor(out, status_local.contiguous())
+    return out
+
+
+def unpack_status(packed, world: int):
+    """(commit[world * n], term_leader[world * n]) from a packed gather."""
+    v = packed.reshape(world, 2, -1)
+    return v[:, 0, :].reshape(-1), v[:, 1, :].reshape(-1)
+
+
 class GroupStatusView:
     """Global view of every group's (commitIndex, term, isLeader) words."""
 

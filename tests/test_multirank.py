@@ -29,7 +29,8 @@ def _worker(rank, world, port, G, P, L, out_q):
     from oracle_lib import Oracle
 
     from multiraft_amd import synth_tick_state
-    from multiraft_amd.router import GroupStatusView, allgather_status
+    from multiraft_amd.router import (GroupStatusView, allgather_status, allgather_status_packed,
+                                      unpack_status)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,6 +39,9 @@ def _worker(rank, world, port, G, P, L, out_q):
     o.replicate_tick(lp)
     c, tl = o.export_group_status(lp)
     all_c, all_t = allgather_status(torch.from_numpy(c), torch.from_numpy(tl))
+    # the bench's single packed collective gives the same words
+    pk_c, pk_t = unpack_status(allgather_status_packed(torch.from_numpy(np.concatenate([c, tl]))), world)
+    assert torch.equal(pk_c, all_c) and torch.equal(pk_t, all_t)
     view = GroupStatusView(all_c.numpy(), all_t.numpy())
     shard_to_group = np.arange(10) * (G * world // 10)
     routed = view.route("k", shard_to_group)
