@@ -44,6 +44,14 @@ def main():
         print(f"{name:15s} mean {x.mean():7.2f}  p10 {q[0]:6.2f} p50 {q[1]:6.2f} p90 {q[2]:6.2f} "
               f"p99 {q[3]:7.2f} max {q[4]:7.2f} us")
     print(f"sum over groups: header {hdr.sum()/1e3:.1f} ms, pass {pas.sum()/1e3:.1f} ms, C+D {tail.sum()/1e3:.1f} ms")
+    # The ramp-down: who finishes last, when they started, how long they lived.
+    end = us[:, 3]
+    for frac in (0.001, 0.01, 0.05):
+        k = max(1, int(G * frac))
+        idx = np.argsort(end)[-k:]
+        print(f"last {frac*100:.1f}% to finish ({k} groups): end >= {end[idx].min():.1f} us, start p10/p50/p90 "
+              f"{np.percentile(us[idx, 0], 10):.1f}/{np.percentile(us[idx, 0], 50):.1f}/{np.percentile(us[idx, 0], 90):.1f}, "
+              f"lifetime p50 {np.median(life[idx]):.1f} (all groups p50 {np.median(life):.1f}), pass p50 {np.median(pas[idx]):.1f}")
     grid = np.arange(0, span + 5, 5.0)
     print(" t(us)  in-header  in-pass  in-CD  done")
     for x in grid:
