@@ -316,6 +316,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
+  int bad = uni(seg_err[sg]);  // the claim verdict: a bad segment's slot may be out of range
   if (b >= e) return;
   const int64_t cnt = e - b;
   FOLD_STAMP(0, (int)sg);
@@ -336,11 +337,10 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   else if (lane == 18) src = s.commit;
   else if (lane == 19) src = s.last;
   else if (lane == 20) src = s.dummy;
-  const int vs = src ? src[si] : 0;
+  const int vs = (src && !bad) ? src[si] : 0;
   int term = __builtin_amdgcn_readlane(vs, 16), role = __builtin_amdgcn_readlane(vs, 17),
       commit = __builtin_amdgcn_readlane(vs, 18);
   const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20);
-  int bad = uni(seg_err[sg]);
   FOLD_STAMP(2, term + role + commit + last + dummy);
   for (int64_t base = 0; base < cnt; base += 64) {
     const int64_t i = base + lane;

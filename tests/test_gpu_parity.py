@@ -78,6 +78,25 @@ def test_fold_batch_config2():
         assert_states_equal(e.store_state(), o.state(), G, P, L, "fold")
 
 
+def test_fold_far_bad_slot_gpu():
+    """A segment whose slot lies far outside the image is rejected without
+    reading any replica state (the fold never dereferences it); the other
+    segments of the batch fold as on the oracle."""
+    G, P, L = 1024, 3, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(2))
+    items, seg = synth_fold_batch(st, G, P, L, lp, seed=synth_seed(2))
+    items = items.copy()
+    bad = slice(int(seg[7]), int(seg[8]))
+    items["slot"][bad] = 1 << 30
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        f, err = e.process_append_replies(items, seg)
+        of, oerr = o.process_append_replies(items, seg)
+        assert (err[bad] == 6).all() and (f[bad] == 0).all()  # MRAFT_ITEM_BAD_SLOT
+        assert np.array_equal(err, oerr) and np.array_equal(f, of)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "fold bad slot")
+
+
 @pytest.mark.parametrize("P,seed", [(5, 24), (3, 25), (8, 26), (2, 27)])
 def test_fold_long_segments_gpu(P, seed):
     """Segments longer than one 64-reply batch, repeated peers, many a1
