@@ -26,6 +26,10 @@ namespace {
 #define MRAFT_EL_GM_LDS 2  // grant-mask transpose: 2 ballots (else 1 LDS bytes, 0 __shfl)
 #endif
 
+// A broadcast term word: with the sparse voter loop the candidate bit is not
+// needed (the loop walks the candidate mask), so the word is the bare term.
+#define EL_T(x) (MRAFT_EL_SPARSE ? (x) : ((x) & 0x7fffffff))
+
 template <int P>
 __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *__restrict__ cand,
                                                          int R, int32_t *__restrict__ gflags) {
@@ -75,7 +79,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // One broadcast per replica per round, through this wave's LDS words: its
     // term with the candidate bit on top.
     int cx[8];
-    const int mycx = (int)((unsigned)at | ((unsigned)isc << 31));
+    const int mycx = MRAFT_EL_SPARSE ? at : (int)((unsigned)at | ((unsigned)isc << 31));
     if (MRAFT_EL_CX_LDS) {
       lds_cx[threadIdx.x] = mycx;
       __builtin_amdgcn_wave_barrier();
@@ -98,6 +102,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // k below the wave's largest candidate count (ascending peer order kept).
     const unsigned long long cb = __ballot(isc);
     int cm = (int)((cb >> seg) & 0xffull);
+    pd |= (int)(act && (cm & ~(1 << p)) != 0);                         // :57, every RV this voter handles
     int kmax = __builtin_popcount(cm);
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
@@ -108,10 +113,9 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       cm &= cm - 1;
       const int cxc = __shfl(mycx, c, 8);
       const bool cisc = any;
-      const int cat = cxc & 0x7fffffff;
+      const int cat = EL_T(cxc);
       pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
       const bool h = act && cisc && c != p;                            // this voter handles c's RV
-      pd |= (int)h;
       const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
       const bool gt = h && cat > term;                                 // :63-66
       term = gt ? cat : term;
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       const int om = ((1 << P) - 1) & ~(1 << p);
       int gt = 0, tv = 0;
 #pragma unroll
-      for (int v = 0; v < P; ++v) gt |= (int)((cx[v] & 0x7fffffff) > at) << v;
+      for (int v = 0; v < P; ++v) gt |= (int)(EL_T(cx[v]) > at) << v;
       // reply.Term = max(voter's own term, pmx) > at: every refusal when pmx > at.
       const int smask = om & ~mine & (pmx > at ? om : gt);
       int mm = mine & om;
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       const int lpos = mm ? __builtin_ctz(mm) : 32;
       const int spos = smask ? __builtin_ctz(smask) : 32;
 #pragma unroll
-      for (int v = 0; v < P; ++v) tv = spos == v ? (cx[v] & 0x7fffffff) : tv;
+      for (int v = 0; v < P; ++v) tv = spos == v ? EL_T(cx[v]) : tv;
       const bool lead = ok0 && lpos < spos;
       const bool sd = ok0 && spos < lpos;
       const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
