@@ -23,7 +23,7 @@ namespace {
 #define MRAFT_EL_TALLY_CF 1  // closed-form vote tally (else the per-reply fold)
 #endif
 #ifndef MRAFT_EL_GM_LDS
-#define MRAFT_EL_GM_LDS 2  // grant-mask transpose: 2 ballots (else 1 LDS bytes, 0 __shfl)
+#define MRAFT_EL_GM_LDS 1  // grant-mask transpose: 1 LDS bytes, 2 ballots, 0 __shfl
 #endif
 
 // A broadcast term word: with the sparse voter loop the candidate bit is not
@@ -103,11 +103,9 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     const unsigned long long cb = __ballot(isc);
     int cm = (int)((cb >> seg) & 0xffull);
     pd |= (int)(act && (cm & ~(1 << p)) != 0);                         // :57, every RV this voter handles
-    int kmax = __builtin_popcount(cm);
-#pragma unroll
-    for (int o = 8; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
-    kmax = __builtin_amdgcn_readfirstlane(kmax);
-    for (int k = 0; k < kmax; ++k) {
+    // until every segment of the wave has walked its candidates (the ballot is
+    // scalar: no cross-lane max of the counts)
+    while (__ballot(cm != 0)) {
       const bool any = cm != 0;
       const int c = any ? __builtin_ctz(cm) : 0;
       cm &= cm - 1;
@@ -146,7 +144,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // Grants transposed through LDS: byte v of the segment's word = voter v's
     // grant mask; bit v of mine = voter v granted this lane.
     int mine = 0;
-    if (MRAFT_EL_GM_LDS) {
+    if (MRAFT_EL_GM_LDS == 1) {
       lds_gm[threadIdx.x] = (uint8_t)gm;
       __builtin_amdgcn_wave_barrier();
       const unsigned long long gw = *reinterpret_cast<const unsigned long long *>(&lds_gm[threadIdx.x & ~7u]);
@@ -184,8 +182,12 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       for (int k = 1; k < (P / 2 > 1 ? P / 2 : 1); ++k) mm &= mm - 1;  // the (P/2)-th grant
       const int lpos = mm ? __builtin_ctz(mm) : 32;
       const int spos = smask ? __builtin_ctz(smask) : 32;
+      if (MRAFT_EL_CX_LDS) {
+        tv = EL_T(lds_cx[(threadIdx.x & ~7u) + min(spos, 7)]);  // used only when spos < P
+      } else {
 #pragma unroll
-      for (int v = 0; v < P; ++v) tv = spos == v ? EL_T(cx[v]) : tv;
+        for (int v = 0; v < P; ++v) tv = spos == v ? EL_T(cx[v]) : tv;
+      }
       const bool lead = ok0 && lpos < spos;
       const bool sd = ok0 && spos < lpos;
       const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
