@@ -391,8 +391,10 @@ def main():
         "dtype": "int32",
         "data": f"synthetic: seeded config-#{args.config} generator (include/mraft_synth.h), fresh "
                 "HBM-resident copy per step",
-        "config": {"workload": f"config #{args.config} fused replication tick (a3+a4+a2+a1) with the GetState "
-                               "export fused in"
+        "config": {"workload": (f"config #{args.config}" if not args.global_groups else
+                                f"{G_total:,} groups split over {world} rank(s) (config #4 when 262,144; "
+                                f"generator and mix of config #{args.config})")
+                               + " fused replication tick (a3+a4+a2+a1) with the GetState export fused in"
                                + ((" + RCCL all-gather of commit/term words" if not on_host else
                                    f" + {args.dist_backend} all-gather of commit/term words (rehearsal)")
                                   if dist_on else "")
