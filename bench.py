@@ -180,7 +180,9 @@ def main():
     ap.add_argument("--log", type=int, default=4096, help="log capacity L")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc-json", default="",
+                    help="PMC traffic summary (default: profiles/pmc_traffic.json for 65,536 groups "
+                         "per GPU, profiles/pmc_traffic_g<G>.json otherwise)")
     ap.add_argument("--log-pad", type=int, default=0,
                     help="experiment: pad every log row by this many entries (capacity L + pad, "
                          "same logs and algorithmic words; only the row stride changes)")
@@ -366,6 +368,9 @@ def main():
     ker_s = float(np.mean(ker_ms)) / 1e3
     achieved = algo_bytes / ker_s
     traffic, traffic_src = None, None
+    if not args.pmc_json:
+        args.pmc_json = os.path.join(ROOT, "profiles", "pmc_traffic.json" if G == 65536
+                                     else f"pmc_traffic_g{G}.json")
     if os.path.exists(args.pmc_json):
         # PMC traffic of this exact kernel source and config, from the
         # committed rocprofv3 summary (tools/profile_round.sh + pmc_summary.py).
@@ -374,7 +379,7 @@ def main():
             if ((pm.get("groups"), pm.get("peers"), pm.get("log")) == (G, P, L)
                     and pm.get("kernel_src_sha") == kernel_src_sha()):
                 traffic = pm.get("hbm_bytes_per_launch")
-                traffic_src = f"profiles/pmc_traffic.json ({pm.get('tag')})"
+                traffic_src = f"profiles/{os.path.basename(args.pmc_json)} ({pm.get('tag')})"
         except Exception:
             traffic = None
     out = {

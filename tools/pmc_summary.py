@@ -98,7 +98,10 @@ def main():
         "hbm_bytes_per_launch": fv * 1024 * fetch_factor + wv * 1024 * write_factor,
         "algorithmic_bytes_per_launch": bench.get("roofline", {}).get("algorithmic_bytes_per_launch"),
     }
-    json.dump(out, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+    # the headline config keeps the plain name; other group counts (config #4
+    # on one GPU) get their own file, which bench.py picks by group count
+    name = "pmc_traffic.json" if out["groups"] == 65536 else f"pmc_traffic_g{out['groups']}.json"
+    json.dump(out, open(os.path.join(dst, name), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 

@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p "$OUT"
-ARGS="--steps ${STEPS:-5} --warmup 1 --no-cpu-baseline"
+ARGS="--steps ${STEPS:-5} --warmup 1 --no-cpu-baseline ${BENCH_EXTRA:-}"
 make -s -C tools
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err"
