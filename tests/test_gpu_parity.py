@@ -314,6 +314,24 @@ def test_tick_full_config3_gpu():
             _assert_big_states_equal(e.store_state(), o.state(), G, P, L, f"full tick {k}")
 
 
+def test_tick_full_config4_one_gpu():
+    """BASELINE config #4 as its N=1 point (`bench.py --global-groups 262144`):
+    all 262,144 groups x 5 peers x 4,096-entry logs (21.5 GB of logs) on one
+    GPU, one tick bit-exact against the oracle (state, persist bits, group
+    flags, fused GetState words), and the roofline's word count."""
+    G, P, L = 262144, 5, 4096
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3), nthreads=16)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        del st
+        assert e.replicate_tick_count(lp) == o.replicate_tick_count(lp)
+        gf, c, tl = e.replicate_tick_export(lp)
+        assert np.array_equal(gf, o.replicate_tick(lp, nthreads=16)), "config #4 tick flags"
+        oc, otl = o.export_group_status(lp)
+        assert np.array_equal(c, oc) and np.array_equal(tl, otl)
+        _assert_big_states_equal(e.store_state(), o.state(), G, P, L, "config #4 tick")
+
+
 def test_election_storm_full_config5_gpu():
     """BASELINE config #5 at full size: 65,536 groups x 7 peers, 64 rounds."""
     from multiraft_amd import synth_election_state
