@@ -13,6 +13,10 @@ namespace {
 
 enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the pass
 
+#ifndef MRAFT_COPY_PIPE
+#define MRAFT_COPY_PIPE 1  // software-pipelined copy-only loop (0: the plain loop, for A/B runs)
+#endif
+
 #ifndef MRAFT_TICK_NT
 #define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
 #endif
@@ -210,6 +214,55 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
   int cmask = 0;
 #pragma unroll
   for (int q = 0; q < NI; ++q) cmask |= (mode[q] == M_COPY) ? (1 << q) : 0;
+#if MRAFT_COPY_PIPE
+  if constexpr (VEC && VC == 1) {
+    // Software-pipelined: chunk c+256 is loaded before chunk c is stored, so
+    // a wave never waits for its own stores before issuing the next load
+    // (vmcnt counts both in order). The next chunk is loaded only when the
+    // loop will run for it (same exit rule as below): no extra traffic.
+    if (c > phi || (!cmask && !(slo <= shi && c <= shi))) return;
+    int4 cur = make_int4(0, 0, 0, 0);
+    if (c + 4 * lane <= phi) cur = ld4(src + eo + c + 4 * lane);
+    for (;;) {
+      const int i0 = c + 4 * lane;
+      const int cmask_n = c + CW >= nend ? 0 : cmask;
+      const int cn = c + CW;
+      const bool more = cn <= phi && (cmask_n || (slo <= shi && cn <= shi));
+      int4 nxt = make_int4(0, 0, 0, 0);
+      if (more && cn + 4 * lane <= phi) nxt = ld4(src + eo + cn + 4 * lane);
+      if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+        const int e[4] = {cur.x, cur.y, cur.z, cur.w};
+        int lu = -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i0 + u >= slo && i0 + u <= shi && e[u] == T) lu = u;
+        const unsigned long long m = __ballot(lu >= 0);
+        if (m) {
+          const int l = 63 - __clzll((long long)m);
+          found = c + 4 * l + __shfl(lu, l, 64);
+        }
+      }
+      if (!COUNT) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          if (!((cmask >> q) & 1)) continue;
+          if (i0 + 3 < nend) {
+            st4(log + fo[q] + i0, cur.x, cur.y, cur.z, cur.w);
+          } else {
+            const int e[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (i0 + u < nend) st1(log + fo[q] + i0 + u, e[u]);
+          }
+        }
+      }
+      if (!more) return;
+      cmask = cmask_n;
+      c = cn;
+      cur = nxt;
+    }
+  }
+#endif
   for (; c <= phi; c += CW) {
     const bool scan = slo <= shi && c <= shi && c + CW - 1 >= slo;
     if (!cmask && !(slo <= shi && c <= shi)) break;
