@@ -13,8 +13,11 @@ decisions/s = groups x steps / time. Every timed step runs on its own pristine
 copy of the state (a tick mutates the state; re-running it on mutated state
 would be a different, lighter workload).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch with
-torch.distributed.run (one process per GPU). Prints one JSON line (rank 0).
+Usage: python bench.py [--gpus N --steps K --warmup W]. For N > 1 either launch
+with torch.distributed.run (one process per GPU) or let bench.py start the N
+rank processes itself; N > 1 defaults to BASELINE config #4 (262,144 groups
+split over the GPUs, strong scaling) with one RCCL all-gather of the GetState
+words per tick through the C ABI. Prints one JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -165,14 +168,68 @@ def permute_groups(st, lp, G, P, L, how):
     return out, np.ascontiguousarray(lp[perm])
 
 
+def describe_workload(strong, world, G_total, P, L, config, dist_on, rccl, backend):
+    if strong and world > 1:
+        w = ((f"config #4: " if G_total == 262144 else "")
+             + f"{G_total:,} groups x {P} peers x {L:,}-entry logs split over {world} "
+             f"GPUs (strong scaling; config #3's generator and mix)")
+    elif strong:
+        w = f"{G_total:,} groups x {P} x {L:,} on one GPU (config #4's total; config #3 mix)"
+    else:
+        w = f"config #{config}" + (f" x {world} ranks (weak scaling)" if world > 1 else "")
+    w += " fused replication tick (a3+a4+a2+a1) with the GetState export fused in"
+    if dist_on:
+        w += (" + RCCL all-gather of commit/term words (C ABI, mraft_allgather_status)"
+              if rccl else f" + {backend} all-gather of commit/term words (rehearsal)")
+    if config == 2:
+        w += " [cache-resident working set: not an HBM measurement]"
+    return w
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N rank processes (one per GPU) and
+    wait for them. The parent never touches the GPU (it only forwards the
+    arguments); rank 0's stdout is the result line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            c = p.poll()
+            if c is None:
+                continue
+            pending.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in pending:  # one rank failed: end the others (exact PIDs)
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a torch.distributed launcher bench.py starts "
+                         "them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
+    ap.add_argument("--groups", type=int, default=0,
+                    help="groups per GPU (weak scaling); default 65,536 (config #3) on one GPU")
     ap.add_argument("--global-groups", type=int, default=0,
-                    help="fixed total split over the ranks instead (strong scaling; config #4 = 262144)")
+                    help="fixed total split over the ranks (strong scaling); default 262,144 "
+                         "(config #4) with more than one rank")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3],
                     help="BASELINE config: 3 = 65,536 x 5 x 4,096 (headline); 2 = 1,024 x 3 x 256 "
                          "(cache-resident: not an HBM measurement)")
@@ -190,14 +247,25 @@ def main():
                     help="experiment: permute the groups (same work, different dispatch order): "
                          "natural, lpt-xcd, random, taillight[FRAC]")
     ap.add_argument("--fanin-at-1", action="store_true",
-                    help="rehearsal: set up the process group and run the per-tick fan-in even with "
-                         "one rank (exercises the RCCL + overlap path on a single GPU)")
+                    help="rehearsal: run the per-tick RCCL fan-in even with one rank (a one-rank "
+                         "communicator: exercises the C-ABI gather + overlap path on a single GPU)")
     ap.add_argument("--fanin", default="overlap", choices=["overlap", "inline"],
-                    help="RCCL fan-in placement: overlap = on its own stream beside the next tick; "
-                         "inline = on the tick's stream")
+                    help="RCCL fan-in placement: overlap = on the engine's fan-in stream beside the "
+                         "next tick; inline = on the tick's stream")
+    ap.add_argument("--fanin-cus", type=int, default=8,
+                    help="CUs reserved for the fan-in stream (mraft_fanin_reserve_cus; 0 = none): "
+                         "without them the overlapped gather queues for CU slots behind the next "
+                         "tick (0.31 ms vs 0.015 ms on one rank, profiles/r2_v1_fanin_cus*.json)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch plumbing only (no GPU call): start the ranks, build every rank's "
+                         "shard of the seeded workload, run the control plane and print the line "
+                         "with value null")
     ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (CPU rehearsal)")
+                    help="fan-in data path: nccl = the library's RCCL all-gather over xGMI (C ABI); "
+                         "gloo = host gather through torch.distributed (CPU rehearsal)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     # The result line is the only thing on stdout: libraries that print there
     # (RCCL's version banner at communicator init) are sent to stderr.
     sys.stdout.flush()
@@ -211,31 +279,35 @@ def main():
     import torch
     import torch.distributed as dist
 
-    ndev = torch.cuda.device_count()
-    local_dev = local % max(ndev, 1)  # gloo rehearsals may share one GPU
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
+    if not args.dry_run:
+        ndev = torch.cuda.device_count()
+        local_dev = local % max(ndev, 1)  # gloo rehearsals may share one GPU
+        torch.cuda.set_device(local_dev)
+        dev = torch.device("cuda", local_dev)
     if dist_on:
         if world == 1:  # --fanin-at-1 without a launcher
             for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29561"), ("RANK", "0"),
                          ("WORLD_SIZE", "1")):
                 os.environ.setdefault(k, v)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
+        # control plane (barriers, the communicator id, max-over-ranks time) on
+        # the host; the data path (the fan-in) is the library's RCCL gather
+        dist.init_process_group("gloo")
 
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
-    from multiraft_amd.router import allgather_status_packed
+    from multiraft_amd.router import RcclFanIn, allgather_status_packed
 
     if args.config == 2:
         args.groups, args.peers, args.log = 1024, 3, 256
-    G, P, L, K, W = args.groups, args.peers, args.log, args.steps, args.warmup
-    if args.global_groups:
-        if args.global_groups % world:
+    strong = bool(args.global_groups) or (world > 1 and not args.groups)
+    if strong:
+        G_total = args.global_groups or 262144  # config #4 (shardkv/config.go:338-380 deployment)
+        if G_total % world:
             raise SystemExit("--global-groups must be a multiple of the world size")
-        G = args.global_groups // world
-    G_total = G * world
+        G = G_total // world
+    else:
+        G = args.groups or 65536
+        G_total = G * world
+    P, L, K, W = args.peers, args.log, args.steps, args.warmup
     seed = synth_seed(args.config)
     t = time.perf_counter()
     st, lp, _ = synth_tick_state(G_total, P, L, seed=seed, g_begin=rank * G, g_end=(rank + 1) * G,
@@ -247,6 +319,29 @@ def main():
         st["log_term"] = np.ascontiguousarray(
             np.pad(st["log_term"].reshape(G * P, L), ((0, 0), (0, args.log_pad))).reshape(-1))
         L = L + args.log_pad
+
+    rccl = dist_on and args.dist_backend == "nccl"
+    if args.dry_run:
+        if dist_on:
+            dist.barrier()
+            n = torch.tensor([float(G)], dtype=torch.float64)
+            dist.all_reduce(n)
+            assert int(n.item()) == G_total, "the shards do not cover the workload"
+        if rank == 0:
+            print(json.dumps({
+                "metric": METRIC, "value": None, "unit": "decisions/s", "n_gpus": world,
+                "steps": K, "warmup": W, "higher_is_better": True,
+                "scaling": "strong" if strong else "weak", "dry_run": True,
+                "config": {"workload": describe_workload(strong, world, G_total, P, L, args.config,
+                                                         dist_on, rccl, args.dist_backend),
+                           "groups_per_gpu": G, "global_groups": G_total, "peers": P,
+                           "log_capacity": L, "shard_of_rank0": [0, G],
+                           "leaders_in_shard_rank0": int((lp >= 0).sum())}}),
+                file=result_out, flush=True)
+        if dist_on:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     # Ranks allocate in turn (a CPU rehearsal may put several ranks on one GPU).
     for r in range(world):
@@ -265,28 +360,33 @@ def main():
               f"{' (restore inside timed steps)' if restore else ''}")
 
     eng = Engine(G, P, L, device=local_dev, alloc=False)
-    # A dedicated (non-null) stream shared by torch and the engine, so the
-    # events below bracket exactly the engine's kernels.
-    stream = torch.cuda.Stream(dev)
+    if rccl and args.fanin_cus:
+        # the tick runs on a stream masked off the reserved CUs (include/mraft.h)
+        eng.fanin_reserve_cus(args.fanin_cus)
+        stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
+    else:
+        # A dedicated (non-null) stream shared by torch and the engine, so the
+        # events below bracket exactly the engine's kernels.
+        stream = torch.cuda.Stream(dev)
+        eng.set_stream(stream.cuda_stream)
     torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
     lp_d = torch.from_numpy(lp).to(dev)
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    on_host = dist_on and args.dist_backend != "nccl"
+    on_host = dist_on and not rccl
     # Per-step GetState export blocks (commitIndex | term<<1|leader, one buffer
     # so the router's fan-in is ONE collective per tick) and their gathers:
     # never reused within a run, so a step's all-gather can overlap the next
-    # step's tick on its own stream with no buffer hazard.
+    # step's tick on the fan-in stream with no buffer hazard.
     nbuf = W + K
     status = torch.zeros((nbuf, 2 * G), dtype=torch.int32, device=dev)
-    comm = None
-    if dist_on and not on_host:
-        # (a high-priority stream measured no better: the all-gather still waits
-        # for CU slots behind the next tick)
-        comm = stream if args.fanin == "inline" else torch.cuda.Stream(dev)
+    fan = RcclFanIn(eng, rank, world) if rccl else None
+    overlap = args.fanin == "overlap"
     gathered = (torch.empty((nbuf, world * 2 * G), dtype=torch.int32, device=dev)
-                if comm is not None else None)
-    tick_done = [torch.cuda.Event() for _ in range(nbuf)] if comm is not None else []
+                if fan is not None else None)
+    comm_stream = None
+    if fan is not None:
+        comm_stream = (torch.cuda.ExternalStream(eng.fanin_stream(), device=dev) if overlap
+                       else stream)
 
     # Algorithmic words of one tick on the pristine state.
     eng.bind(master)
@@ -294,13 +394,13 @@ def main():
     algo_bytes = 4 * (rd + wr)
 
     # Per-launch kernel timing on the engine's stream. With nothing else on the
-    # stream between ticks (one rank, no restores) one marker between
+    # stream between ticks (no fan-in, no restores) one marker between
     # consecutive ticks serves as the end of one and the start of the next.
     chain = not dist_on and not restore
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
 
-    # The all-gather, timed on its own (reported beside the step).
-    ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if dist_on else []
+    # The all-gather, timed on its own stream (reported beside the step).
+    ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if fan is not None else []
     ag_ms = []
 
     def mark_start(i):
@@ -331,39 +431,48 @@ def main():
                 if timed:
                     ag_ms.append((time.perf_counter() - t1) * 1e3)
             else:
-                # RCCL all-gather of this tick's words on the comm stream, after
-                # the tick and overlapped with the next tick (which writes
-                # another block): the next batch never waits for the fan-in.
-                tick_done[j].record(stream)
-                comm.wait_event(tick_done[j])
-                with torch.cuda.stream(comm):
-                    if timed:
-                        ag_marks[2 * i].record(comm)
-                    allgather_status_packed(status[j], out=gathered[j])
-                    if timed:
-                        ag_marks[2 * i + 1].record(comm)
+                # RCCL all-gather of this tick's words (C ABI). Overlapped: on
+                # the fan-in stream after the tick, beside the next tick (which
+                # writes another block), so the next batch never waits for it.
+                if timed and overlap:
+                    # the gather starts once the tick is done: its start mark
+                    # waits for the tick on the fan-in stream as well
+                    comm_stream.wait_stream(stream)
+                if timed:
+                    ag_marks[2 * i].record(comm_stream)
+                fan.gather(status[j], gathered[j], overlap=overlap)
+                if timed:
+                    ag_marks[2 * i + 1].record(comm_stream)
 
     for i in range(W):
         step(i, False)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
         step(i, True)
     torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
     if dist_on:
         dist.barrier()
-    dt = time.perf_counter() - t0
     ker_ms = [mark_start(i).elapsed_time(mark_end(i)) for i in range(K)]
     log(rank, "tick kernel ms per step: " + " ".join(f"{x:.3f}" for x in ker_ms))
     flags = gf_d.cpu().numpy()
-    if dist_on and not on_host:
+    if fan is not None:
         ag_ms = [ag_marks[2 * i].elapsed_time(ag_marks[2 * i + 1]) for i in range(K)]
+        # the last tick's words, gathered over RCCL, equal every rank's export
+        want = [torch.zeros(2 * G, dtype=torch.int32) for _ in range(world)]
+        dist.all_gather(want, status[K - 1].cpu())
+        assert torch.equal(gathered[K - 1].cpu(), torch.cat(want)), "RCCL fan-in words differ"
     if dist_on:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cpu" if on_host else dev)
+        tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+        km = torch.tensor([float(np.mean(ker_ms))], dtype=torch.float64)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        ker_max_ms = float(km.item())
 
     ker_s = float(np.mean(ker_ms)) / 1e3
     achieved = algo_bytes / ker_s
@@ -382,6 +491,8 @@ def main():
                 traffic_src = f"profiles/{os.path.basename(args.pmc_json)} ({pm.get('tag')})"
         except Exception:
             traffic = None
+    workload = describe_workload(strong, world, G_total, P, L, args.config, dist_on, rccl,
+                                 args.dist_backend)
     out = {
         "metric": METRIC,
         "value": G_total * K / dt,
@@ -391,26 +502,19 @@ def main():
         "warmup": W,
         "ms_per_step": dt / K * 1e3,
         "higher_is_better": True,
-        "scaling": "strong" if args.global_groups else "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": f"synthetic: seeded config-#{args.config} generator (include/mraft_synth.h), fresh "
                 "HBM-resident copy per step",
-        "config": {"workload": (f"config #{args.config}" if not args.global_groups else
-                                f"{G_total:,} groups split over {world} rank(s) (config #4 when 262,144; "
-                                f"generator and mix of config #{args.config})")
-                               + " fused replication tick (a3+a4+a2+a1) with the GetState export fused in"
-                               + ((" + RCCL all-gather of commit/term words" if not on_host else
-                                   f" + {args.dist_backend} all-gather of commit/term words (rehearsal)")
-                                  if dist_on else "")
-                               + (" [cache-resident working set: not an HBM measurement]"
-                                  if args.config == 2 else ""),
+        "config": {"workload": workload,
                    "groups_per_gpu": G, "global_groups": G_total, "peers": P, "log_capacity": L,
                    "committed_groups_last_step": int(((flags & 2) != 0).sum()),
                    "active_groups": active, "restore_in_timed_step": restore,
                    "allgather_ms_mean": float(np.mean(ag_ms)) if ag_ms else None,
                    "allgather_bytes_per_rank": 8 * G if dist_on else 0,
-                   "allgather_placement": args.fanin if comm is not None else None},
+                   "allgather_placement": (args.fanin if fan is not None else None),
+                   "fanin_reserved_cus": args.fanin_cus if fan is not None else 0},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
@@ -420,13 +524,24 @@ def main():
                      "algorithmic_read_bytes": 4 * rd, "algorithmic_write_bytes": 4 * wr,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "algorithmic_bytes_per_decision": algo_bytes / max(active, 1),
-                     "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms))},
+                     "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms)),
+                     "scope": "rank 0's GPU" if world > 1 else "the GPU"},
         "cpu_baseline": None,
     }
-    if rank == 0 and not dist_on and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, args.cpu_seconds, rank)
+    if world > 1:
+        out["roofline"]["kernel_ms_mean_max_over_ranks"] = ker_max_ms
+    if rank == 0 and not args.no_cpu_baseline:
+        # rank 0 only (the other ranks wait at the barrier below); a shorter
+        # sample with more than one rank
+        budget = args.cpu_seconds if world == 1 else min(args.cpu_seconds, 6.0)
+        out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, budget, rank)
     if rank == 0:
         print(json.dumps(out), file=result_out, flush=True)
+    if dist_on:
+        dist.barrier()
+    if fan is not None:
+        eng.fanin_synchronize()
+        fan.close()
     eng.close()
     if dist_on:
         dist.destroy_process_group()

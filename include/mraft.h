@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MRAFT_ABI_VERSION 2
+#define MRAFT_ABI_VERSION 3
 
 /* Node states, raft_rpc.go:8-12 (values preserved). */
 enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
@@ -500,6 +500,58 @@ int mraft_realloc_gid(int32_t *shards, int32_t nshards, const int32_t *gids, int
 int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer,
                               int32_t *commit, int32_t *term_leader,
                               int32_t where);
+
+/* ---- multi-GPU fan-in: RCCL over xGMI ---------------------
+ * Groups partition over the GPUs of a node (one engine handle and one process
+ * per GPU); no decision reads another group. The only exchange is the shard
+ * router's view of every group's GetState words, which replaces the host
+ * polling of GetState()/commit progress by the services
+ * (src/kvraft/server.go:114, src/shardctrler/server.go:154,
+ * src/shardkv/client.go:68-100): once per tick every rank all-gathers its
+ * [2*G] status block (commitIndex[0:G], currentTerm<<1|isLeader[G:2G], as
+ * written by mraft_replicate_tick_export / mraft_export_group_status into the
+ * two halves of one buffer) into a [nranks*2*G] rank-major buffer.
+ *
+ * The communicator is a plain RCCL ncclComm_t passed as void*: the host may
+ * bring its own, or make one with mraft_comm_unique_id (on one rank) +
+ * distribution of the 128 id bytes over its own control plane +
+ * mraft_comm_init (on every rank). */
+#define MRAFT_COMM_ID_BYTES 128
+
+/* ncclGetUniqueId: the bootstrap id of a new communicator (one rank calls it
+ * and ships the bytes to the others). */
+int mraft_comm_unique_id(uint8_t out[MRAFT_COMM_ID_BYTES]);
+/* ncclCommInitRank on the engine's device: *out_comm is an ncclComm_t. Every
+ * rank must call it (collectively) with the same id. */
+int mraft_comm_init(mraft_engine *h, int32_t nranks, int32_t rank,
+                    const uint8_t id[MRAFT_COMM_ID_BYTES], void **out_comm);
+int mraft_comm_destroy(void *comm);
+
+/* mraft_allgather_status flags */
+enum {
+  /* Enqueue on the engine's fan-in stream behind everything already enqueued
+   * on its stream (an event, no host wait): later work on the engine stream
+   * (the next tick) does not wait for the gather. The caller must not reuse
+   * `local`/`gathered` before mraft_fanin_synchronize or a later gather. */
+  MRAFT_FANIN_OVERLAP = 1
+};
+
+/* All-gather of the [2*G] status words of every rank over `comm` (ncclAllGather,
+ * int32): gathered[r*2*G + k] = rank r's local[k]. Device buffers
+ * (MRAFT_DEVICE, asynchronous) or host buffers (MRAFT_HOST, staged,
+ * synchronous; OVERLAP ignored). */
+int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local,
+                           int32_t *gathered, int32_t where, uint32_t flags);
+/* Wait for the fan-in stream. */
+int mraft_fanin_synchronize(mraft_engine *h);
+/* The fan-in stream (a hipStream_t), e.g. for events. */
+void *mraft_fanin_stream(mraft_engine *h);
+/* Reserve n_cus compute units for the fan-in: the engine's own stream becomes
+ * a stream whose kernels (the tick) may use every CU but those, and the
+ * fan-in stream one limited to those, so an overlapped gather does not queue
+ * for CU slots behind a tick that fills the device. n_cus = 0 restores the
+ * unmasked streams. Replaces a stream set with mraft_set_stream. */
+int mraft_fanin_reserve_cus(mraft_engine *h, int32_t n_cus);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,9 @@ G_SNAPSHOT_INSTALLED = 256
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
  G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
+FANIN_OVERLAP = 1
+COMM_ID_BYTES = 128
 SYN_MATCH, SYN_MISMATCH, SYN_BEYOND, SYN_STALE, SYN_BELOW_DUMMY, SYN_HEARTBEAT = range(6)
 
 
@@ -89,6 +91,8 @@ ABI_SYMBOLS = (
     "mraft_restore", "mraft_encode_persistent", "mraft_decode_persistent",
     "mraft_key2shard", "mraft_realloc_gid", "mraft_replicate_tick_export",
     "mraft_collect_apply_compact",
+    "mraft_comm_unique_id", "mraft_comm_init", "mraft_comm_destroy", "mraft_allgather_status",
+    "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -131,6 +135,13 @@ _SIGS = {
     "mraft_replicate_tick_export": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32]),
     "mraft_collect_apply_compact": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i32]),
     "mraft_realloc_gid": (ctypes.c_int, [_vp, _i32, _vp, _i32]),
+    "mraft_comm_unique_id": (ctypes.c_int, [_vp]),
+    "mraft_comm_init": (ctypes.c_int, [_vp, _i32, _i32, _vp, ctypes.POINTER(_vp)]),
+    "mraft_comm_destroy": (ctypes.c_int, [_vp]),
+    "mraft_allgather_status": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _u32]),
+    "mraft_fanin_synchronize": (ctypes.c_int, [_vp]),
+    "mraft_fanin_stream": (_vp, [_vp]),
+    "mraft_fanin_reserve_cus": (ctypes.c_int, [_vp, _i32]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

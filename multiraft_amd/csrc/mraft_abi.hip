@@ -3,7 +3,9 @@
 // Host side of the engine: device state ownership (one HBM-resident SoA image
 // per handle), staging of host batches, duplicate-slot claims and kernel
 // launches on the handle's stream. No exception or C++ type crosses the ABI.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cstdarg>
 #include <cstdio>
@@ -20,6 +22,10 @@ struct mraft_engine {
   bool owned = false, bound = false;
   mraft_soa dev{};
   hipStream_t own_stream = nullptr, stream = nullptr;
+  // fan-in (mraft_allgather_status): its own stream, ordered after the engine
+  // stream by an event; optional CU-masked pair (mraft_fanin_reserve_cus)
+  hipStream_t fanin_own = nullptr, fanin_masked = nullptr, tick_masked = nullptr;
+  hipEvent_t fanin_ev = nullptr;
   unsigned long long *claim = nullptr;
   uint32_t epoch = 0;
   std::vector<void *> scratch_ptr;
@@ -226,14 +232,18 @@ int mraft_destroy(mraft_engine *h) {
   for (void *p : h->scratch_ptr)
     if (p) (void)hipFree(p);
   if (h->claim) (void)hipFree(h->claim);
-  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
+  if (h->fanin_masked) (void)hipStreamSynchronize(h->fanin_masked);
+  for (hipStream_t s : {h->own_stream, h->fanin_own, h->fanin_masked, h->tick_masked})
+    if (s) (void)hipStreamDestroy(s);
+  if (h->fanin_ev) (void)hipEventDestroy(h->fanin_ev);
   delete h;
   return MRAFT_OK;
 }
 
 int mraft_set_stream(mraft_engine *h, void *stream) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
-  h->stream = stream ? (hipStream_t)stream : h->own_stream;
+  h->stream = stream ? (hipStream_t)stream : (h->tick_masked ? h->tick_masked : h->own_stream);
   return MRAFT_OK;
 }
 
@@ -741,6 +751,135 @@ int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer, int32
   TRY(sg.map(term_leader, sizeof(int32_t) * h->G, false, true, &t));
   mraft::launch_export(dev_of(h), (const int32_t *)lp, (int32_t *)c, (int32_t *)t, h->stream);
   return sg.finish();
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- fan-in (§8e)
+
+namespace {
+
+#define NCCL_TRY(expr)                                                                  \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return fail(MRAFT_E_HIP, "%s failed: %s", #expr, ncclGetErrorString(r_));         \
+  } while (0)
+
+int fanin_stream_of(mraft_engine *h, hipStream_t *out) {
+  if (h->fanin_masked) {
+    *out = h->fanin_masked;
+    return MRAFT_OK;
+  }
+  if (!h->fanin_own) HIP_TRY(hipStreamCreateWithFlags(&h->fanin_own, hipStreamNonBlocking));
+  *out = h->fanin_own;
+  return MRAFT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mraft_comm_unique_id(uint8_t out[MRAFT_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == MRAFT_COMM_ID_BYTES, "RCCL unique id size");
+  if (!out) return fail(MRAFT_E_INVAL, "out is null");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof id);
+  return MRAFT_OK;
+}
+
+int mraft_comm_init(mraft_engine *h, int32_t nranks, int32_t rank, const uint8_t id[MRAFT_COMM_ID_BYTES],
+                    void **out_comm) {
+  if (!h || !id || !out_comm) return fail(MRAFT_E_INVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(MRAFT_E_INVAL, "bad rank %d of %d", rank, nranks);
+  *out_comm = nullptr;
+  HIP_TRY(hipSetDevice(h->device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  ncclComm_t c = nullptr;
+  NCCL_TRY(ncclCommInitRank(&c, nranks, uid, rank));
+  *out_comm = (void *)c;
+  return MRAFT_OK;
+}
+
+int mraft_comm_destroy(void *comm) {
+  if (!comm) return MRAFT_OK;
+  NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
+  return MRAFT_OK;
+}
+
+int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local, int32_t *gathered,
+                           int32_t where, uint32_t flags) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (!comm || !local || !gathered) return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  ncclComm_t c = (ncclComm_t)comm;
+  int nranks = 0;
+  NCCL_TRY(ncclCommCount(c, &nranks));
+  const size_t words = 2 * (size_t)h->G;
+  if (where == MRAFT_HOST) {
+    Stage sg(h, where);
+    void *l, *g;
+    TRY(sg.map(local, sizeof(int32_t) * words, true, false, &l));
+    TRY(sg.map(gathered, sizeof(int32_t) * words * nranks, false, true, &g));
+    NCCL_TRY(ncclAllGather(l, g, words, ncclInt32, c, h->stream));
+    return sg.finish();
+  }
+  hipStream_t st = h->stream;
+  if (flags & MRAFT_FANIN_OVERLAP) {
+    TRY(fanin_stream_of(h, &st));
+    if (!h->fanin_ev) HIP_TRY(hipEventCreateWithFlags(&h->fanin_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->fanin_ev, h->stream));
+    HIP_TRY(hipStreamWaitEvent(st, h->fanin_ev, 0));
+  }
+  NCCL_TRY(ncclAllGather(local, gathered, words, ncclInt32, c, st));
+  HIP_TRY(hipGetLastError());
+  return MRAFT_OK;
+}
+
+int mraft_fanin_synchronize(mraft_engine *h) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  HIP_TRY(hipSetDevice(h->device));
+  hipStream_t st;
+  TRY(fanin_stream_of(h, &st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return MRAFT_OK;
+}
+
+void *mraft_fanin_stream(mraft_engine *h) {
+  if (!h) return nullptr;
+  hipStream_t st = nullptr;
+  if (hipSetDevice(h->device) != hipSuccess || fanin_stream_of(h, &st) != MRAFT_OK) return nullptr;
+  return (void *)st;
+}
+
+int mraft_fanin_reserve_cus(mraft_engine *h, int32_t n_cus) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  HIP_TRY(hipSetDevice(h->device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, h->device));
+  const int ncu = prop.multiProcessorCount;
+  if (n_cus < 0 || n_cus >= ncu) return fail(MRAFT_E_INVAL, "n_cus %d of %d CUs", n_cus, ncu);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  for (hipStream_t *s : {&h->fanin_masked, &h->tick_masked})
+    if (*s) {
+      HIP_TRY(hipStreamSynchronize(*s));
+      HIP_TRY(hipStreamDestroy(*s));
+      *s = nullptr;
+    }
+  if (n_cus == 0) {
+    h->stream = h->own_stream;
+    return MRAFT_OK;
+  }
+  // The highest n_cus CU bits go to the fan-in, the rest to the tick.
+  const int nw = (ncu + 31) / 32;
+  std::vector<uint32_t> tick(nw, 0), fan(nw, 0);
+  for (int cu = 0; cu < ncu; ++cu) (cu >= ncu - n_cus ? fan : tick)[cu / 32] |= 1u << (cu % 32);
+  HIP_TRY(hipExtStreamCreateWithCUMask(&h->tick_masked, (uint32_t)nw, tick.data()));
+  HIP_TRY(hipExtStreamCreateWithCUMask(&h->fanin_masked, (uint32_t)nw, fan.data()));
+  h->stream = h->tick_masked;
+  return MRAFT_OK;
 }
 
 }  // extern "C"

@@ -370,6 +370,51 @@ class Engine:
         return commit, tl
 
 
+    # ---- multi-GPU fan-in (include/mraft.h) -----------------
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> int:
+        """ncclCommInitRank on this engine's device (collective over the ranks):
+        returns the ncclComm_t as an integer handle."""
+        if len(uid) != _abi.COMM_ID_BYTES:
+            raise ValueError("unique id must be 128 bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        c = ctypes.c_void_p()
+        _ck(self._lib.mraft_comm_init(self._h, nranks, rank, ctypes.addressof(buf), ctypes.byref(c)),
+            "mraft_comm_init")
+        return c.value
+
+    def allgather_status(self, comm: int, local, gathered=None, where: int = DEVICE,
+                         overlap: bool = False):
+        """All-gather this rank's [2*G] status block (commit | term<<1|leader)
+        into the [nranks*2*G] rank-major `gathered` buffer over RCCL."""
+        if where == HOST:
+            local = np.ascontiguousarray(local, dtype=np.int32)
+        _ck(self._lib.mraft_allgather_status(self._h, comm, ptr(local), ptr(gathered), where,
+                                             _abi.FANIN_OVERLAP if overlap else 0),
+            "mraft_allgather_status")
+        return gathered
+
+    def fanin_synchronize(self):
+        _ck(self._lib.mraft_fanin_synchronize(self._h), "mraft_fanin_synchronize")
+
+    def fanin_stream(self) -> int:
+        return self._lib.mraft_fanin_stream(self._h) or 0
+
+    def fanin_reserve_cus(self, n_cus: int):
+        _ck(self._lib.mraft_fanin_reserve_cus(self._h, n_cus), "mraft_fanin_reserve_cus")
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (mraft_comm_unique_id): 128 bootstrap bytes one rank
+    creates and the host ships to the others over its own control plane."""
+    buf = ctypes.create_string_buffer(_abi.COMM_ID_BYTES)
+    _ck(_abi.lib().mraft_comm_unique_id(ctypes.addressof(buf)), "mraft_comm_unique_id")
+    return buf.raw
+
+
+def comm_destroy(comm: int):
+    _ck(_abi.lib().mraft_comm_destroy(comm), "mraft_comm_destroy")
+
+
 def export_group_status_into(eng: Engine, leader_peer, commit, term_leader, where: int = DEVICE):
     """GetState for every group into caller buffers (device tensors by default)."""
     _ck(eng._lib.mraft_export_group_status(eng._h, ptr(leader_peer), ptr(commit), ptr(term_leader),

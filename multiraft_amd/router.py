@@ -84,6 +84,38 @@ class ShardCtrlerState:
         return self.configs[-1] if num < 0 or num >= len(self.configs) else self.configs[num]
 
 
+class RcclFanIn:
+    """The fan-in over the library's RCCL communicator (include/mraft.h
+    §multi-GPU fan-in). Rank 0 makes the communicator's unique id and the host
+    control plane (here any torch.distributed group, e.g. gloo) ships the 128
+    bytes to the other ranks; every rank then joins with mraft_comm_init."""
+
+    def __init__(self, eng, rank: int, world: int, broadcast_id=None):
+        from .engine import comm_unique_id
+        uid = comm_unique_id() if rank == 0 else bytes(128)
+        if world > 1:
+            if broadcast_id is None:
+                import torch.distributed as dist
+
+                def broadcast_id(b):
+                    box = [b]
+                    dist.broadcast_object_list(box, src=0)
+                    return box[0]
+            uid = broadcast_id(uid)
+        self.eng, self.rank, self.world = eng, rank, world
+        self.comm = eng.comm_init(world, rank, uid)
+
+    def gather(self, local, out, overlap: bool = True):
+        """local: [2*G] device block of this rank; out: [world*2*G] device."""
+        return self.eng.allgather_status(self.comm, local, out, overlap=overlap)
+
+    def close(self):
+        from .engine import comm_destroy
+        if self.comm:
+            comm_destroy(self.comm)
+            self.comm = None
+
+
 def allgather_status(commit_local, term_leader_local):
     """All-gather the per-group status words of this rank's groups (torch
     tensors, same length on every rank) into global [world * G] tensors."""

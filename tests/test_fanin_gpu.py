@@ -1,0 +1,58 @@
+"""The multi-GPU fan-in behind the C ABI (include/mraft.h) on one
+GPU: a one-rank RCCL communicator made with mraft_comm_unique_id +
+mraft_comm_init, and mraft_allgather_status of the words the fused tick
+exported (mraft_replicate_tick_export). The gathered block must equal the
+exported words and the oracle's GetState words (src/raft/raft.go:237-246),
+on the engine stream, overlapped on the fan-in stream, with CUs reserved for
+the fan-in, and through host buffers."""
+import numpy as np
+import pytest
+
+from oracle_lib import Oracle
+
+from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
+from multiraft_amd.router import GroupStatusView, RcclFanIn, unpack_status
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("mode", ["inline", "overlap", "reserved_cus", "host"])
+def test_one_rank_rccl_gather_equals_export(mode):
+    import torch
+    G, P, L = 4096, 5, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
+    o = Oracle(G, P, L, st)
+    ogf = o.replicate_tick(lp)
+    oc, otl = o.export_group_status(lp)
+    with Engine(G, P, L, device=0) as e:
+        e.load_state(st)
+        if mode == "reserved_cus":
+            e.fanin_reserve_cus(8)
+        fan = RcclFanIn(e, rank=0, world=1)
+        try:
+            if mode == "host":
+                gf, c, tl = e.replicate_tick_export(lp)
+                assert np.array_equal(gf, ogf)
+                out = np.zeros(2 * G, np.int32)
+                e.allgather_status(fan.comm, np.concatenate([c, tl]), out, where=0)
+                got = out
+            else:
+                dev = torch.device("cuda", 0)
+                lp_d = torch.from_numpy(lp).to(dev)
+                gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
+                status = torch.zeros(2 * G, dtype=torch.int32, device=dev)
+                out = torch.full((2 * G,), -7, dtype=torch.int32, device=dev)
+                torch.cuda.synchronize()
+                e.replicate_tick_export(lp_d, gf_d, status[:G], status[G:], where=DEVICE)
+                fan.gather(status, out, overlap=(mode != "inline"))
+                e.synchronize()
+                e.fanin_synchronize()
+                assert np.array_equal(gf_d.cpu().numpy(), ogf)
+                assert np.array_equal(status.cpu().numpy(), np.concatenate([oc, otl]))
+                got = out.cpu().numpy()
+            gc, gt = unpack_status(torch.from_numpy(got), 1)
+            assert np.array_equal(gc.numpy(), oc) and np.array_equal(gt.numpy(), otl)
+            view = GroupStatusView(gc.numpy(), gt.numpy())
+            assert int(view.is_leader.sum()) == int(((otl & 1) != 0).sum())
+        finally:
+            fan.close()
