@@ -400,8 +400,31 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   const int64_t src_n = en ? n_entry_terms : gp_of(h) * h->L;
   mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h),
                       h->P, h->claim, h->epoch, (int32_t *)e, h->stream);
-  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (mraft_ae_reply *)r,
-                          (int32_t *)e, h->stream);
+  void *soff = nullptr, *stage = nullptr;
+  int64_t n_stage = 0;
+  if (!en) {
+    // Entries by reference into the engine's log: stage those whose source
+    // row this batch also writes (the reference's copy at gather time,
+    // raft_append_entry.go:50-54). Sizing the staging buffer costs one host
+    // round trip on this path.
+    void *tot;
+    TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
+    TRY(scratch(h, 15, sizeof(unsigned long long), &tot));
+    HIP_TRY(hipMemsetAsync(tot, 0, sizeof(unsigned long long), h->stream));
+    mraft::launch_ae_stage_plan((const mraft_ae_args *)a, n, src_n, h->L, h->claim, h->epoch,
+                                (const int32_t *)e, (int64_t *)soff, (unsigned long long *)tot, h->stream);
+    unsigned long long ht = 0;
+    HIP_TRY(hipMemcpyAsync(&ht, tot, sizeof ht, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (ht > 0) {
+      n_stage = (int64_t)ht;
+      TRY(scratch(h, 16, sizeof(int32_t) * (size_t)ht, &stage));
+      mraft::launch_ae_stage_copy(h->dev.log_term, (const mraft_ae_args *)a, n, (const int64_t *)soff,
+                                  (int32_t *)stage, h->stream);
+    }
+  }
+  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
+                          n_stage, (const int64_t *)soff, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
   return sg.finish();
 }
 

@@ -112,9 +112,45 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
                         // messages share one L2 for the leader entries (another 8 %)
 #endif
 
+// Entries by reference into the engine's own log (entry_terms NULL): the
+// reference copies args.Entries when it builds the message (appendOneRound,
+// raft_append_entry.go:50-54), before any handler runs. An item whose source
+// row is also a receiving slot of this batch (a stale second leader of the
+// group; claim epoch set by k_claim) would race with that item's writes, so
+// its entries are staged first: k_ae_stage_plan assigns each such item a range
+// of the staging buffer, k_ae_stage_copy copies the pre-batch entries there.
+__global__ void k_ae_stage_plan(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L,
+                                const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                const int32_t *__restrict__ err, int64_t *__restrict__ soff,
+                                unsigned long long *__restrict__ total) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const mraft_ae_args a = args[i];
+  int64_t o = -1;
+  if (!err[i] && a.n_entries > 0 && a.entries_offset >= 0 && a.entries_offset + a.n_entries <= n_log) {
+    const int64_t r0 = a.entries_offset / L, r1 = (a.entries_offset + a.n_entries - 1) / L;
+    bool hit = false;
+    for (int64_t r = r0; r <= r1 && !hit; ++r) hit = (uint32_t)(claim[r] >> 32) == epoch;
+    if (hit) o = (int64_t)atomicAdd(total, (unsigned long long)a.n_entries);
+  }
+  soff[i] = o;
+}
+
+__global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const mraft_ae_args *__restrict__ args,
+                                int64_t n, const int64_t *__restrict__ soff, int32_t *__restrict__ stage) {
+  const int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t o = soff[i];
+  if (o < 0) return;
+  const mraft_ae_args a = args[i];
+  wave_copy(log + a.entries_offset, stage + o, a.n_entries);
+}
+
 __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
-                                                   int64_t n, const int32_t *__restrict__ ent,
-                                                   int64_t n_ent, mraft_ae_reply *__restrict__ rep,
+                                                   int64_t n, const int32_t *__restrict__ ent0,
+                                                   int64_t n_ent0, const int32_t *__restrict__ stage,
+                                                   int64_t n_stage, const int64_t *__restrict__ soff,
+                                                   mraft_ae_reply *__restrict__ rep,
                                                    int32_t *__restrict__ err) {
   int64_t gb = blockIdx.x;
   if (MRAFT_AE_XCD) {
@@ -128,11 +164,19 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
   // Three round trips before the merge: the item (error word and args
   // together), the follower's scalars (one load per lane), log[prev].
   const int e = err[i];
-  const mraft_ae_args a = args[i];
-  // Both loads in flight before the branch (else the compiler sinks the args
+  mraft_ae_args a = args[i];
+  const int64_t so = soff ? soff[i] : -1;
+  // All loads in flight before the branch (else the compiler sinks the args
   // load behind the error check: one more round trip).
   asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
-               "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset));
+               "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so));
+  const int32_t *__restrict__ ent = ent0;
+  int64_t n_ent = n_ent0;
+  if (so >= 0) {  // staged entries (k_ae_stage_plan)
+    ent = stage;
+    n_ent = n_stage;
+    a.entries_offset = so;
+  }
   if (e) {
     if (lane == 0) rep[i] = r;
     return;
@@ -912,11 +956,24 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
                      out, err);
 }
 
+void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
+                          const unsigned long long *claim, uint32_t epoch, const int32_t *err,
+                          int64_t *soff, unsigned long long *total, hipStream_t st) {
+  hipLaunchKernelGGL(k_ae_stage_plan, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, claim,
+                     epoch, err, soff, total);
+}
+
+void launch_ae_stage_copy(const int32_t *log, const mraft_ae_args *args, int64_t n, const int64_t *soff,
+                          int32_t *stage, hipStream_t st) {
+  hipLaunchKernelGGL(k_ae_stage_copy, dim3(blocks_for(n, 4)), dim3(256), 0, st, log, args, n, soff, stage);
+}
+
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
-                      int64_t n_ent, mraft_ae_reply *rep, int32_t *err, hipStream_t st) {
+                      int64_t n_ent, const int32_t *stage, int64_t n_stage, const int64_t *soff,
+                      mraft_ae_reply *rep, int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n * 64, 64 * MRAFT_AE_WPB)), dim3(64 * MRAFT_AE_WPB), 0, st,
-                     s, args, n, ent, n_ent, rep, err);
+  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n, MRAFT_AE_WPB)), dim3(64 * MRAFT_AE_WPB), 0, st, s, args, n,
+                     ent, n_ent, stage, n_stage, soff, rep, err);
 }
 
 #if MRAFT_FOLD_TRACE

@@ -329,5 +329,135 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
   }
 }
 
+// The whole streaming pass as ONE software-pipelined loop (VEC layout, one
+// dwordx4 per lane and stream per 256-entry chunk): compare chunk c, then
+// issue chunk c+256's loads (the leader's and every still-comparing
+// follower's), then chunk c's stores. gfx9's vmcnt counts loads and stores in
+// one in-order counter, so in pass_chunk + copy_loop a compare chunk waited
+// for the previous chunk's stores before its own loads returned (a store round
+// trip plus a load round trip per chunk); here the next loads are in flight
+// before the stores issue. Same results, loads and stores as pass_chunk
+// followed by copy_loop: chunk c+256 is loaded only when the loop runs for it,
+// and every load stays inside the row it streams (lanes whose 4 entries end
+// before plo / start do not load).
+template <int NI, bool COUNT>
+__device__ __forceinline__ void stream_pass(const int32_t *__restrict__ src, int32_t *__restrict__ log,
+                                            long long eo, const long long (&fo)[NI],
+                                            const int (&start)[NI], const int (&cend)[NI], int nend,
+                                            int (&mode)[NI], int (&cfrom)[NI], const int (&capok)[NI],
+                                            int &fullmask, int slo, int shi, int T, int &found, int c,
+                                            int plo, int phi) {
+  constexpr int CW = 256;
+  const int lane = lane_id();
+  auto runs = [&](int cc) {
+    if (cc > phi) return false;
+    bool a = slo <= shi && cc <= shi;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) a = a || mode[q] != M_DONE;
+    return a;
+  };
+  auto load_leader = [&](int cc) {
+    const int i0 = cc + 4 * lane;
+    int4 x = make_int4(0, 0, 0, 0);
+    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src + eo + i0);
+    return x;
+  };
+  auto load_follower = [&](int q, int cc) {
+    const int i0 = cc + 4 * lane;
+    int4 x = make_int4(0, 0, 0, 0);
+    if (mode[q] == M_CMP && start[q] <= cc + CW - 1 && cend[q] > cc && i0 + 3 >= start[q] && i0 < cend[q])
+      x = ld4(log + fo[q] + i0);
+    return x;
+  };
+  if (!runs(c)) return;
+  int4 e = load_leader(c);
+  int4 f[NI];
+#pragma unroll
+  for (int q = 0; q < NI; ++q) f[q] = load_follower(q, c);
+  for (;;) {
+    const int i0 = c + 4 * lane;
+    const int ev[4] = {e.x, e.y, e.z, e.w};
+    // Commit scan: highest index of this chunk in [slo, shi] with term T.
+    if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+      int lu = -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u >= slo && i0 + u <= shi && ev[u] == T) lu = u;
+      const unsigned long long m = __ballot(lu >= 0);
+      if (m) {
+        const int l = 63 - __clzll((long long)m);
+        found = c + 4 * l + __shfl(lu, l, 64);
+      }
+    }
+    // Compare: first mismatch of every follower still comparing.
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (mode[q] != M_CMP || start[q] > c + CW - 1) continue;
+      int im = -1;
+      if (cend[q] > c) {
+        const int fv[4] = {f[q].x, f[q].y, f[q].z, f[q].w};
+        int first = 4;
+#pragma unroll
+        for (int u = 3; u >= 0; --u)
+          if (i0 + u >= start[q] && i0 + u < cend[q] && ev[u] != fv[u]) first = u;
+        const unsigned long long m = __ballot(first < 4);
+        if (m) {
+          const int l = first_lane(m);
+          im = c + 4 * l + __shfl(first, l, 64);
+        }
+      }
+      if (im < 0 && cend[q] <= c + CW - 1) {
+        // Compared region ends in this chunk without a mismatch: every entry
+        // matched (no truncation: the non-FIFO guard, :146-155) or the
+        // follower's log ends before the entries do ("beyond the end").
+        if (cend[q] < nend) im = cend[q];
+        else mode[q] = M_DONE;
+      }
+      if (im >= 0) {
+        cfrom[q] = im;
+        if (capok[q]) {
+          mode[q] = M_COPY;
+        } else {
+          mode[q] = M_DONE;  // MRAFT_ITEM_LOG_FULL: no state change
+          fullmask |= 1 << q;
+        }
+      }
+    }
+    // This chunk's copies, and who still needs the next chunk.
+    int cmask = 0;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (mode[q] != M_COPY) continue;
+      cmask |= 1 << q;
+      if (c + CW >= nend) mode[q] = M_DONE;
+    }
+    const int cn = c + CW;
+    const bool more = runs(cn);
+    int4 en = make_int4(0, 0, 0, 0);
+    int4 fn[NI];
+    if (more) en = load_leader(cn);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) fn[q] = more ? load_follower(q, cn) : make_int4(0, 0, 0, 0);
+    if (!COUNT) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if (!((cmask >> q) & 1)) continue;
+        if (i0 >= cfrom[q] && i0 + 3 < nend) {
+          st4(log + fo[q] + i0, e.x, e.y, e.z, e.w);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + u >= cfrom[q] && i0 + u < nend) st1(log + fo[q] + i0 + u, ev[u]);
+        }
+      }
+    }
+    if (!more) return;
+    c = cn;
+    e = en;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) f[q] = fn[q];
+  }
+}
+
 }  // namespace
 }  // namespace mraft

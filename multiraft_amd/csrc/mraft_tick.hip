@@ -34,6 +34,8 @@
 #include "mraft_internal.h"
 #include "mraft_pass.h"
 
+#include <cstdlib>
+
 namespace mraft {
 
 namespace {
@@ -161,6 +163,12 @@ struct Fold {
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
 #endif
+#ifndef MRAFT_TICK_HDR_EXTRA
+#define MRAFT_TICK_HDR_EXTRA 0  // experiment: extra dependent header round trips (wrong only in timing)
+#endif
+#ifndef MRAFT_TICK_STREAM
+#define MRAFT_TICK_STREAM 0  // 1: one software-pipelined streaming loop (stream_pass; spills: slower)
+#endif
 #ifndef MRAFT_TICK_TRACE
 #define MRAFT_TICK_TRACE 0  // diagnostic build: s_memrealtime stamps per group (tools/trace_tick.py)
 #endif
@@ -226,7 +234,18 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
     return;
   }
-  const long long ld = (long long)g * P + lp;
+  long long ld = (long long)g * P + lp;
+#if MRAFT_TICK_HDR_EXTRA
+  // Experiment only (header-latency slope): MRAFT_TICK_HDR_EXTRA
+  // more dependent round trips before the header (a load of an unrelated line
+  // whose value, zeroed behind the compiler's back, feeds the leader index).
+#pragma unroll
+  for (int k = 0; k < MRAFT_TICK_HDR_EXTRA; ++k) {
+    int z = s.votes[(ld * 977 + 131 * k) % ((long long)s.G * P)];
+    asm volatile("v_and_b32 %0, 0, %0" : "+v"(z));
+    ld += uni(z);
+  }
+#endif
   const long long lrow = ld * L;
   // Every load that depends only on the leader index, issued together.
   const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
@@ -425,7 +444,11 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
     constexpr int VC = MRAFT_TICK_VC;
-    if (vec) {
+    if (vec && MRAFT_TICK_STREAM) {
+      const int c = plo - (int)((eo + plo) & (MRAFT_TICK_ALIGN - 1));
+      stream_pass<NI, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok, fullmask, slo,
+                             shi, T, found, c, plo, phi);
+    } else if (vec) {
       int c = plo - (int)((eo + plo) & (MRAFT_TICK_ALIGN - 1));
       for (; c <= phi; c += 256 * V) {
         bool cmp = false;
@@ -643,12 +666,23 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
   }
 }
 
+// Experiment knob (not a product setting): MRAFT_TICK_DYN_LDS=<bytes> gives
+// every tick workgroup that much dynamic LDS, capping the waves per CU at
+// 160 KiB / bytes (occupancy experiments, tools/exp_lottery3.py).
+inline size_t tick_dyn_lds() {
+  static const size_t v = [] {
+    const char *e = getenv("MRAFT_TICK_DYN_LDS");
+    return e ? (size_t)atol(e) : (size_t)0;
+  }();
+  return v;
+}
+
 template <int P, bool COUNT>
 void launch_tick_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
                    Export ex, hipStream_t st) {
   const int blocks = (s.G + MRAFT_TICK_WPB - 1) / MRAFT_TICK_WPB;
-  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), 0, st, s, lpeer, gflags,
-                     counts, ex);
+  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), tick_dyn_lds(), st, s,
+                     lpeer, gflags, counts, ex);
 }
 
 template <bool COUNT>

@@ -259,6 +259,31 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
   int32_t *first = claim_slots(e, &args[0].slot, n, sizeof(mraft_ae_args), item_err);
   const int32_t *src = entry_terms ? entry_terms : S.log_term;
   int64_t src_n = entry_terms ? n_entry_terms : (int64_t)e->G * e->P * e->L;
+  /* Entries by reference into the engine's own log (entry_terms NULL, the
+   * view mraft_gather_append_args hands out): the reference copies
+   * args.Entries when it builds the message (appendOneRound,
+   * raft_append_entry.go:50-54), before any handler runs, so every item reads
+   * the log as it was before the batch — even when another item of the same
+   * batch rewrites its source row (two leaders of one group). Stage them. */
+  int32_t *staged = NULL;
+  int64_t *soff = NULL;
+  if (!entry_terms && n > 0) {
+    soff = (int64_t *)malloc(sizeof(int64_t) * (size_t)n);
+    int64_t tot = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const mraft_ae_args *a = &args[i];
+      soff[i] = -1;
+      if (item_err[i] || a->n_entries < 0 || a->entries_offset < 0 ||
+          (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n))
+        continue;
+      soff[i] = tot;
+      tot += a->n_entries;
+    }
+    staged = (int32_t *)malloc(sizeof(int32_t) * (size_t)(tot > 0 ? tot : 1));
+    for (int64_t i = 0; i < n; ++i)
+      if (soff[i] >= 0 && args[i].n_entries > 0)
+        memcpy(staged + soff[i], src + args[i].entries_offset, sizeof(int32_t) * (size_t)args[i].n_entries);
+  }
   for (int64_t i = 0; i < n; ++i) {
     memset(&replies[i], 0, sizeof(replies[i]));
     if (item_err[i]) continue;
@@ -269,9 +294,11 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
       continue;
     }
     int fc;
-    item_err[i] = handle_ae_one(e, a->slot, a, src + a->entries_offset, -1,
+    item_err[i] = handle_ae_one(e, a->slot, a, staged ? staged + soff[i] : src + a->entries_offset, -1,
                                 &replies[i], &fc);
   }
+  free(staged);
+  free(soff);
   free(first);
   return MRAFT_OK;
 }

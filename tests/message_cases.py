@@ -1,0 +1,93 @@
+"""Message-level batch builders shared by the CPU and GPU parity tests: the
+gather -> handle -> fold path a host drives for network-delivered batches
+(include/mraft.h; raft_append_entry.go:20-162)."""
+import numpy as np
+
+from multiraft_amd._abi import AE_RESULT, LEADER
+
+
+def all_follower_items(lp, G, P):
+    """(leader slot, peer) for every follower of every group with a leader."""
+    g = np.repeat(np.arange(G), P - 1)
+    ld = g * P + np.repeat(lp, P - 1)
+    q = np.tile(np.arange(P - 1), G)
+    peers = np.where(q < np.repeat(lp, P - 1), q, q + 1)
+    keep = np.repeat(lp >= 0, P - 1)
+    return ld[keep].astype(np.int32), peers[keep].astype(np.int32)
+
+
+def external_entries(args, ok, log_term, misalign=True):
+    """Copy every gathered item's entries (a view into the leader's log row,
+    entries_offset) into one external buffer, as the network would deliver
+    them; item j starts at a 16-B aligned position plus (j % 4) words when
+    `misalign`. Returns (args with rebased entries_offset, buffer)."""
+    a2 = args.copy()
+    n = np.where(ok, args["n_entries"], 0).astype(np.int64)
+    pad = (np.arange(len(args)) % 4) if misalign else np.zeros(len(args), np.int64)
+    span = ((n + 3) // 4) * 4 + 4                      # each item in its own 16-B aligned slab
+    start = np.concatenate([[0], np.cumsum(span)[:-1]]) + pad
+    total = int(span.sum()) + 4
+    buf = np.zeros(total, np.int32)
+    idx_item = np.repeat(np.arange(len(args)), n)
+    within = np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n)
+    src = args["entries_offset"].astype(np.int64)[idx_item] + within
+    dst = start[idx_item] + within
+    buf[dst] = log_term[src]
+    a2["entries_offset"] = np.where(ok, start, 0)
+    return a2, buf
+
+
+def results_of(slots, peers, args, rep, herr, G, P):
+    """AE_RESULT records for the replies of the handled items, one segment per
+    leader slot (ascending slot, peer order kept), and the segment boundaries."""
+    ok = herr == 0
+    res = np.zeros(int(ok.sum()), dtype=AE_RESULT)
+    res["slot"], res["peer"] = slots[ok], peers[ok]
+    res["args_term"], res["args_prev_log_index"] = args["term"][ok], args["prev_log_index"][ok]
+    res["args_n_entries"] = args["n_entries"][ok]
+    res["reply_term"], res["reply_success"] = rep["term"][ok], rep["success"][ok]
+    res["reply_conflict_index"] = rep["conflict_index"][ok]
+    order = np.argsort(res["slot"], kind="stable")
+    res = res[order]
+    cut = np.nonzero(np.diff(res["slot"]))[0] + 1
+    seg = np.concatenate([[0], cut, [len(res)]]).astype(np.int64)
+    return res, seg
+
+
+def stale_second_leader_state(st, lp, G, P, L, rng, groups):
+    """Make a second, stale leader in each of `groups`: replica q != lp[g]
+    becomes Leader one term below the real leader, with a log that diverges
+    from the real leader's after index d and nextIndex pointing into it. The
+    batch [lp -> q, q -> r] then has q's row both written (by the first item)
+    and read as entries (by the second)."""
+    st = {k: v.copy() for k, v in st.items()}
+    pairs = []
+    for g in groups:
+        l = int(lp[g])
+        q = (l + 1) % P
+        r = (l + 2) % P
+        ls, qs = g * P + l, g * P + q
+        T = int(st["current_term"][ls])
+        st["state"][qs] = LEADER
+        st["current_term"][qs] = max(1, T - 1)
+        st["dummy_index"][qs] = 0
+        llast = int(st["last_index"][ls])
+        qlast = min(L - 1, max(4, llast))
+        lrow = st["log_term"][ls * L:(ls + 1) * L]
+        qrow = st["log_term"][qs * L:(qs + 1) * L]
+        d = int(rng.integers(1, max(2, min(qlast, llast) - 1)))
+        lrow[d + 1:llast + 1] = T             # the real leader's entries past d: its own term
+        qrow[:d + 1] = lrow[:d + 1]
+        qrow[d + 1:qlast + 1] = max(1, T - 1)  # q's diverging tail
+        st["last_index"][qs] = qlast
+        st["commit_index"][qs] = min(int(st["commit_index"][qs]), d)
+        st["last_applied"][qs] = min(int(st["last_applied"][qs]), int(st["commit_index"][qs]))
+        # the real leader's view of q: probe at a point inside the common prefix
+        st["next_index"][ls * P + q] = int(rng.integers(1, d + 1))
+        # the stale leader's view of r
+        st["next_index"][qs * P + r] = int(rng.integers(1, qlast + 1))
+        pairs.append((ls, q))
+        pairs.append((qs, r))
+    slots = np.array([s for s, _ in pairs], np.int32)
+    peers = np.array([p for _, p in pairs], np.int32)
+    return st, slots, peers

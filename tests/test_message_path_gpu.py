@@ -1,0 +1,100 @@
+"""Message-level parity on the GPU (the entry points a host calls for
+network-delivered batches, include/mraft.h): gather (a3,
+raft_append_entry.go:20-54) -> HandleAppendEntries (a4, :108-162) ->
+processAppendEntriesReply + advanceCommitIndexForLeader (a2 + a1, :66-105),
+against the CPU oracle, bit for bit: replies, error codes, flags and the full
+state — at BASELINE config #3 size, with external entry buffers at aligned and
+misaligned offsets and tails of thousands of entries, and with entries by
+reference into the engine's own log, including batches that rewrite a row
+another of their items reads."""
+import numpy as np
+import pytest
+
+from message_cases import all_follower_items, external_entries, results_of, stale_second_leader_state
+from oracle_lib import Oracle, assert_states_equal
+
+from multiraft_amd import Engine, synth_seed, synth_tick_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _big_equal(a, b, G, P, L, ctx, rows=8192):
+    for k in a:
+        if k != "log_term":
+            assert np.array_equal(a[k], b[k]), f"{ctx}: {k}"
+    la, lb = a["log_term"].reshape(G * P, L), b["log_term"].reshape(G * P, L)
+    live = a["last_index"] - a["dummy_index"]
+    col = np.arange(L)[None, :]
+    for r0 in range(0, G * P, rows):
+        m = col <= live[r0:r0 + rows, None]
+        assert np.array_equal(np.where(m, la[r0:r0 + rows], 0), np.where(m, lb[r0:r0 + rows], 0)), \
+            f"{ctx}: log rows {r0}..{r0 + rows}"
+
+
+def _message_round(e, o, st, slots, peers, G, P, L, mode, equal):
+    args, gerr = e.gather_append_args(slots, peers)
+    oargs, ogerr = o.gather_append_args(slots, peers)
+    assert np.array_equal(gerr, ogerr) and np.array_equal(args, oargs)
+    ok = gerr == 0
+    if mode == "reference":
+        rep, herr = e.handle_append_entries(args, None)
+        orep, oherr = o.handle_append_entries(args, None)
+    else:
+        a2, buf = external_entries(args, ok, st["log_term"], misalign=(mode == "misaligned"))
+        a2 = a2[ok]
+        rep, herr = e.handle_append_entries(a2, buf)
+        orep, oherr = o.handle_append_entries(a2, buf)
+        args, slots, peers = args[ok], slots[ok], peers[ok]
+    assert np.array_equal(herr, oherr), f"{mode}: handle errors"
+    assert np.array_equal(rep, orep), f"{mode}: replies"
+    equal(e.store_state(), o.state(), G, P, L, f"{mode}: after handle")
+    res, seg = results_of(slots, peers, args, rep, herr, G, P)
+    f, ferr = e.process_append_replies(res, seg)
+    of, oferr = o.process_append_replies(res, seg)
+    assert np.array_equal(ferr, oferr) and np.array_equal(f, of), f"{mode}: fold"
+    equal(e.store_state(), o.state(), G, P, L, f"{mode}: after fold")
+    return rep, herr
+
+
+@pytest.mark.parametrize("mode", ["aligned", "misaligned", "reference"])
+def test_message_path_full_config3_gpu(mode):
+    """65,536 groups x 5 peers x 4,096-entry logs (the bench workload): all
+    262,144 AppendEntries of one round through gather -> handle -> fold."""
+    G, P, L = 65536, 5, 4096
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
+    slots, peers = all_follower_items(lp, G, P)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        rep, herr = _message_round(e, o, st, slots, peers, G, P, L, mode, _big_equal)
+        n_ent = e.gather_append_args(slots, peers)[0]["n_entries"]
+    # the round exercised long tails and every outcome
+    assert int(n_ent.max()) > 3000
+    assert (rep["success"] == 1).sum() > 50000 and (rep["success"] == 0).sum() > 50000
+
+
+@pytest.mark.parametrize("mode", ["aligned", "misaligned", "reference"])
+def test_handle_long_batches_gpu(mode):
+    """Thousand-entry tails into full-size rows at a small G (the pipelined
+    copy loop over an external buffer runs many iterations; uneven ends)."""
+    G, P, L = 96, 5, 4096
+    st, lp, _ = synth_tick_state(G, P, L, seed=123)
+    slots, peers = all_follower_items(lp, G, P)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        _message_round(e, o, st, slots, peers, G, P, L, mode, assert_states_equal)
+
+
+def test_stale_second_leader_by_reference_gpu():
+    """Entries by reference (entry_terms NULL) in a batch that rewrites a row
+    another of its items reads (lp -> q and q -> r, q a stale leader): the
+    engine stages those entries as the reference's gather-time copy would."""
+    G, P, L = 256, 5, 128
+    rng = np.random.default_rng(17)
+    st, lp, _ = synth_tick_state(G, P, L, seed=92)
+    st, slots, peers = stale_second_leader_state(st, lp, G, P, L, rng, range(0, G, 2))
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        _message_round(e, o, st, slots, peers, G, P, L, "reference", assert_states_equal)

@@ -414,3 +414,29 @@ def test_election_rounds_mt_equals_st():
     a, b = Oracle(G, P, L, st), Oracle(G, P, L, st)
     assert np.array_equal(a.election_rounds(mask), b.election_rounds(mask, nthreads=6))
     assert_states_equal(a.state(), b.state(), G, P, L, "election mt")
+
+
+def test_handle_by_reference_stages_entries():
+    """Entries by reference into the engine's log (entry_terms NULL): every
+    item sees the log as it was when the batch was gathered (appendOneRound
+    copies args.Entries, raft_append_entry.go:50-54), also when another item
+    of the batch rewrites its source row (a stale second leader: lp -> q and
+    q -> r in one batch)."""
+    from message_cases import external_entries, stale_second_leader_state
+    G, P, L = 48, 5, 64
+    rng = np.random.default_rng(5)
+    st, lp, _ = synth_tick_state(G, P, L, seed=91)
+    st, slots, peers = stale_second_leader_state(st, lp, G, P, L, rng, range(0, G, 3))
+    a = Oracle(G, P, L, st)
+    b = Oracle(G, P, L, st)
+    args, gerr = a.gather_append_args(slots, peers)
+    assert (gerr == 0).all()
+    rep, herr = a.handle_append_entries(args, None)
+    a2, buf = external_entries(args, gerr == 0, st["log_term"], misalign=False)
+    rep2, herr2 = b.handle_append_entries(a2, buf)
+    assert np.array_equal(herr, herr2) and np.array_equal(rep, rep2)
+    assert_states_equal(a.state(), b.state(), G, P, L, "staged vs copied entries")
+    # the batch does rewrite rows it also reads: q's row changed under lp -> q
+    q_rows = slots[1::2]
+    assert not np.array_equal(a.state()["log_term"].reshape(G * P, L)[q_rows],
+                              st["log_term"].reshape(G * P, L)[q_rows])

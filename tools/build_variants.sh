@@ -17,7 +17,8 @@ for spec in "$@"; do
   g++ -O3 -std=c++17 -fPIC -c mraft_persist.cpp -o build_$tag/mraft_persist.o &
   g++ -O3 -std=c++17 -fPIC -c mraft_router.cpp -o build_$tag/mraft_router.o &
   wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o \
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   rm -rf build_$tag
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
       $defs -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
