@@ -36,8 +36,12 @@
  * Data model: G groups x P peers = G*P replica slots,
  * slot = group*P + peer ("me" of a slot is its peer index). Per slot the Raft
  * struct fields of raft.go:16-40 are stored struct-of-arrays; the log is a
- * fixed-capacity array of L terms per slot with slot 0 holding the dummy entry
- * (raft_log.go:3-12): entry with Index i lives at log[slot*L + (i - dummy)].
+ * ring of L terms per slot whose dummy entry (logs[0], raft_log.go:3-12) sits
+ * at log_head: entry with Index i lives at
+ *   log[slot*L + (log_head + i - dummy) mod L],   dummy <= i <= last,
+ * so Snapshot / InstallSnapshot's sliceFrom (raft_snapshot.go:10,40;
+ * raft_log.go:18-21,75-77) are O(1) rebases of log_head and dummyIndex, and a
+ * replica holds at most L live entries (last - dummy + 1 <= L).
  * Commands never cross the boundary; they stay index-aligned on the host.
  */
 #ifndef MRAFT_H
@@ -121,11 +125,16 @@ typedef struct {
   int32_t *dummy_index;   /* logs[0].Index (snapshot base), raft_log.go:33  */
   int32_t *last_index;    /* logs[len-1].Index, raft_log.go:44-46           */
   int32_t *granted_votes; /* StartElection's grantedVotes closure counter   */
-  int32_t *log_term;      /* [G*P*L] log[slot*L + (Index - dummy)] = Term   */
+  int32_t *log_term;      /* [G*P*L] ring: log[slot*L + (log_head + Index -
+                             dummy) mod L] = Term                           */
   int32_t *match_index;   /* [G*P*P] matchIndex[slot*P + peer]              */
   int32_t *next_index;    /* [G*P*P] nextIndex[slot*P + peer]               */
   int32_t *persist_dirty; /* MRAFT_PERSIST_* bits: persist() call sites run
                              since the last mraft_collect_persist (below)  */
+  int32_t *log_head;      /* ring position of the dummy entry, in [0, L)    */
+  int32_t *has_snapshot;  /* hasSnapshot (raft.go:158,168-177): set by an
+                             installing HandleInstallSnapshot
+                             (raft_snapshot.go:52), consumed by the applier */
 } mraft_soa;
 
 /* Persistence (SURVEY.md §5 "Checkpoint / resume", §8f #4). The reference
@@ -287,8 +296,8 @@ int mraft_bind_state(mraft_engine *h, const mraft_soa *device_ptrs);
 
 /* a3, appendOneRound's args gather (raft_append_entry.go:20-54) for n
  * (slot, peer) pairs: fills args (entries by reference into the leader's own
- * log: entries_offset indexes the engine's log_term array, see
- * mraft_state_view) and item_err (NEED_SNAPSHOT, PREV_BEYOND_LAST, or
+ * log: entries_offset = leader slot * L + (prev + 1 - dummyIndex), the
+ * logical position of the first entry in that replica's ring) and item_err (NEED_SNAPSHOT, PREV_BEYOND_LAST, or
  * MRAFT_ITEM_BAD_STATE when the slot is not a leader — appendOneRound returns
  * without sending, :22-25). */
 int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
@@ -298,8 +307,12 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
 
 /* a4, HandleAppendEntries (raft_append_entry.go:108-162 with matchLog,
  * raft_log.go:92-96) for n items at distinct slots. entry_terms holds the
- * entries' terms (n_entry_terms words; pass NULL to read entries from the
- * engine's own log_term array, as produced by mraft_gather_append_args). */
+ * entries' terms (n_entry_terms words; pass NULL to read entries by reference
+ * from the engine's own log, as produced by mraft_gather_append_args: every
+ * item then sees the log as it was before the call, like the reference's copy
+ * of args.Entries at gather time, raft_append_entry.go:50-54; items whose
+ * source row wraps or is written by the same call are staged first, which
+ * costs one host round trip). */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,
@@ -351,21 +364,34 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts,
                 int64_t n, int32_t *out_index, int32_t *out_term,
                 int32_t *out_is_leader, int32_t *item_err, int32_t where);
 
-/* Applier (raft.go:153-203, without the snapshot message): for every slot,
- * out_from/out_to [G*P] = the ApplyMsg index range (lastApplied,
- * commitIndex] (out_from > out_to when empty), then lastApplied =
- * max(lastApplied, commitIndex) (:200). The entries' terms are in log_term;
- * the host maps indices to its commands. */
+/* Applier (raft.go:153-203): for every slot, in the order the reference
+ * sends them on applyCh,
+ *   1. when hasSnapshot is set (an InstallSnapshot installed since the last
+ *      call, raft_snapshot.go:52): the SnapshotValid message (:168-177),
+ *      out_snap_index = SnapshotIndex = dummyIndex, out_snap_term =
+ *      SnapshotTerm = dummyTerm, and hasSnapshot is cleared; otherwise
+ *      out_snap_index = -1 (the host delivers the snapshot bytes it saved);
+ *   2. the CommandValid messages of the index range (lastApplied, commitIndex]
+ *      = [out_from, out_to] (out_from > out_to when empty, :179-190), then
+ *      lastApplied = max(lastApplied, commitIndex) (:200).
+ * Arrays of G*P. out_snap_index / out_snap_term may both be NULL: no
+ * snapshot messages, hasSnapshot untouched. The entries' terms are in
+ * log_term; the host maps indices to its commands. */
 int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to,
+                        int32_t *out_snap_index, int32_t *out_snap_term,
                         int32_t where);
 
-/* Applier, compacted: only the slots with commitIndex >
- * lastApplied, in ascending slot order: out_slots[k], and their ApplyMsg
- * range (out_from[k] - 1, out_to[k]] = (lastApplied, commitIndex]. *out_n =
- * the number of such slots; the first min(*out_n, cap) are written and only
- * those advance lastApplied to commitIndex (raft.go:200), so a caller with a
- * small buffer calls again for the rest. */
+/* Applier, compacted: only the slots with a message to
+ * send — hasSnapshot set or commitIndex > lastApplied — in ascending slot
+ * order: out_slots[k]; the SnapshotValid message first when there is one
+ * (out_snap_index[k] = dummyIndex, out_snap_term[k] = dummyTerm, else -1 / 0;
+ * raft.go:168-177), then the entry range (out_from[k] - 1, out_to[k]] =
+ * (lastApplied, commitIndex] (:179-190). *out_n = the number of such slots;
+ * the first min(*out_n, cap) are written and only those clear hasSnapshot and
+ * advance lastApplied to commitIndex (:200), so a caller with a small buffer
+ * calls again for the rest. */
 int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots,
+                                int32_t *out_snap_index, int32_t *out_snap_term,
                                 int32_t *out_from, int32_t *out_to,
                                 int64_t cap, int64_t *out_n, int32_t where);
 

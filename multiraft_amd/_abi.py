@@ -43,7 +43,7 @@ _P32 = ctypes.POINTER(ctypes.c_int32)
 
 STATE_FIELDS = ("current_term", "voted_for", "state", "commit_index", "last_applied",
                 "dummy_index", "last_index", "granted_votes", "log_term", "match_index",
-                "next_index", "persist_dirty")
+                "next_index", "persist_dirty", "log_head", "has_snapshot")
 
 
 class MraftSoa(ctypes.Structure):
@@ -116,7 +116,7 @@ _SIGS = {
     "mraft_replicate_tick": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_replicate_tick_count": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
     "mraft_start": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32]),
-    "mraft_collect_apply": (ctypes.c_int, [_vp, _vp, _vp, _i32]),
+    "mraft_collect_apply": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32]),
     "mraft_election_rounds": (ctypes.c_int, [_vp, _vp, _i32, _vp, _i32]),
     "mraft_snapshot": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i32]),
     "mraft_gather_install_snapshot_args": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _i32]),
@@ -133,7 +133,7 @@ _SIGS = {
     "mraft_decode_persistent": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64]),
     "mraft_key2shard": (ctypes.c_int, [ctypes.c_char_p, _i64, _i32]),
     "mraft_replicate_tick_export": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i32]),
-    "mraft_collect_apply_compact": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i32]),
+    "mraft_collect_apply_compact": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i32]),
     "mraft_realloc_gid": (ctypes.c_int, [_vp, _i32, _vp, _i32]),
     "mraft_comm_unique_id": (ctypes.c_int, [_vp]),
     "mraft_comm_init": (ctypes.c_int, [_vp, _i32, _i32, _vp, ctypes.POINTER(_vp)]),

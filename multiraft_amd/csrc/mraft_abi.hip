@@ -61,6 +61,7 @@ mraft::Dev dev_of(const mraft_engine *h) {
   d.commit = h->dev.commit_index; d.applied = h->dev.last_applied; d.dummy = h->dev.dummy_index;
   d.last = h->dev.last_index; d.votes = h->dev.granted_votes; d.log = h->dev.log_term;
   d.match = h->dev.match_index; d.next = h->dev.next_index; d.pdirty = h->dev.persist_dirty;
+  d.head = h->dev.log_head; d.hsnap = h->dev.has_snapshot;
   d.G = h->G; d.P = h->P; d.L = h->L;
   return d;
 }
@@ -71,7 +72,8 @@ const ArrDesc kArrays[] = {
     {&mraft_soa::current_term, 0}, {&mraft_soa::voted_for, 0},   {&mraft_soa::state, 0},
     {&mraft_soa::commit_index, 0}, {&mraft_soa::last_applied, 0}, {&mraft_soa::dummy_index, 0},
     {&mraft_soa::last_index, 0},   {&mraft_soa::granted_votes, 0}, {&mraft_soa::log_term, 1},
-    {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2},  {&mraft_soa::persist_dirty, 0}};
+    {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2},  {&mraft_soa::persist_dirty, 0},
+    {&mraft_soa::log_head, 0},     {&mraft_soa::has_snapshot, 0}};
 
 size_t arr_bytes(const mraft_engine *h, int kind) {
   int64_t gp = gp_of(h);
@@ -403,15 +405,16 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   void *soff = nullptr, *stage = nullptr;
   int64_t n_stage = 0;
   if (!en) {
-    // Entries by reference into the engine's log: stage those whose source
-    // row this batch also writes (the reference's copy at gather time,
-    // raft_append_entry.go:50-54). Sizing the staging buffer costs one host
+    // Entries by reference into the engine's log: stage those whose range
+    // wraps around the source ring or whose source row this batch also
+    // writes (the reference's copy at gather time, raft_append_entry.go:50-54);
+    // the rest are read in place. Sizing the staging buffer costs one host
     // round trip on this path.
     void *tot;
     TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
     TRY(scratch(h, 15, sizeof(unsigned long long), &tot));
     HIP_TRY(hipMemsetAsync(tot, 0, sizeof(unsigned long long), h->stream));
-    mraft::launch_ae_stage_plan((const mraft_ae_args *)a, n, src_n, h->L, h->claim, h->epoch,
+    mraft::launch_ae_stage_plan((const mraft_ae_args *)a, n, src_n, h->L, h->dev.log_head, h->claim, h->epoch,
                                 (const int32_t *)e, (int64_t *)soff, (unsigned long long *)tot, h->stream);
     unsigned long long ht = 0;
     HIP_TRY(hipMemcpyAsync(&ht, tot, sizeof ht, hipMemcpyDeviceToHost, h->stream));
@@ -419,8 +422,8 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
     if (ht > 0) {
       n_stage = (int64_t)ht;
       TRY(scratch(h, 16, sizeof(int32_t) * (size_t)ht, &stage));
-      mraft::launch_ae_stage_copy(h->dev.log_term, (const mraft_ae_args *)a, n, (const int64_t *)soff,
-                                  (int32_t *)stage, h->stream);
+      mraft::launch_ae_stage_copy(h->dev.log_term, h->dev.log_head, h->L, (const mraft_ae_args *)a, n,
+                                  (const int64_t *)soff, (int32_t *)stage, h->stream);
     }
   }
   mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
@@ -480,33 +483,41 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts, in
   return sg.finish();
 }
 
-int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int32_t where) {
+int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int32_t *out_snap_index,
+                        int32_t *out_snap_term, int32_t where) {
   TRY(check(h));
   if (!out_from || !out_to) return fail(MRAFT_E_INVAL, "null argument");
+  if (!out_snap_index != !out_snap_term) return fail(MRAFT_E_INVAL, "snapshot outputs: both or neither");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
-  void *f, *t;
+  void *f, *t, *si, *st;
   TRY(sg.map(out_from, sizeof(int32_t) * gp_of(h), false, true, &f));
   TRY(sg.map(out_to, sizeof(int32_t) * gp_of(h), false, true, &t));
-  mraft::launch_collect_apply(dev_of(h), (int32_t *)f, (int32_t *)t, h->stream);
+  TRY(sg.map(out_snap_index, sizeof(int32_t) * gp_of(h), false, true, &si));
+  TRY(sg.map(out_snap_term, sizeof(int32_t) * gp_of(h), false, true, &st));
+  mraft::launch_collect_apply(dev_of(h), (int32_t *)f, (int32_t *)t, (int32_t *)si, (int32_t *)st, h->stream);
   return sg.finish();
 }
 
-int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *out_from,
-                                int32_t *out_to, int64_t cap, int64_t *out_n, int32_t where) {
+int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *out_snap_index,
+                                int32_t *out_snap_term, int32_t *out_from, int32_t *out_to, int64_t cap,
+                                int64_t *out_n, int32_t where) {
   TRY(check(h));
-  if (cap < 0 || !out_n || (cap > 0 && (!out_slots || !out_from || !out_to)))
+  if (cap < 0 || !out_n ||
+      (cap > 0 && (!out_slots || !out_from || !out_to || !out_snap_index || !out_snap_term)))
     return fail(MRAFT_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
-  void *sl, *f, *t, *n, *bc;
+  void *sl, *si, *stm, *f, *t, *n, *bc;
   TRY(sg.map(out_slots, sizeof(int32_t) * (size_t)cap, false, true, &sl));
+  TRY(sg.map(out_snap_index, sizeof(int32_t) * (size_t)cap, false, true, &si));
+  TRY(sg.map(out_snap_term, sizeof(int32_t) * (size_t)cap, false, true, &stm));
   TRY(sg.map(out_from, sizeof(int32_t) * (size_t)cap, false, true, &f));
   TRY(sg.map(out_to, sizeof(int32_t) * (size_t)cap, false, true, &t));
   TRY(sg.map(out_n, sizeof(int64_t), false, true, &n));
   TRY(scratch(h, 6, sizeof(int32_t) * (size_t)((gp_of(h) + 255) / 256), &bc));
-  mraft::launch_collect_apply_compact(dev_of(h), (int32_t *)bc, cap, (int32_t *)sl, (int32_t *)f,
-                                      (int32_t *)t, (int64_t *)n, h->stream);
+  mraft::launch_collect_apply_compact(dev_of(h), (int32_t *)bc, cap, (int32_t *)sl, (int32_t *)si,
+                                      (int32_t *)stm, (int32_t *)f, (int32_t *)t, (int64_t *)n, h->stream);
   return sg.finish();
 }
 

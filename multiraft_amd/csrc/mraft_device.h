@@ -26,8 +26,24 @@ struct Dev {
   int32_t *term, *voted, *role, *commit, *applied, *dummy, *last, *votes;
   int32_t *log, *match, *next;
   int32_t *pdirty;  // persist_dirty (include/mraft.h MRAFT_PERSIST_*); may be null
+  int32_t *head;    // log_head: ring position of each replica's dummy entry
+  int32_t *hsnap;   // has_snapshot (raft.go:158): set by an installing InstallSnapshot
   int32_t G, P, L;
 };
+
+// The log ring (include/mraft.h): Index i of a replica with dummy d and head h
+// lives at row + ring(i - d + h, L). Valid for arguments in [-L, 2L): live
+// entries have i - d in [0, L), and the pass's masked-out lanes stay within
+// one row length of them.
+__device__ __forceinline__ int ring(int k, int L) {
+  k = k >= L ? k - L : k;
+  return k < 0 ? k + L : k;
+}
+
+// Term of Index i of replica `slot` (dummy d, head h).
+__device__ __forceinline__ int term_at(const Dev &s, int64_t slot, int d, int h, int i) {
+  return s.log[slot * s.L + ring(i - d + h, s.L)];
+}
 
 // Records a persist() / SaveStateAndSnapshot() call site of the reference for
 // replica `slot` (one writer per slot per launch).
@@ -39,18 +55,19 @@ __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
 
 __device__ __forceinline__ int first_lane(unsigned long long m) { return __ffsll((long long)m) - 1; }
 
-// Largest idx in [lo, hi] with row[idx - base] != a, scanning downward; returns
-// lo - 1 when every term in the range equals a. Wave-uniform arguments;
-// row[lo - base] must be readable when lo <= hi (lanes past lo re-read it).
-__device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base,
-                                                 int lo, int hi, int a) {
+// Largest idx in [lo, hi] with term(idx) != a, scanning downward, in a ring
+// row whose Index `base` (the dummy) sits at `head` (row length L); returns
+// lo - 1 when every term in the range equals a. Wave-uniform arguments; the
+// term of lo must be readable when lo <= hi (lanes past lo re-read it).
+__device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base, int head,
+                                                 int L, int lo, int hi, int a) {
   const int lane = lane_id();
   for (int top = hi; top >= lo; top -= kChunk) {
     int v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int idx = top - lane - kWave * u;
-      const int w = row[max(idx, lo) - base];  // unconditional: the loads issue back to back
+      const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the loads issue back to back
       v[u] = idx >= lo ? w : a;
     }
     // Every ballot, no exit per vector (which lets the compiler sink each load
@@ -66,16 +83,16 @@ __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row
   return lo - 1;
 }
 
-// Largest idx in [lo, hi] with row[idx - base] == a; lo - 1 if none.
-__device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row, int base,
-                                                 int lo, int hi, int a) {
+// Largest idx in [lo, hi] with term(idx) == a (ring row as above); lo - 1 if none.
+__device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row, int base, int head,
+                                                 int L, int lo, int hi, int a) {
   const int lane = lane_id();
   for (int top = hi; top >= lo; top -= kChunk) {
     int v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int idx = top - lane - kWave * u;
-      const int w = row[max(idx, lo) - base];
+      const int w = row[ring(max(idx, lo) - base + head, L)];
       v[u] = idx >= lo ? w : a + 1;
     }
     int r = lo - 1;
@@ -93,15 +110,15 @@ __device__ __forceinline__ int wave_scan_down_eq(const int32_t *__restrict__ row
 // a = term(prev): the largest index in [dummy+2, prev-1] whose term differs
 // from a, else dummy + 1. The first probe reads one term per lane (64 terms:
 // most runs end there), then 256-term iterations.
-__device__ __forceinline__ int wave_conflict_scan(const int32_t *__restrict__ frow, int fdummy,
-                                                  int prev, int a) {
+__device__ __forceinline__ int wave_conflict_scan(const int32_t *__restrict__ frow, int fdummy, int fhead,
+                                                  int L, int prev, int a) {
   const int lo = fdummy + 2, hi = prev - 1;
   const int idx = hi - lane_id();
-  const int v = idx >= lo ? frow[idx - fdummy] : a;
+  const int v = idx >= lo ? frow[ring(idx - fdummy + fhead, L)] : a;
   const unsigned long long m = __ballot(v != a);
   if (m) return hi - first_lane(m);
   if (hi - 64 < lo) return fdummy + 1;
-  const int r = wave_scan_down_ne(frow, fdummy, lo, hi - 64, a);
+  const int r = wave_scan_down_ne(frow, fdummy, fhead, L, lo, hi - 64, a);
   return r < lo ? fdummy + 1 : r;
 }
 
@@ -148,24 +165,22 @@ __device__ __forceinline__ void wave_copy(const int32_t *__restrict__ E, int32_t
   }
 }
 
-// row[dst + k] = row[from + k] for k in [0, cnt), from > dst (raftLog.setLogs(
-// sliceFrom), raft_log.go:18-21,75-77): ascending chunks, every load of a chunk
-// before its stores, so the overlapping move is safe.
-__device__ __forceinline__ void wave_shift_left(int32_t *__restrict__ row, int from, int cnt,
-                                                int dst = 0) {
+// n terms of a ring row from Index `from` (dummy `base` at `head`) into dst,
+// in order: the ring unrolled (persistence read-out, staged entries).
+__device__ __forceinline__ void wave_copy_from_ring(const int32_t *__restrict__ row, int base, int head,
+                                                    int L, int from, int32_t *__restrict__ dst, int cnt) {
   const int lane = lane_id();
-  for (int base = 0; base < cnt; base += kChunk) {
+  for (int b = 0; b < cnt; b += kChunk) {
     int v[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int k = base + lane + kWave * u;
-      v[u] = k < cnt ? row[from + k] : 0;
+      const int k = b + lane + kWave * u;
+      v[u] = k < cnt ? row[ring(from + k - base + head, L)] : 0;
     }
-    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      const int k = base + lane + kWave * u;
-      if (k < cnt) row[dst + k] = v[u];
+      const int k = b + lane + kWave * u;
+      if (k < cnt) dst[k] = v[u];
     }
   }
 }

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     role = s.role[sl];
     votes = s.votes[sl];
     last = s.last[sl];
-    lterm = s.log[sl * s.L + (last - s.dummy[sl])];                    // lastEntry, raft_log.go:50-53
+    lterm = term_at(s, sl, s.dummy[sl], s.head[sl], last);             // lastEntry, raft_log.go:50-53
   }
   // The logs do not change during an election storm, so isLogUpToDate of
   // every candidate's (lastTerm, lastIndex) against this voter's

@@ -25,11 +25,11 @@ void launch_claim(const void *items, int64_t n, int stride, int slot_off, const 
 
 void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
                         mraft_ae_args *out, int32_t *err, hipStream_t st);
-void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
+void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, const int32_t *head,
                           const unsigned long long *claim, uint32_t epoch, const int32_t *err,
                           int64_t *soff, unsigned long long *total, hipStream_t st);
-void launch_ae_stage_copy(const int32_t *log, const mraft_ae_args *args, int64_t n, const int64_t *soff,
-                          int32_t *stage, hipStream_t st);
+void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
+                          const int64_t *soff, int32_t *stage, hipStream_t st);
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
                       int64_t n_ent, const int32_t *stage, int64_t n_stage, const int64_t *soff,
                       mraft_ae_reply *rep, int32_t *err, hipStream_t st);
@@ -37,9 +37,11 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
                  int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err, hipStream_t st);
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
                   int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st);
-void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t st);
+void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,
+                          hipStream_t st);
 void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t cap, int32_t *oslot,
-                                  int32_t *ofrom, int32_t *oto, int64_t *total, hipStream_t st);
+                                  int32_t *osnap_index, int32_t *osnap_term, int32_t *ofrom, int32_t *oto,
+                                  int64_t *total, hipStream_t st);
 void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,
                      int32_t *err, hipStream_t st);
 void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,

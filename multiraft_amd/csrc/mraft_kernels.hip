@@ -27,7 +27,7 @@ __global__ void k_init_state(Dev s) {
     // raft.go:53-68,79-80: Follower, term 0, votedFor -1, logs = [dummy{0,0}],
     // commitIndex = lastApplied = dummyIndex.
     s.term[i] = 0; s.voted[i] = -1; s.role[i] = kFollower; s.commit[i] = 0; s.applied[i] = 0;
-    s.dummy[i] = 0; s.last[i] = 0; s.votes[i] = 0;
+    s.dummy[i] = 0; s.last[i] = 0; s.votes[i] = 0; s.head[i] = 0; s.hsnap[i] = 0;
     if (s.pdirty) s.pdirty[i] = 0;
   }
 }
@@ -83,7 +83,7 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
   } else if (s.role[slot] != kLeader) {                                // raft_append_entry.go:22-25
     e = MRAFT_ITEM_BAD_STATE;
   } else {
-    const int dummy = s.dummy[slot], last = s.last[slot];
+    const int dummy = s.dummy[slot], last = s.last[slot], head = s.head[slot];
     const int prev = s.next[(int64_t)slot * P + peer] - 1;             // :26
     if (prev < dummy) e = MRAFT_ITEM_NEED_SNAPSHOT;                    // :27
     else if (prev > last) e = MRAFT_ITEM_PREV_BEYOND_LAST;             // :41-43
@@ -92,10 +92,10 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
       a.leader_id = slot % P;
       a.term = s.term[slot];
       a.prev_log_index = prev;
-      a.prev_log_term = s.log[(int64_t)slot * L + (prev - dummy)];     // :49
+      a.prev_log_term = s.log[(int64_t)slot * L + ring(prev - dummy + head, L)];  // :49
       a.n_entries = last - prev;                                       // :50
       a.leader_commit = s.commit[slot];                                // :51
-      a.entries_offset = (int64_t)slot * L + (prev + 1 - dummy);       // :54 (by reference)
+      a.entries_offset = (int64_t)slot * L + (prev + 1 - dummy);       // :54 (by reference: logical)
     }
   }
   out[i] = a;
@@ -112,14 +112,22 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
                         // messages share one L2 for the leader entries (another 8 %)
 #endif
 
-// Entries by reference into the engine's own log (entry_terms NULL): the
-// reference copies args.Entries when it builds the message (appendOneRound,
-// raft_append_entry.go:50-54), before any handler runs. An item whose source
-// row is also a receiving slot of this batch (a stale second leader of the
-// group; claim epoch set by k_claim) would race with that item's writes, so
-// its entries are staged first: k_ae_stage_plan assigns each such item a range
-// of the staging buffer, k_ae_stage_copy copies the pre-batch entries there.
+// Entries by reference into the engine's own log (entry_terms NULL):
+// entries_offset = source slot * L + (Index - dummy) of the first entry, a
+// logical position in that replica's ring. The reference copies args.Entries
+// when it builds the message (appendOneRound, raft_append_entry.go:50-54),
+// before any handler runs. k_ae_stage_plan decides per item:
+//   soff = -1      malformed reference (MRAFT_ITEM_BAD_SLOT);
+//   soff <= -2     read in place at log word (-soff - 2): the range is
+//                  contiguous in the ring and no item of this batch writes
+//                  the source row;
+//   soff >= 0      staged at stage[soff]: the range wraps around the ring, or
+//                  the source row is also a receiving slot of this batch (a
+//                  stale second leader of the group; claim epoch set by
+//                  k_claim) and would race with that item's writes.
+// k_ae_stage_copy then copies the staged ranges, unrolling the ring.
 __global__ void k_ae_stage_plan(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L,
+                                const int32_t *__restrict__ head,
                                 const unsigned long long *__restrict__ claim, uint32_t epoch,
                                 const int32_t *__restrict__ err, int64_t *__restrict__ soff,
                                 unsigned long long *__restrict__ total) {
@@ -127,23 +135,33 @@ __global__ void k_ae_stage_plan(const mraft_ae_args *__restrict__ args, int64_t 
   if (i >= n) return;
   const mraft_ae_args a = args[i];
   int64_t o = -1;
-  if (!err[i] && a.n_entries > 0 && a.entries_offset >= 0 && a.entries_offset + a.n_entries <= n_log) {
-    const int64_t r0 = a.entries_offset / L, r1 = (a.entries_offset + a.n_entries - 1) / L;
-    bool hit = false;
-    for (int64_t r = r0; r <= r1 && !hit; ++r) hit = (uint32_t)(claim[r] >> 32) == epoch;
-    if (hit) o = (int64_t)atomicAdd(total, (unsigned long long)a.n_entries);
+  if (!err[i] && a.n_entries >= 0 && a.entries_offset >= 0 && a.entries_offset + a.n_entries <= n_log &&
+      a.entries_offset % L + a.n_entries <= L) {
+    if (a.n_entries == 0) {
+      o = -2;
+    } else {
+      const int64_t r = a.entries_offset / L;
+      const int k0 = (int)(a.entries_offset % L);
+      const int p0 = ring(k0 + head[r], L);
+      if (p0 + a.n_entries > L || (uint32_t)(claim[r] >> 32) == epoch)
+        o = (int64_t)atomicAdd(total, (unsigned long long)a.n_entries);
+      else
+        o = -(r * L + p0) - 2;
+    }
   }
   soff[i] = o;
 }
 
-__global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const mraft_ae_args *__restrict__ args,
-                                int64_t n, const int64_t *__restrict__ soff, int32_t *__restrict__ stage) {
+__global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const int32_t *__restrict__ head, int L,
+                                const mraft_ae_args *__restrict__ args, int64_t n,
+                                const int64_t *__restrict__ soff, int32_t *__restrict__ stage) {
   const int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (i >= n) return;
   const int64_t o = soff[i];
   if (o < 0) return;
   const mraft_ae_args a = args[i];
-  wave_copy(log + a.entries_offset, stage + o, a.n_entries);
+  const int64_t r = a.entries_offset / L;
+  wave_copy_from_ring(log + r * L, 0, head[r], L, (int)(a.entries_offset % L), stage + o, a.n_entries);
 }
 
 __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
@@ -172,10 +190,16 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
                "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so));
   const int32_t *__restrict__ ent = ent0;
   int64_t n_ent = n_ent0;
-  if (so >= 0) {  // staged entries (k_ae_stage_plan)
-    ent = stage;
-    n_ent = n_stage;
-    a.entries_offset = so;
+  if (soff) {  // entries by reference: where k_ae_stage_plan put them
+    if (so >= 0) {
+      ent = stage;
+      n_ent = n_stage;
+      a.entries_offset = so;
+    } else if (so <= -2) {
+      a.entries_offset = -so - 2;
+    } else {
+      a.n_entries = -1;  // malformed reference: MRAFT_ITEM_BAD_SLOT below
+    }
   }
   if (e) {
     if (lane == 0) rep[i] = r;
@@ -188,10 +212,11 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
     return;
   }
   const int f = a.slot, prev = a.prev_log_index, nn = a.n_entries;
-  const int32_t *sa = lane == 0 ? s.term : lane == 1 ? s.dummy : lane == 2 ? s.last : s.commit;
-  const int sv = lane < 4 ? sa[f] : 0;
+  const int32_t *sa = lane == 0 ? s.term : lane == 1 ? s.dummy : lane == 2 ? s.last : lane == 3 ? s.commit : s.head;
+  const int sv = lane < 5 ? sa[f] : 0;
   const int fterm = __builtin_amdgcn_readlane(sv, 0), fdummy = __builtin_amdgcn_readlane(sv, 1),
-            flast = __builtin_amdgcn_readlane(sv, 2), fc = __builtin_amdgcn_readlane(sv, 3);
+            flast = __builtin_amdgcn_readlane(sv, 2), fc = __builtin_amdgcn_readlane(sv, 3),
+            fhead = __builtin_amdgcn_readlane(sv, 4);
   if (a.term < fterm) {                                                // :112-115
     r.term = fterm;
     if (lane == 0) { rep[i] = r; mark_persist(s, f, MRAFT_PERSIST_STATE); }  // deferred :111
@@ -204,12 +229,12 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
   if (prev < fdummy) {                                                 // :123-127
     r.term = 0; r.conflict_index = fdummy + 1;
   } else {
-    const int ftp = prev > flast ? 0 : frow[prev - fdummy];
+    const int ftp = prev > flast ? 0 : frow[ring(prev - fdummy + fhead, L)];
     if (prev > flast || ftp != a.prev_log_term) {                      // matchLog, raft_log.go:92-96
       r.term = a.term;
       if (prev > flast) r.conflict_index = flast + 1;                  // :131-133
       else if (prev > fdummy + 1)
-        r.conflict_index = wave_conflict_scan(frow, fdummy, prev, ftp);  // :136-142
+        r.conflict_index = wave_conflict_scan(frow, fdummy, fhead, L, prev, ftp);  // :136-142
       else r.conflict_index = prev;
     } else {
       // :146-155 through the streaming pass the tick uses (mraft_pass.h):
@@ -217,27 +242,28 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
       // the first mismatch; dwordx4 when entries and row are 16-B aligned
       // alike and every vector read stays inside its buffer.
       const long long eo = a.entries_offset - (long long)(prev + 1);    // entry Index x -> ent[eo + x]
-      const long long fo[1] = {(long long)f * L - fdummy};               // follower Index x -> log[fo + x]
+      const LinRow src{ent, eo};
+      const RingRow fr[1] = {RingRow{s.log, (long long)f * L, fhead - fdummy, L}};  // follower ring
       const int plo = prev + 1, phi = prev + nn, nend = prev + nn + 1;
       const int start[1] = {plo}, cend[1] = {min(phi, flast) + 1};
       const int capok[1] = {(int64_t)prev + nn - fdummy <= (int64_t)L - 1};
       int mode[1] = {M_CMP}, cfrom[1] = {0}, fullmask = 0, found = -1;
-      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)(s.log + fo[0] + plo);
+      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)fr[0].at(plo);
       const bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0 && ((ea ^ fa) & 15) == 0 &&
                        (ea & ~(uintptr_t)15) >= (uintptr_t)ent &&
                        ((uintptr_t)(ent + eo + phi) | 15) < (uintptr_t)(ent + n_ent);
       if (vec) {
         int c = plo - (int)((ea >> 2) & 31);                           // 128-B aligned chunks
         for (; c <= phi && mode[0] == M_CMP; c += 256)
-          pass_chunk<1, 1, true, false>(ent, s.log, eo, fo, start, cend, nend, mode, cfrom, capok,
-                                        fullmask, 1, 0, 0, found, c, plo, phi);
-        copy_loop<1, 1, true, false>(ent, s.log, eo, fo, mode, c, nend, phi, 1, 0, 0, found);
+          pass_chunk<1, 1, true, false>(src, fr, start, cend, nend, mode, cfrom, capok, fullmask, 1, 0, 0, found,
+                                        c, plo, phi);
+        copy_loop<1, 1, true, false>(src, fr, mode, c, nend, plo, phi, 1, 0, 0, found);
       } else {
         int c = plo;
         for (; c <= phi && mode[0] == M_CMP; c += 256)
-          pass_chunk<1, 1, false, false>(ent, s.log, eo, fo, start, cend, nend, mode, cfrom, capok,
-                                         fullmask, 1, 0, 0, found, c, plo, phi);
-        copy_loop<1, 1, false, false>(ent, s.log, eo, fo, mode, c, nend, phi, 1, 0, 0, found);
+          pass_chunk<1, 1, false, false>(src, fr, start, cend, nend, mode, cfrom, capok, fullmask, 1, 0, 0, found,
+                                         c, plo, phi);
+        copy_loop<1, 1, false, false>(src, fr, mode, c, nend, plo, phi, 1, 0, 0, found);
       }
       int last_after = flast;
       if (fullmask) {
@@ -316,15 +342,15 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 // Highest idx in [lo, hi] with row[idx - base] == a, or lo - 1: the a1 scan
 // of the reply fold, 64·U terms per round trip (wave-uniform arguments).
 template <int U>
-__device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row, int base, int lo, int hi,
-                                                 int a) {
+__device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row, int base, int head, int L,
+                                                 int lo, int hi, int a) {
   const int lane = lane_id();
   for (int top = hi; top >= lo; top -= kWave * U) {
     int v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = top - lane - kWave * u;
-      const int w = row[max(idx, lo) - base];  // unconditional: the U loads issue back to back
+      const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the U loads issue back to back
       v[u] = idx >= lo ? w : a + 1;
     }
     // Every ballot of the iteration (no early exit: an exit per vector lets
@@ -381,10 +407,12 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   else if (lane == 18) src = s.commit;
   else if (lane == 19) src = s.last;
   else if (lane == 20) src = s.dummy;
+  else if (lane == 21) src = s.head;
   const int vs = (src && !bad) ? src[si] : 0;
   int term = __builtin_amdgcn_readlane(vs, 16), role = __builtin_amdgcn_readlane(vs, 17),
       commit = __builtin_amdgcn_readlane(vs, 18);
-  const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20);
+  const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20),
+            head = __builtin_amdgcn_readlane(vs, 21);
   FOLD_STAMP(2, term + role + commit + last + dummy);
   for (int64_t base = 0; base < cnt; base += 64) {
     const int64_t i = base + lane;
@@ -449,13 +477,13 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     int x = -1;
     if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
     if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
-    if (plo <= phi && lrow[phi - dummy] == t0) x = phi;                  // :98
+    if (plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
     unsigned long long pend = __ballot(plo < phi && x < 0);
     while (pend) {
       const int src = first_lane(pend);
       pend &= pend - 1;
       const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
-      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU>(lrow, dummy, lo, hi, t0);  // lo - 1 if none
+      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
       if (lane == src && r >= lo) x = r;
     }
     FOLD_STAMP(4, x);
@@ -510,11 +538,11 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
     if (k < 1) {
       err[i] = MRAFT_ITEM_BAD_SLOT;
     } else if (s.role[sl] == kLeader) {                                // raft.go:93-95
-      const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl];
+      const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl], h = s.head[sl];
       if ((int64_t)last + k - dummy > (int64_t)s.L - 1) {
         err[i] = MRAFT_ITEM_LOG_FULL;
       } else {
-        for (int j = 1; j <= k; ++j) s.log[(int64_t)sl * s.L + (last + j - dummy)] = t;  // :96-100
+        for (int j = 1; j <= k; ++j) s.log[(int64_t)sl * s.L + ring(last + j - dummy + h, s.L)] = t;  // :96-100
         s.last[sl] = last + k;
         mark_persist(s, sl, MRAFT_PERSIST_STATE);                      // :101
         idx = last + 1; term = t; isl = 1;                             // :103
@@ -525,10 +553,17 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
 }
 
 // ---------------------------------------------------------------- applier
-__global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__restrict__ to) {
+__global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__restrict__ to,
+                                int32_t *__restrict__ snap_index, int32_t *__restrict__ snap_term) {
   const int64_t gp = (int64_t)s.G * s.P;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < gp;
        i += (int64_t)gridDim.x * blockDim.x) {
+    if (snap_index) {                                                  // raft.go:168-177
+      const bool hs = s.hsnap[i] != 0;
+      snap_index[i] = hs ? s.dummy[i] : -1;
+      snap_term[i] = hs ? s.log[i * s.L + s.head[i]] : 0;              // dummyTerm
+      if (hs) s.hsnap[i] = 0;
+    }
     const int la = s.applied[i], ci = s.commit[i];
     from[i] = la + 1;                                                  // raft.go:179-190
     to[i] = ci;
@@ -541,7 +576,7 @@ __global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__re
 __global__ __launch_bounds__(256) void k_apply_count(Dev s, int32_t *__restrict__ bcnt) {
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const bool pend = i < gp && s.commit[i] > s.applied[i];
+  const bool pend = i < gp && (s.hsnap[i] != 0 || s.commit[i] > s.applied[i]);
   const unsigned long long m = __ballot(pend);
   __shared__ int wc[4];
   if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(m);
@@ -573,13 +608,14 @@ __global__ __launch_bounds__(1024) void k_apply_scan(int32_t *__restrict__ bcnt,
 }
 
 __global__ __launch_bounds__(256) void k_apply_emit(Dev s, const int32_t *__restrict__ boff, int64_t cap,
-                                                    int32_t *__restrict__ oslot, int32_t *__restrict__ ofrom,
+                                                    int32_t *__restrict__ oslot, int32_t *__restrict__ osi,
+                                                    int32_t *__restrict__ ost, int32_t *__restrict__ ofrom,
                                                     int32_t *__restrict__ oto) {
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int la = 0, ci = 0;
-  if (i < gp) { la = s.applied[i]; ci = s.commit[i]; }
-  const bool pend = i < gp && ci > la;
+  int la = 0, ci = 0, hs = 0;
+  if (i < gp) { la = s.applied[i]; ci = s.commit[i]; hs = s.hsnap[i]; }
+  const bool pend = i < gp && (hs != 0 || ci > la);
   const unsigned long long m = __ballot(pend);
   __shared__ int wc[4];
   if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(m);
@@ -590,31 +626,35 @@ __global__ __launch_bounds__(256) void k_apply_emit(Dev s, const int32_t *__rest
   off += __popcll(m & ((1ull << lane_id()) - 1));
   if (pend && off < cap) {
     oslot[off] = (int32_t)i;
+    osi[off] = hs ? s.dummy[i] : -1;                                   // raft.go:168-177
+    ost[off] = hs ? s.log[i * s.L + s.head[i]] : 0;                    // dummyTerm
+    if (hs) s.hsnap[i] = 0;
     ofrom[off] = la + 1;                                               // raft.go:179-190
     oto[off] = ci;
-    s.applied[i] = ci;                                                 // :200
+    if (ci > la) s.applied[i] = ci;                                    // :200
   }
 }
 
 // ---------------------------------------------------------------- snapshots
 // Snapshot (raft_snapshot.go:3-13): wave per item.
+// Snapshot: setLogs(sliceFrom(index)) (raft_snapshot.go:10, raft_log.go:18-21,
+// 75-77) is an O(1) rebase of the ring — the head moves to the entry at
+// `index`, which becomes the dummy with its own term; no term moves.
 __global__ __launch_bounds__(256) void k_snapshot(Dev s, const int32_t *__restrict__ slots,
                                                   const int32_t *__restrict__ index, int64_t n,
                                                   int32_t *__restrict__ err) {
-  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n || err[i]) return;
   const int sl = slots[i], x = index[i];
   const int d = s.dummy[sl], last = s.last[sl];
   if (x <= d) return;                                                  // :6-9
   if (x > last) {                                                      // sliceFrom panics
-    if (lane_id() == 0) err[i] = MRAFT_ITEM_PREV_BEYOND_LAST;
+    err[i] = MRAFT_ITEM_PREV_BEYOND_LAST;
     return;
   }
-  wave_shift_left(s.log + (int64_t)sl * s.L, x - d, last - x + 1);     // :10
-  if (lane_id() == 0) {
-    s.dummy[sl] = x;
-    mark_persist(s, sl, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);  // :12
-  }
+  s.head[sl] = ring(s.head[sl] + (x - d), s.L);                        // :10
+  s.dummy[sl] = x;
+  mark_persist(s, sl, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);    // :12
 }
 
 // appendOneRound's snapshot branch (raft_append_entry.go:27-34).
@@ -636,66 +676,62 @@ __global__ void k_gather_is(Dev s, const int32_t *__restrict__ slots, const int3
     a.term = s.term[slot];                                             // :29
     a.leader_id = slot % P;                                            // :30
     a.last_included_index = s.dummy[slot];                             // :31
-    a.last_included_term = s.log[(int64_t)slot * s.L];                 // :32 dummyTerm
+    a.last_included_term = s.log[(int64_t)slot * s.L + s.head[slot]];  // :32 dummyTerm
   }
   out[i] = a;
   err[i] = e;
 }
 
 // HandleInstallSnapshot (raft_snapshot.go:15-54): wave per item.
+// HandleInstallSnapshot (raft_snapshot.go:15-54), thread per item. Installing
+// by sliceFrom(LastIncludedIndex) (:38-40) is an O(1) ring rebase.
 __global__ __launch_bounds__(256) void k_handle_is(Dev s, const mraft_is_args *__restrict__ args,
                                                    int64_t n, mraft_is_reply *__restrict__ rep,
                                                    int32_t *__restrict__ flags,
                                                    int32_t *__restrict__ err) {
-  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int lane = lane_id();
   if (err[i]) {
-    if (lane == 0) { rep[i] = mraft_is_reply{0, 0}; flags[i] = 0; }
+    rep[i] = mraft_is_reply{0, 0};
+    flags[i] = 0;
     return;
   }
   const mraft_is_args a = args[i];
   const int f = a.slot, fterm = s.term[f];
   int fl = 0;
   if (a.term < fterm) {                                                // :20-22
-    if (lane == 0) { rep[i] = mraft_is_reply{fterm, 0}; flags[i] = 0; }
+    rep[i] = mraft_is_reply{fterm, 0};
+    flags[i] = 0;
     return;
   }
   const int lii = a.last_included_index;
   const int fcommit = s.commit[f];
-  int32_t *row = s.log + (int64_t)f * s.L;
   const bool install = lii > fcommit;                                  // :31-33
-  const int fd = s.dummy[f], flast = s.last[f];
+  const int fd = s.dummy[f], flast = s.last[f], fh = s.head[f];
   if (install && lii <= flast && lii < fd) {                           // sliceFrom panics
-    if (lane == 0) { rep[i] = mraft_is_reply{0, 0}; flags[i] = 0; err[i] = MRAFT_ITEM_BELOW_DUMMY; }
+    rep[i] = mraft_is_reply{0, 0};
+    flags[i] = 0;
+    err[i] = MRAFT_ITEM_BELOW_DUMMY;
     return;
   }
-  int newlast = -1;
+  if (a.term > fterm) { s.term[f] = a.term; s.voted[f] = -1; }         // :23-26
+  s.role[f] = kFollower;                                               // :28
   if (install) {
-    if (lii > flast) {                                                 // :35-37
-      newlast = lii;
-    } else {                                                           // :38-40
-      // entries (lii, flast] move to slots 1..; slot 0 takes LastIncludedTerm
-      // below (:44-45), so no lane rewrites an address another lane stored.
-      if (lii > fd) wave_shift_left(row, lii - fd + 1, flast - lii, 1);
-    }
+    // :35-37 a new log [dummy] keeps its head; :38-40 sliceFrom moves it
+    const int nh = lii > flast ? fh : ring(fh + (lii - fd), s.L);
+    s.log[(int64_t)f * s.L + nh] = a.last_included_term;               // :44-45
+    if (lii > flast) s.last[f] = lii;
+    else s.head[f] = nh;
+    s.hsnap[f] = 1;                                                    // :52 hasSnapshot
+    s.dummy[f] = lii;
+    s.commit[f] = lii;                                                 // :42
+    s.applied[f] = lii;                                                // :43
     fl = MRAFT_F_SNAPSHOT_INSTALLED;
   }
-  if (lane == 0) {
-    if (a.term > fterm) { s.term[f] = a.term; s.voted[f] = -1; }       // :23-26
-    s.role[f] = kFollower;                                             // :28
-    if (install) {
-      row[0] = a.last_included_term;                                   // :44-45
-      if (newlast >= 0) s.last[f] = newlast;
-      s.dummy[f] = lii;
-      s.commit[f] = lii;                                               // :42
-      s.applied[f] = lii;                                              // :43
-    }
-    mark_persist(s, f, (a.term > fterm ? MRAFT_PERSIST_STATE : 0) |   // :26
-                           (install ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
-    rep[i] = mraft_is_reply{a.term, 0};                                // deferred reply.Term
-    flags[i] = fl;
-  }
+  mark_persist(s, f, (a.term > fterm ? MRAFT_PERSIST_STATE : 0) |     // :26
+                         (install ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
+  rep[i] = mraft_is_reply{a.term, 0};                                  // deferred reply.Term
+  flags[i] = fl;
 }
 
 // processInstallSnapshotReply (raft_snapshot.go:56-69): lane per segment.
@@ -761,7 +797,7 @@ __global__ void k_start_election(Dev s, const int32_t *__restrict__ slots, int64
     a.term = t;
     a.candidate_id = sl % s.P;
     a.last_log_index = last;                                           // :12
-    a.last_log_term = s.log[(int64_t)sl * s.L + (last - s.dummy[sl])];  // :13
+    a.last_log_term = term_at(s, sl, s.dummy[sl], s.head[sl], last);  // :13
   }
   out[i] = a;
 }
@@ -784,7 +820,7 @@ __global__ void k_handle_rv(Dev s, const mraft_rv_args *__restrict__ args, int64
       if (a.term > term) { role = kFollower; term = a.term; voted = -1; }  // :63-66
       r.term = term;                                                   // :67
       const int mylast = s.last[v];
-      const int mylt = s.log[(int64_t)v * s.L + (mylast - s.dummy[v])];
+      const int mylt = term_at(s, v, s.dummy[v], s.head[v], mylast);
       const bool up = a.last_log_term > mylt ||                        // raft_log.go:99-104
                       (mylt == a.last_log_term && a.last_log_index >= mylast);
       if ((voted == -1 || voted == a.candidate_id) && up) {            // :69-74
@@ -889,7 +925,8 @@ __global__ __launch_bounds__(256) void k_read_persistent_terms(Dev s,
   const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   if (i >= n) return;
   const mraft_persistent r = hdr[i];
-  wave_copy(s.log + (int64_t)r.slot * s.L, out + r.terms_offset, r.last_index - r.dummy_index + 1);
+  wave_copy_from_ring(s.log + (int64_t)r.slot * s.L, r.dummy_index, s.head[r.slot], s.L, r.dummy_index,
+                      out + r.terms_offset, r.last_index - r.dummy_index + 1);
 }
 
 // Make (raft.go:51-87) + readPersist (:217-235): wave per (validated) item.
@@ -906,6 +943,8 @@ __global__ __launch_bounds__(256) void k_restore(Dev s, const mraft_persistent *
     s.voted[sl] = r.voted_for;                                         // :232
     s.role[sl] = kFollower;                                            // :58
     s.dummy[sl] = r.dummy_index;
+    s.head[sl] = 0;                                                    // a fresh raftLog
+    s.hsnap[sl] = 0;                                                   // Make: no snapshot pending
     s.last[sl] = r.last_index;
     s.commit[sl] = r.dummy_index;                                      // :79
     s.applied[sl] = r.dummy_index;                                     // :80
@@ -956,16 +995,17 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
                      out, err);
 }
 
-void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
+void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, const int32_t *head,
                           const unsigned long long *claim, uint32_t epoch, const int32_t *err,
                           int64_t *soff, unsigned long long *total, hipStream_t st) {
-  hipLaunchKernelGGL(k_ae_stage_plan, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, claim,
+  hipLaunchKernelGGL(k_ae_stage_plan, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, head, claim,
                      epoch, err, soff, total);
 }
 
-void launch_ae_stage_copy(const int32_t *log, const mraft_ae_args *args, int64_t n, const int64_t *soff,
-                          int32_t *stage, hipStream_t st) {
-  hipLaunchKernelGGL(k_ae_stage_copy, dim3(blocks_for(n, 4)), dim3(256), 0, st, log, args, n, soff, stage);
+void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
+                          const int64_t *soff, int32_t *stage, hipStream_t st) {
+  hipLaunchKernelGGL(k_ae_stage_copy, dim3(blocks_for(n, 4)), dim3(256), 0, st, log, head, L, args, n, soff,
+                     stage);
 }
 
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
@@ -1010,26 +1050,28 @@ void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int
                      ol, err);
 }
 
-void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, hipStream_t st) {
+void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,
+                          hipStream_t st) {
   int blocks = blocks_for((int64_t)s.G * s.P);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_collect_apply, dim3(blocks), dim3(kBlock), 0, st, s, from, to);
+  hipLaunchKernelGGL(k_collect_apply, dim3(blocks), dim3(kBlock), 0, st, s, from, to, snap_index, snap_term);
 }
 
 void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t cap, int32_t *oslot,
-                                  int32_t *ofrom, int32_t *oto, int64_t *total, hipStream_t st) {
+                                  int32_t *osnap_index, int32_t *osnap_term, int32_t *ofrom, int32_t *oto,
+                                  int64_t *total, hipStream_t st) {
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t nb = (gp + 255) / 256;
   hipLaunchKernelGGL(k_apply_count, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt);
   hipLaunchKernelGGL(k_apply_scan, dim3(1), dim3(1024), 0, st, scratch_bcnt, nb, total);
   hipLaunchKernelGGL(k_apply_emit, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt, cap, oslot,
-                     ofrom, oto);
+                     osnap_index, osnap_term, ofrom, oto);
 }
 
 void launch_snapshot(const Dev &s, const int32_t *slots, const int32_t *index, int64_t n,
                      int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_snapshot, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, slots, index, n, err);
+  hipLaunchKernelGGL(k_snapshot, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, index, n, err);
 }
 
 void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
@@ -1041,7 +1083,7 @@ void launch_gather_is(const Dev &s, const int32_t *slots, const int32_t *peers, 
 void launch_handle_is(const Dev &s, const mraft_is_args *args, int64_t n, mraft_is_reply *rep,
                       int32_t *flags, int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_handle_is, dim3(blocks_for(n * 64)), dim3(kBlock), 0, st, s, args, n, rep,
+  hipLaunchKernelGGL(k_handle_is, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, args, n, rep,
                      flags, err);
 }
 

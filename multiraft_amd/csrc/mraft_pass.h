@@ -13,6 +13,30 @@ namespace {
 
 enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the pass
 
+// Where the term of Index idx of a stream lives. Entries come from a
+// contiguous buffer (a network batch or staged copy: LinRow) or from the
+// leader's own ring (the fused tick: RingRow); followers are always rings
+// (include/mraft.h: row + (head + idx - dummy) mod L, base = head - dummy).
+struct LinRow {
+  const int32_t *p;
+  long long off;
+  __device__ __forceinline__ const int32_t *at(int idx) const { return p + off + idx; }
+};
+// Every lane that loads or stores in the pass holds an Index at or above the
+// row's dummy (loads and stores are masked to [plo, phi] / [start, cend) /
+// [cfrom, nend), and a dwordx4 group aligned in the ring cannot begin below
+// it), so idx + base >= 0 there and only the upper wrap is needed; masked
+// lanes may form any address, they never dereference it.
+struct RingRow {
+  int32_t *p;
+  long long row;
+  int base, L;
+  __device__ __forceinline__ int32_t *at(int idx) const {
+    const int k = idx + base;
+    return p + row + (k >= L ? k - L : k);
+  }
+};
+
 #ifndef MRAFT_COPY_PIPE
 #define MRAFT_COPY_PIPE 1  // software-pipelined copy-only loop (0: the plain loop, for A/B runs)
 #endif
@@ -56,12 +80,10 @@ __device__ __forceinline__ void st1(int32_t *p, int a) {
 // into it; and (2) the exact commit scan: the largest index in [slo, shi]
 // whose term equals T (kept in `found`, the pass ascends).
 // VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
-// otherwise lane j owns c+64(4v+u)+j. Leader entry idx is log[eo + idx],
-// follower q's is log[fo[q] + idx].
-template <int NI, int V, bool VEC, bool COUNT>
-__device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int32_t *__restrict__ log,
-                                           long long eo,
-                                           const long long (&fo)[NI], const int (&start)[NI],
+// otherwise lane j owns c+64(4v+u)+j. Entry idx is at src.at(idx), follower
+// q's term of Index idx at fr[q].at(idx).
+template <int NI, int V, bool VEC, bool COUNT, class Src>
+__device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[NI], const int (&start)[NI],
                                            const int (&cend)[NI], int nend, int (&mode)[NI],
                                            int (&cfrom)[NI], const int (&capok)[NI],
                                            int &fullmask, int slo, int shi, int T, int &found,
@@ -79,11 +101,11 @@ __device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int3
   for (int v = 0; v < V; ++v) {
     if (VEC) {
       int4 x = make_int4(0, 0, 0, 0);
-      if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(src + eo + idx[v][0]);
+      if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(src.at(idx[v][0]));
       e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src + eo + idx[v][u]) : 0;
+      for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src.at(idx[v][u])) : 0;
     }
   }
   int f[NI][V][4];
@@ -98,13 +120,13 @@ __device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int3
     for (int v = 0; v < V; ++v) {
       if (VEC) {
         if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
-          const int4 x = ld4(log + fo[q] + idx[v][0]);
+          const int4 x = ld4(fr[q].at(idx[v][0]));
           f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
         }
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(log + fo[q] + idx[v][u]);
+          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(fr[q].at(idx[v][u]));
       }
     }
   }
@@ -187,11 +209,11 @@ __device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int3
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
-            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
+            st4(fr[q].at(idx[v][0]), e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
+              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(fr[q].at(idx[v][u]), e[v][u]);
           }
         }
       }
@@ -204,11 +226,9 @@ __device__ __forceinline__ void pass_chunk(const int32_t *__restrict__ src, int3
 // follower in M_COPY receives the leader's entries [c, nend) (its copy start
 // is already behind c), VC dwordx4 loads per lane in flight per iteration,
 // and the commit scan [slo, shi] continues on the same loads.
-template <int NI, int VC, bool VEC, bool COUNT>
-__device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32_t *__restrict__ log,
-                                          long long eo,
-                                          const long long (&fo)[NI], const int (&mode)[NI], int c,
-                                          int nend, int phi, int slo, int shi, int T, int &found) {
+template <int NI, int VC, bool VEC, bool COUNT, class Src>
+__device__ __forceinline__ void copy_loop(const Src &src, const RingRow (&fr)[NI], const int (&mode)[NI], int c,
+                                          int nend, int plo, int phi, int slo, int shi, int T, int &found) {
   constexpr int CW = 256 * VC;
   const int lane = lane_id();
   int cmask = 0;
@@ -222,14 +242,14 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
     // loop will run for it (same exit rule as below): no extra traffic.
     if (c > phi || (!cmask && !(slo <= shi && c <= shi))) return;
     int4 cur = make_int4(0, 0, 0, 0);
-    if (c + 4 * lane <= phi) cur = ld4(src + eo + c + 4 * lane);
+    if (c + 4 * lane + 3 >= plo && c + 4 * lane <= phi) cur = ld4(src.at(c + 4 * lane));
     for (;;) {
       const int i0 = c + 4 * lane;
       const int cmask_n = c + CW >= nend ? 0 : cmask;
       const int cn = c + CW;
       const bool more = cn <= phi && (cmask_n || (slo <= shi && cn <= shi));
       int4 nxt = make_int4(0, 0, 0, 0);
-      if (more && cn + 4 * lane <= phi) nxt = ld4(src + eo + cn + 4 * lane);
+      if (more && cn + 4 * lane <= phi) nxt = ld4(src.at(cn + 4 * lane));
       if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
         const int e[4] = {cur.x, cur.y, cur.z, cur.w};
         int lu = -1;
@@ -247,12 +267,12 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
         for (int q = 0; q < NI; ++q) {
           if (!((cmask >> q) & 1)) continue;
           if (i0 + 3 < nend) {
-            st4(log + fo[q] + i0, cur.x, cur.y, cur.z, cur.w);
+            st4(fr[q].at(i0), cur.x, cur.y, cur.z, cur.w);
           } else {
             const int e[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (i0 + u < nend) st1(log + fo[q] + i0 + u, e[u]);
+              if (i0 + u < nend) st1(fr[q].at(i0 + u), e[u]);
           }
         }
       }
@@ -275,11 +295,11 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
     for (int v = 0; v < VC; ++v) {
       if (VEC) {
         int4 x = make_int4(0, 0, 0, 0);
-        if (idx[v][0] <= phi) x = ld4(src + eo + idx[v][0]);
+        if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(src.at(idx[v][0]));
         e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
       } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[v][u] = idx[v][u] <= phi ? ld1(src + eo + idx[v][u]) : 0;
+        for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src.at(idx[v][u])) : 0;
       }
     }
     if (scan) {
@@ -316,11 +336,11 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
 #pragma unroll
         for (int v = 0; v < VC; ++v) {
           if (VEC && idx[v][3] < nend) {
-            st4(log + fo[q] + idx[v][0], e[v][0], e[v][1], e[v][2], e[v][3]);
+            st4(fr[q].at(idx[v][0]), e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[v][u] < nend) st1(log + fo[q] + idx[v][u], e[v][u]);
+              if (idx[v][u] < nend) st1(fr[q].at(idx[v][u]), e[v][u]);
           }
         }
       }
@@ -340,9 +360,8 @@ __device__ __forceinline__ void copy_loop(const int32_t *__restrict__ src, int32
 // followed by copy_loop: chunk c+256 is loaded only when the loop runs for it,
 // and every load stays inside the row it streams (lanes whose 4 entries end
 // before plo / start do not load).
-template <int NI, bool COUNT>
-__device__ __forceinline__ void stream_pass(const int32_t *__restrict__ src, int32_t *__restrict__ log,
-                                            long long eo, const long long (&fo)[NI],
+template <int NI, bool COUNT, class Src>
+__device__ __forceinline__ void stream_pass(const Src &src, const RingRow (&fr)[NI],
                                             const int (&start)[NI], const int (&cend)[NI], int nend,
                                             int (&mode)[NI], int (&cfrom)[NI], const int (&capok)[NI],
                                             int &fullmask, int slo, int shi, int T, int &found, int c,
@@ -359,14 +378,14 @@ __device__ __forceinline__ void stream_pass(const int32_t *__restrict__ src, int
   auto load_leader = [&](int cc) {
     const int i0 = cc + 4 * lane;
     int4 x = make_int4(0, 0, 0, 0);
-    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src + eo + i0);
+    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src.at(i0));
     return x;
   };
   auto load_follower = [&](int q, int cc) {
     const int i0 = cc + 4 * lane;
     int4 x = make_int4(0, 0, 0, 0);
     if (mode[q] == M_CMP && start[q] <= cc + CW - 1 && cend[q] > cc && i0 + 3 >= start[q] && i0 < cend[q])
-      x = ld4(log + fo[q] + i0);
+      x = ld4(fr[q].at(i0));
     return x;
   };
   if (!runs(c)) return;
@@ -443,11 +462,11 @@ __device__ __forceinline__ void stream_pass(const int32_t *__restrict__ src, int
       for (int q = 0; q < NI; ++q) {
         if (!((cmask >> q) & 1)) continue;
         if (i0 >= cfrom[q] && i0 + 3 < nend) {
-          st4(log + fo[q] + i0, e.x, e.y, e.z, e.w);
+          st4(fr[q].at(i0), e.x, e.y, e.z, e.w);
         } else {
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (i0 + u >= cfrom[q] && i0 + u < nend) st1(log + fo[q] + i0 + u, ev[u]);
+            if (i0 + u >= cfrom[q] && i0 + u < nend) st1(fr[q].at(i0 + u), ev[u]);
         }
       }
     }

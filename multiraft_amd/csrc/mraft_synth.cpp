@@ -143,6 +143,9 @@ void gen_group(uint64_t seed, int32_t g, int32_t gl, int32_t P, int32_t L,
   st->commit_index[ld] = lcommit;
   st->last_applied[ld] = lcommit;
   st->dummy_index[ld] = 0;
+  if (st->log_head) st->log_head[ld] = 0;
+  if (st->has_snapshot)
+    for (int32_t p = 0; p < P; ++p) st->has_snapshot[sb + p] = 0;
   st->last_index[ld] = last;
   st->granted_votes[ld] = 0;
   if (st->persist_dirty)
@@ -156,6 +159,7 @@ void gen_group(uint64_t seed, int32_t g, int32_t gl, int32_t P, int32_t L,
     st->voted_for[f] = rng.below(2) ? lp : -1;
     st->state[f] = (c == MRAFT_SYN_STALE && rng.below(2)) ? MRAFT_CANDIDATE : MRAFT_FOLLOWER;
     st->dummy_index[f] = fdummies[p];
+    if (st->log_head) st->log_head[f] = 0;
     st->last_index[f] = flasts[p];
     const int32_t fc = rng.range(fdummies[p], std::max(fdummies[p], std::min(flasts[p], lcommit)));
     st->commit_index[f] = fc;
@@ -258,6 +262,8 @@ extern "C" int mraft_synth_election_state(uint64_t seed, int32_t G, int32_t P, i
         st->granted_votes[s] = 0;
         if (st->persist_dirty) st->persist_dirty[s] = 0;
         st->dummy_index[s] = 0;
+        if (st->log_head) st->log_head[s] = 0;
+        if (st->has_snapshot) st->has_snapshot[s] = 0;
         int32_t last = B + (int32_t)rng.below(5) - 2;
         last = std::max(1, std::min(L - 1, last));
         st->last_index[s] = last;

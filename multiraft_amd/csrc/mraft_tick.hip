@@ -83,39 +83,45 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Reply fold of one group (processAppendEntriesReply, :66-88, in peer order),
-// wave-uniform. Inputs per follower slot q come from lane q.
-template <int P>
+// wave-uniform. Inputs per follower slot q come from lane q. The fold keeps
+// only what the rest of the tick needs (bit q of gate_m: the reply passed the
+// term/state/prev gate; of rs_m: it set matchIndex), so little wave-uniform
+// state stays live across the streaming pass; phase D recomputes each lane's
+// nextIndex / matchIndex from its own item. COUNT keeps the per-reply arrays
+// the algorithmic word count reads.
+template <int P, bool COUNT>
 struct Fold {
   static constexpr int NI = P - 1;
-  int term, stepped, any, mstar;
-  int gate[NI], rs[NI], rp[NI], rn[NI], rx[NI], ic[NI];
+  static constexpr int NA = COUNT ? NI : 1;
+  int term, stepped, any, mstar, gate_m, rs_m;
+  int rp[NA], ic[NA];
 
   // is_m: followers whose reply is an InstallSnapshot reply
   // (processInstallSnapshotReply, raft_snapshot.go:56-69) for
-  // LastIncludedIndex lii; rp/rn of those items read (lii, 0).
-  __device__ __forceinline__ void run(int T, int lp, int (&mm)[P], unsigned long long have_m,
-                                      unsigned long long succ_m, unsigned long long is_m, int lii,
+  // LastIncludedIndex lii; their (prev, n) read (lii, 0).
+  __device__ __forceinline__ void run(int T, int lp, int (&mm)[P], int have_m, int succ_m, int is_m, int lii,
                                       int rterm, int prev, int n, int rci, int icls) {
     term = T;
     stepped = 0;
     any = 0;
     mstar = INT32_MIN;
+    gate_m = 0;
+    rs_m = 0;
     int role = kLeader;
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       const int pq = q < lp ? q : q + 1;
-      gate[q] = 0;
-      rs[q] = (int)((succ_m >> q) & 1);
-      rp[q] = uni(__shfl(prev, q, 64));
-      rn[q] = uni(__shfl(n, q, 64));
-      rx[q] = rp[q] + 1;                                                 // nextIndex[q] (gathered)
-      ic[q] = uni(__shfl(icls, q, 64));
-      if (ic[q] >= IC_IS_STALE) {
-        rp[q] = lii;
-        rn[q] = 0;
+      int qrp = uni(__shfl(prev, q, 64)), qrn = uni(__shfl(n, q, 64));
+      const int qic = uni(__shfl(icls, q, 64));
+      if (qic >= IC_IS_STALE) {
+        qrp = lii;
+        qrn = 0;
+      }
+      if (COUNT) {
+        rp[q < NA ? q : 0] = qrp;
+        ic[q < NA ? q : 0] = qic;
       }
       const int rt = uni(__shfl(rterm, q, 64));
-      const int rc = uni(__shfl(rci, q, 64));
       if (!((have_m >> q) & 1)) continue;
       if (rt > term) {                                                   // :67-72, snapshot :59-64
         term = rt;
@@ -123,24 +129,21 @@ struct Fold {
         stepped = 1;
       } else if ((is_m >> q) & 1) {
         if (role == kLeader && T == term) {                              // snapshot :65-67
-          gate[q] = 1;
-          rs[q] = 1;
+          gate_m |= 1 << q;
+          rs_m |= 1 << q;
 #pragma unroll
           for (int j = 0; j < P; ++j)
             if (j == pq) mm[j] = lii;
-          rx[q] = lii + 1;
         }
       } else if (rt == term && role == kLeader && T == term) {           // :73-74 (prev gate holds)
-        gate[q] = 1;
-        if (rs[q]) {
+        gate_m |= 1 << q;
+        if ((succ_m >> q) & 1) {
+          rs_m |= 1 << q;
 #pragma unroll
           for (int j = 0; j < P; ++j)
-            if (j == pq) mm[j] = rp[q] + rn[q];                          // :76
-          rx[q] = rp[q] + rn[q] + 1;                                     // :77
+            if (j == pq) mm[j] = qrp + qrn;                              // :76
           mstar = max(mstar, quorum_match<P>(mm, lp));                   // :78 -> a1
           any = 1;
-        } else {
-          rx[q] = rc;                                                    // :82
         }
       }
     }
@@ -249,19 +252,21 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const long long lrow = ld * L;
   // Every load that depends only on the leader index, issued together.
   const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
-            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]);
+            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]), lhead = uni(s.head[ld]);
+  const int lb = lhead - ldummy;  // leader Index i at lrow + ring(i + lb): the log ring
   int mm[P];
 #pragma unroll
   for (int j = 0; j < P; ++j) mm[j] = uni(s.match[ld * P + j]);
   const int p = lane < lp ? lane : lane + 1;
   const long long f = (long long)g * P + p;
-  int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0;
+  int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
   if (lane < NI) {
     nxt = s.next[ld * P + p];
     fterm = s.term[f];
     fdummy = s.dummy[f];
     flast = s.last[f];
     fcommit = s.commit[f];
+    fhead = s.head[f];
   }
   long long hR = 1;  // algorithmic words of the header (wave-uniform)
   if (role != kLeader || c0 < ldummy) {
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   int icls = IC_NONE;
   const int prev = nxt - 1;                                              // :26
   if (lane < NI) icls = prev < ldummy ? IC_SNAP : (prev > last ? IC_PANIC : IC_GO);  // :27, :41
-  const unsigned long long snap_m = __ballot(icls == IC_SNAP);
+  const int snap_m = (int)__ballot(icls == IC_SNAP);  // lanes >= NI never set a bit: 32 bits suffice
   if (__ballot(icls == IC_PANIC)) {  // a3 would panic: the whole group is skipped
     if (COUNT) {
       if (lane == 0) atomicAdd(&counts[0], (unsigned long long)hR);
@@ -292,18 +297,18 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     return;
   }
   int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + (last - ldummy)]);  // speculative a1 probe
+  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + ring(last + lb, L)]);  // speculative a1 probe
   int prev_term = 0, ft = 0;
   if (icls == IC_GO && MRAFT_TICK_EXP != 3) {
-    prev_term = s.log[lrow + (prev - ldummy)];                           // :49
-    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + (prev - fdummy)];
+    prev_term = s.log[lrow + ring(prev + lb, L)];                        // :49
+    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + ring(prev - fdummy + fhead, L)];
   }
   const int n = last - prev;                                             // :50
   int rterm = 0, rsucc = 0, rci = 0;
   bool adopt = false;
   // InstallSnapshot (raft_append_entry.go:27-34 -> raft_snapshot.go:15-54),
   // LastIncludedIndex = leader dummyIndex, LastIncludedTerm = dummyTerm.
-  const int lit = snap_m ? uni(s.log[lrow]) : 0;
+  const int lit = snap_m ? uni(s.log[lrow + lhead]) : 0;
   if (icls == IC_SNAP) {
     if (T >= fterm && ldummy > fcommit && ldummy <= flast && ldummy < fdummy) {
       icls = IC_IS_PANIC;                                                // sliceFrom panics
@@ -355,15 +360,17 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       pv[q] = 0;
       if ((m >> q) & 1) {
         const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64));
-        pv[q] = s.log[sf * L + (max(sp - 1 - lane, sd + 2) - sd)];  // prev >= dummy + 2: readable
+        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
+                  sh = uni(__shfl(fhead, q, 64));
+        pv[q] = s.log[sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L)];  // prev >= dummy + 2: readable
       }
     }
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       if ((m >> q) & 1) {
         const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(ft, q, 64));
+        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(ft, q, 64)),
+                  sh = uni(__shfl(fhead, q, 64));
         const int lo = sd + 2, hi = sp - 1;
         const unsigned long long mm = __ballot(hi - lane >= lo && pv[q] != sa);
         int ci;
@@ -372,7 +379,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         } else if (hi - 64 < lo) {
           ci = sd + 1;
         } else {
-          const int r = wave_scan_down_ne(s.log + sf * L, sd, lo, hi - 64, sa);
+          const int r = wave_scan_down_ne(s.log + sf * L, sd, sh, L, lo, hi - 64, sa);
           ci = r < lo ? sd + 1 : r;
         }
         if (lane == q) {
@@ -383,30 +390,19 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
   }
 
-  if (!COUNT) {  // InstallSnapshot sliceFrom(LastIncludedIndex) (:38-40)
-    unsigned long long m = __ballot(icls == IC_IS_INSTALL && ldummy <= flast);
-    while (m) {
-      const int src = first_lane(m);
-      m &= m - 1;
-      const long long sf = (long long)g * P + (src < lp ? src : src + 1);
-      const int sd = __shfl(fdummy, src, 64), sl = __shfl(flast, src, 64);
-      if (ldummy > sd) wave_shift_left(s.log + sf * L, ldummy - sd + 1, sl - ldummy, 1);
-    }
-  }
-
   // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
-  long long fo[NI];
+  RingRow fr[NI];
   int start[NI], cend[NI], mode[NI], cfrom[NI], capok[NI];
   int mlo = last + 1, maybe_full = 0;
-  const long long eo = lrow - ldummy;
+  const RingRow lsrc{s.log, lrow, lb, L};
   bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
     const int qp = q < lp ? q : q + 1;
     const int sp = uni(__shfl(prev, q, 64)), sd = uni(__shfl(fdummy, q, 64)),
-              sl = uni(__shfl(flast, q, 64));
-    fo[q] = ((long long)g * P + qp) * L - sd;
+              sl = uni(__shfl(flast, q, 64)), sh = uni(__shfl(fhead, q, 64));
+    fr[q] = RingRow{s.log, ((long long)g * P + qp) * L, sh - sd, L};
     start[q] = sp + 1;
     cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
     cfrom[q] = 0;
@@ -414,7 +410,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     mode[q] = ((merge_m >> q) & 1) ? M_CMP : M_DONE;
     if (mode[q] == M_CMP) {
       mlo = min(mlo, start[q]);
-      vec = vec && (((fo[q] - eo) & 3) == 0);
+      vec = vec && (((fr[q].base - lb) & 3) == 0);  // 4-entry groups aligned alike in both rings
       maybe_full |= !capok[q];
     }
   }
@@ -422,17 +418,17 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // Fold before the pass when no follower can be rejected for capacity (then
   // every merge replies success whatever its mismatch point), so the exact
   // commit scan of a Figure-8 group rides along the same streaming pass.
-  Fold<P> fd;
+  Fold<P, COUNT> fd;
   int commit = c0, top = 0, slo = 1, shi = 0;
-  const unsigned long long is_m = __ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
-  const unsigned long long have0 = __ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
-  const unsigned long long succ0 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+  const int is_m = (int)__ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
+  const int have0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
+  const int succ0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
   if (!maybe_full) {
     fd.run(T, lp, mm, have0, succ0, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        const int t = top == last ? probe_last : uni(s.log[lrow + (top - ldummy)]);  // :98
+        const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
         if (t == T) commit = top;
         else { slo = c0 + 1; shi = top - 1; }
       }
@@ -444,21 +440,24 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
     constexpr int VC = MRAFT_TICK_VC;
+    // Chunks start on a 128-B line of the leader's row (physical position of
+    // plo rounded down; the ring wraps at a multiple of 4 entries, so every
+    // lane's dwordx4 stays contiguous).
+    const int c0a = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
     if (vec && MRAFT_TICK_STREAM) {
-      const int c = plo - (int)((eo + plo) & (MRAFT_TICK_ALIGN - 1));
-      stream_pass<NI, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok, fullmask, slo,
-                             shi, T, found, c, plo, phi);
+      stream_pass<NI, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi, T, found,
+                             c0a, plo, phi);
     } else if (vec) {
-      int c = plo - (int)((eo + plo) & (MRAFT_TICK_ALIGN - 1));
+      int c = c0a;
       for (; c <= phi; c += 256 * V) {
         bool cmp = false;
 #pragma unroll
         for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
         if (!cmp) break;
-        pass_chunk<NI, V, true, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
-                                       fullmask, slo, shi, T, found, c, plo, phi);
+        pass_chunk<NI, V, true, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi,
+                                       T, found, c, plo, phi);
       }
-      copy_loop<NI, VC, true, COUNT>(s.log, s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
+      copy_loop<NI, VC, true, COUNT>(lsrc, fr, mode, c, last + 1, plo, phi, slo, shi, T, found);
     } else {
       int c = plo;
       for (; c <= phi; c += 256 * V) {
@@ -466,10 +465,10 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 #pragma unroll
         for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
         if (!cmp) break;
-        pass_chunk<NI, V, false, COUNT>(s.log, s.log, eo, fo, start, cend, last + 1, mode, cfrom, capok,
-                                        fullmask, slo, shi, T, found, c, plo, phi);
+        pass_chunk<NI, V, false, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi,
+                                        T, found, c, plo, phi);
       }
-      copy_loop<NI, VC, false, COUNT>(s.log, s.log, eo, fo, mode, c, last + 1, phi, slo, shi, T, found);
+      copy_loop<NI, VC, false, COUNT>(lsrc, fr, mode, c, last + 1, plo, phi, slo, shi, T, found);
     }
   }
   TICK_STAMP(2);
@@ -484,16 +483,18 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   if (!maybe_full) {
     if (slo <= shi && found > c0) commit = found;
   } else {
-    const unsigned long long have1 = __ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
-    const unsigned long long succ1 = __ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+    const int have1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
+    const int succ1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+#pragma unroll
+    for (int j = 0; j < P; ++j) mm[j] = uni(s.match[ld * P + j]);  // re-read: not kept live across the pass
     fd.run(T, lp, mm, have1, succ1, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        if (uni(s.log[lrow + (top - ldummy)]) == T) {
+        if (uni(s.log[lrow + ring(top + lb, L)]) == T) {
           commit = top;
         } else {
-          const int i = wave_scan_down_eq(s.log + lrow, ldummy, c0 + 1, top - 1, T);
+          const int i = wave_scan_down_eq(s.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
           if (i > c0) commit = i;
         }
       }
@@ -551,9 +552,16 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       cW = (adopt ? 2 : 0) + 1;
       if (icls == IC_IS_INSTALL) {
         const bool newlog = ldummy > flast;                              // :35-37
+        // sliceFrom(LastIncludedIndex) (:38-40) is an O(1) rebase of the
+        // ring: the head moves to the entry at LastIncludedIndex, no term
+        // moves; a new log ([dummy] only, :35-37) keeps its head.
+        // (head and dummy re-read here rather than kept live across the pass)
+        const int fh = s.head[f], nh = newlog ? fh : ring(fh + (ldummy - s.dummy[f]), L);
         if (!COUNT) {
-          s.log[f * L] = lit;                                            // :44-45
+          s.log[f * L + nh] = lit;                                       // :44-45 dummy term
           if (newlog) s.last[f] = ldummy;
+          else s.head[f] = nh;
+          s.hsnap[f] = 1;                                                // raft_snapshot.go:52 hasSnapshot
           s.dummy[f] = ldummy;
           s.commit[f] = ldummy;                                          // :42
           s.applied[f] = ldummy;                                         // :43
@@ -561,11 +569,10 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         cR += 1;                                                         // last
         cW += 3;
         if (newlog) {
-          cW += 2;                                                       // log slot 0, last
+          cW += 2;                                                       // dummy term, last
         } else {
-          const long long k = (long long)flast - ldummy + 1;
-          cR += 1 + k;                                                   // dummy, sliced terms
-          cW += k;
+          cR += 1;                                                       // dummy
+          cW += 1;                                                       // dummy term
         }
       }
     }
@@ -591,19 +598,20 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       ex.put(g, commit, fd.stepped ? fd.term : T, fd.stepped ? kFollower : kLeader);
     }
     TICK_STAMP(3);
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      const int pq = q < lp ? q : q + 1;
-      if (lane == q && fd.gate[q]) {
-        s.next[ld * P + pq] = fd.rx[q];
-        if (fd.rs[q]) s.match[ld * P + pq] = fd.rp[q] + fd.rn[q];
-      }
+    // nextIndex / matchIndex of this lane's follower (:76-77, :82; snapshot
+    // :66-67): success -> prev + n (+1), failure -> ConflictIndex, snapshot
+    // -> LastIncludedIndex (+1).
+    if (lane < NI && ((fd.gate_m >> lane) & 1)) {
+      const bool isr = ((is_m >> lane) & 1) != 0, ok = ((fd.rs_m >> lane) & 1) != 0;
+      const int mv = isr ? ldummy : prev + n;
+      s.next[ld * P + p] = ok ? mv + 1 : rci;
+      if (ok) s.match[ld * P + p] = mv;
     }
   } else {
     // Leader-side words, wave-uniform.
     long long gR = hR + (fd.any ? NI : 0), gW = (fd.stepped ? 3 : 0) + (commit != c0 ? 1 : 0);
 #pragma unroll
-    for (int q = 0; q < NI; ++q) gW += fd.gate[q] ? (fd.rs[q] ? 2 : 1) : 0;
+    for (int q = 0; q < NI; ++q) gW += ((fd.gate_m >> q) & 1) ? (((fd.rs_m >> q) & 1) ? 2 : 1) : 0;
     // Leader log words: union of {prev_q} (PrevLogTerm), [prev_q+1, last]
     // (entries consumed by merges) and the commit scan [stop, top].
     long long A = (long long)last + 1;

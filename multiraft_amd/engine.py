@@ -129,6 +129,10 @@ class Engine:
 
     # ---- state -----------------------------------------------------------
     def load_state(self, st: dict, where: int = HOST):
+        if where == HOST:  # images made before the ring / hasSnapshot: head 0, no snapshot pending
+            for f in ("log_head", "has_snapshot"):
+                if f not in st:
+                    st = dict(st, **{f: np.zeros(self.G * self.P, np.int32)})
         soa = soa_of(st)
         _ck(self._lib.mraft_load_state(self._h, ctypes.byref(soa), where), "mraft_load_state")
 
@@ -227,23 +231,32 @@ class Engine:
                                   ptr(err), HOST), "mraft_start")
         return idx, term, isl, err
 
-    def collect_apply(self):
-        """Applier (raft.go:153-203): per-slot ApplyMsg index ranges (from, to]."""
+    def collect_apply(self, snapshots: bool = False):
+        """Applier (raft.go:153-203): per-slot ApplyMsg index ranges [from, to];
+        with snapshots=True also (snap_index, snap_term): the SnapshotValid
+        message each slot sends first (snap_index -1: none)."""
         gp = self.G * self.P
         fr = np.zeros(gp, np.int32)
         to = np.zeros(gp, np.int32)
-        _ck(self._lib.mraft_collect_apply(self._h, ptr(fr), ptr(to), HOST), "mraft_collect_apply")
-        return fr, to
+        si = np.zeros(gp, np.int32) if snapshots else None
+        stm = np.zeros(gp, np.int32) if snapshots else None
+        _ck(self._lib.mraft_collect_apply(self._h, ptr(fr), ptr(to), ptr(si), ptr(stm), HOST),
+            "mraft_collect_apply")
+        return (fr, to, si, stm) if snapshots else (fr, to)
 
-    def collect_apply_compact(self, cap: int | None = None):
-        """Applier, compacted: (slots, from, to, total) for the slots with
-        commitIndex > lastApplied, ascending; only the returned ones advance."""
+    def collect_apply_compact(self, cap: int | None = None, snapshots: bool = False):
+        """Applier, compacted: (slots, from, to, total) for the slots with a
+        message to send (hasSnapshot or commitIndex > lastApplied), ascending;
+        only the returned ones advance. snapshots=True returns (slots,
+        snap_index, snap_term, from, to, total)."""
         cap = self.G * self.P if cap is None else cap
-        sl, fr, to = (np.zeros(max(cap, 1), np.int32) for _ in range(3))
+        sl, si, stm, fr, to = (np.zeros(max(cap, 1), np.int32) for _ in range(5))
         n = np.zeros(1, np.int64)
-        _ck(self._lib.mraft_collect_apply_compact(self._h, ptr(sl), ptr(fr), ptr(to), cap, ptr(n), HOST),
-            "mraft_collect_apply_compact")
+        _ck(self._lib.mraft_collect_apply_compact(self._h, ptr(sl), ptr(si), ptr(stm), ptr(fr), ptr(to), cap,
+                                                  ptr(n), HOST), "mraft_collect_apply_compact")
         k = int(min(n[0], cap))
+        if snapshots:
+            return sl[:k].copy(), si[:k].copy(), stm[:k].copy(), fr[:k].copy(), to[:k].copy(), int(n[0])
         return sl[:k].copy(), fr[:k].copy(), to[:k].copy(), int(n[0])
 
     # ---- snapshots (raft_snapshot.go) -------------------------------------

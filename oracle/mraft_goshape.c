@@ -87,9 +87,10 @@ go_cluster *goshape_build(int32_t G, int32_t P, int32_t L, const mraft_soa *s) {
     r->caplogs = n > L ? n : L; r->nlogs = n;
     r->logs = (go_entry *)malloc(sizeof(go_entry) * (size_t)r->caplogs);
     memset(r->logs, 0, sizeof(go_entry) * (size_t)r->caplogs);  /* pre-fault (Go's heap is warm) */
+    const int64_t h = s->log_head ? s->log_head[i] : 0;  /* the engine's ring, include/mraft.h */
     for (int64_t k = 0; k < n; ++k) {
       r->logs[k].Index = d + k;
-      r->logs[k].Term = s->log_term[i * L + k];
+      r->logs[k].Term = s->log_term[i * L + (h + k) % L];
     }
     r->nextIndex = (int64_t *)malloc(sizeof(int64_t) * (size_t)P);
     r->matchIndex = (int64_t *)malloc(sizeof(int64_t) * (size_t)P);
@@ -111,7 +112,8 @@ void goshape_store(const go_cluster *c, const mraft_soa *s) {
     s->last_applied[i] = (int32_t)r->lastApplied;
     s->dummy_index[i] = (int32_t)r->logs[0].Index;
     s->last_index[i] = (int32_t)r->logs[r->nlogs - 1].Index;
-    for (int64_t k = 0; k < r->nlogs && k < L; ++k) s->log_term[i * L + k] = (int32_t)r->logs[k].Term;
+    const int64_t h = s->log_head ? s->log_head[i] : 0;
+    for (int64_t k = 0; k < r->nlogs && k < L; ++k) s->log_term[i * L + (h + k) % L] = (int32_t)r->logs[k].Term;
     for (int32_t j = 0; j < P; ++j) {
       s->next_index[i * P + j] = (int32_t)r->nextIndex[j];
       s->match_index[i * P + j] = (int32_t)r->matchIndex[j];
@@ -303,9 +305,10 @@ static void *go_reset_worker(void *arg) {
     r->commitIndex = s->commit_index[i]; r->lastApplied = s->last_applied[i];
     const int64_t d = s->dummy_index[i], n = (int64_t)s->last_index[i] - d + 1;
     r->nlogs = n;
+    const int64_t h = s->log_head ? s->log_head[i] : 0;
     for (int64_t k = 0; k < n; ++k) {
       r->logs[k].Index = d + k;
-      r->logs[k].Term = s->log_term[i * L + k];
+      r->logs[k].Term = s->log_term[i * L + (h + k) % L];
     }
     for (int32_t q = 0; q < P; ++q) {
       r->nextIndex[q] = s->next_index[i * P + q];

@@ -84,10 +84,25 @@ static inline void persist(ora_engine *e, int64_t s, int32_t bits) {
   if (S.persist_dirty) S.persist_dirty[s] |= bits;
 }
 
+/* Position of the entry with Index `index` in the log array: the replica's
+ * row is a ring of L terms whose dummy entry (logs[0], raft_log.go:3-12) sits
+ * at log_head; convertIndex (raft_log.go:55-60) is index - dummyIndex, taken
+ * modulo L from the head. The caller guarantees dummy <= index < dummy + L. */
+static inline int64_t lpos(const ora_engine *e, int64_t slot, int32_t index) {
+  int64_t k = (int64_t)index - S.dummy_index[slot] + S.log_head[slot];
+  if (k >= e->L) k -= e->L;
+  return slot * e->L + k;
+}
+
 /* getEntry(index).Term, raft_log.go:40-42 + convertIndex :55-60 (caller
  * guarantees index >= dummyIndex; the panic is handled by callers). */
 static inline int32_t term_at(const ora_engine *e, int64_t slot, int32_t index) {
-  return S.log_term[slot * e->L + (index - S.dummy_index[slot])];
+  return S.log_term[lpos(e, slot, index)];
+}
+
+/* n terms of slot's log from Index `index` on, in order (a ring may wrap). */
+static void copy_terms(const ora_engine *e, int64_t slot, int32_t index, int32_t n, int32_t *out) {
+  for (int32_t k = 0; k < n; ++k) out[k] = term_at(e, slot, index + k);
 }
 
 static inline int32_t imin(int32_t a, int32_t b) { return a < b ? a : b; } /* utility.go:41-46 */
@@ -148,14 +163,13 @@ int ora_gather_append_args(ora_engine *e, const int32_t *slots,
 /* a4: HandleAppendEntries, raft_append_entry.go:108-162                      */
 /* ------------------------------------------------------------------------ */
 
-/* ent = entries' terms (entry k has Index prev+1+k); ent_cnt_base = word index
- * of entry 0 in the LOG array when entries are a view of a leader log (for
- * counting), or -1. */
+/* ent = entries' terms (entry k has Index prev+1+k); cnt_src = the leader
+ * replica whose log the entries were copied from (for counting its words), or
+ * -1. */
 static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
-                             const int32_t *ent, int64_t ent_cnt_base,
+                             const int32_t *ent, int64_t cnt_src,
                              mraft_ae_reply *r, int *follower_committed) {
   const int32_t L = e->L;
-  const int64_t row = (int64_t)f * L;
   const int32_t prev = a->prev_log_index, n = a->n_entries;
   memset(r, 0, sizeof(*r)); /* reply := new(AppendEntriesReply) */
   *follower_committed = 0;
@@ -168,7 +182,7 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
     int32_t dummy = S.dummy_index[f], last = S.last_index[f];
     for (int32_t k = 0; k < n; ++k) {
       int32_t idx = prev + 1 + k;
-      if (idx > last || S.log_term[row + idx - dummy] != ent[k]) {
+      if (idx > last || term_at(e, f, idx) != ent[k]) {
         if ((int64_t)prev + n - dummy > (int64_t)L - 1) return MRAFT_ITEM_LOG_FULL;
         break;
       }
@@ -199,19 +213,19 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
   int32_t last = S.last_index[f];
   int match = 0;
   if (prev <= last) {
-    CR(A_LOG, row + prev - dummy);
-    match = (a->prev_log_term == S.log_term[row + prev - dummy]);
+    CR(A_LOG, lpos(e, f, prev));
+    match = (a->prev_log_term == term_at(e, f, prev));
   }
   if (!match) {                                                       /* :128-145 */
     r->term = S.current_term[f]; r->success = 0;
     if (prev > last) {
       r->conflict_index = last + 1;                                   /* :131-133 */
     } else {
-      int32_t abandoned = S.log_term[row + prev - dummy];             /* :137 */
+      int32_t abandoned = term_at(e, f, prev);                        /* :137 */
       int32_t index = prev;                                           /* :138 */
       while (index > dummy + 1) {                                     /* :139-141 */
-        CR(A_LOG, row + index - dummy);
-        if (S.log_term[row + index - dummy] != abandoned) break;
+        CR(A_LOG, lpos(e, f, index));
+        if (term_at(e, f, index) != abandoned) break;
         index--;
       }
       r->conflict_index = index;                                      /* :142 */
@@ -225,17 +239,17 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
     if (index - dummy >= last - dummy + 1) {                          /* convertIndex >= len */
       diff = 1;
     } else {
-      CR(A_LOG, row + index - dummy);
-      if (ent_cnt_base >= 0) CR(A_LOG, ent_cnt_base + k);
-      diff = (S.log_term[row + index - dummy] != ent[k]);
+      CR(A_LOG, lpos(e, f, index));
+      if (cnt_src >= 0) CR(A_LOG, lpos(e, cnt_src, index));
+      diff = (term_at(e, f, index) != ent[k]);
     }
     if (diff) {
       /* trunc(entry.Index) then append(args.Entries[k:]...), raft_log.go:62-75 */
       for (int32_t j = k; j < n; ++j) {
         int32_t idx = prev + 1 + j;
-        if (ent_cnt_base >= 0) CR(A_LOG, ent_cnt_base + j);
-        S.log_term[row + idx - dummy] = ent[j];
-        CW(A_LOG, row + idx - dummy);
+        if (cnt_src >= 0) CR(A_LOG, lpos(e, cnt_src, idx));
+        S.log_term[lpos(e, f, idx)] = ent[j];
+        CW(A_LOG, lpos(e, f, idx));
       }
       S.last_index[f] = prev + n;
       CW(A_LAST, f);
@@ -264,7 +278,10 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
    * args.Entries when it builds the message (appendOneRound,
    * raft_append_entry.go:50-54), before any handler runs, so every item reads
    * the log as it was before the batch — even when another item of the same
-   * batch rewrites its source row (two leaders of one group). Stage them. */
+   * batch rewrites its source row (two leaders of one group). Stage them.
+   * entries_offset is then slot * L + (Index - dummyIndex) of the first entry
+   * in the source replica's log (mraft_gather_append_args), read through its
+   * ring. */
   int32_t *staged = NULL;
   int64_t *soff = NULL;
   if (!entry_terms && n > 0) {
@@ -274,22 +291,27 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
       const mraft_ae_args *a = &args[i];
       soff[i] = -1;
       if (item_err[i] || a->n_entries < 0 || a->entries_offset < 0 ||
-          (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n))
+          (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n) ||
+          a->entries_offset % e->L + a->n_entries > e->L)
         continue;
       soff[i] = tot;
       tot += a->n_entries;
     }
     staged = (int32_t *)malloc(sizeof(int32_t) * (size_t)(tot > 0 ? tot : 1));
     for (int64_t i = 0; i < n; ++i)
-      if (soff[i] >= 0 && args[i].n_entries > 0)
-        memcpy(staged + soff[i], src + args[i].entries_offset, sizeof(int32_t) * (size_t)args[i].n_entries);
+      if (soff[i] >= 0 && args[i].n_entries > 0) {
+        const int64_t ss = args[i].entries_offset / e->L;
+        const int32_t k0 = (int32_t)(args[i].entries_offset % e->L);
+        copy_terms(e, ss, S.dummy_index[ss] + k0, args[i].n_entries, staged + soff[i]);
+      }
   }
   for (int64_t i = 0; i < n; ++i) {
     memset(&replies[i], 0, sizeof(replies[i]));
     if (item_err[i]) continue;
     const mraft_ae_args *a = &args[i];
     if (a->n_entries < 0 || a->entries_offset < 0 ||
-        (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n)) {
+        (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n) ||
+        (!entry_terms && a->entries_offset % e->L + a->n_entries > e->L)) {
       item_err[i] = MRAFT_ITEM_BAD_SLOT;
       continue;
     }
@@ -428,15 +450,10 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
 /* ------------------------------------------------------------------------ */
 
 /* raftLog.setLogs(sliceFrom(index)) (raft_log.go:18-21,75-77): keep [index,
- * last], the entry at index becomes slot 0. Marks the words it reads/writes. */
+ * last], the entry at index becomes the dummy (logs[0]). On the ring this is
+ * an index rebase: the head moves to the entry at `index`; no term moves. */
 static void slice_from(ora_engine *e, int32_t s, int32_t index) {
-  const int64_t row = (int64_t)s * e->L;
-  const int32_t d = S.dummy_index[s], last = S.last_index[s];
-  for (int32_t i = index; i <= last; ++i) {
-    CR(A_LOG, row + i - d);
-    S.log_term[row + i - index] = S.log_term[row + i - d];
-    CW(A_LOG, row + i - index);
-  }
+  S.log_head[s] = (int32_t)(lpos(e, s, index) - (int64_t)s * e->L);
   S.dummy_index[s] = index;
 }
 
@@ -470,7 +487,7 @@ static int32_t gather_is_one(ora_engine *e, int32_t slot, int32_t peer, mraft_is
   a->term = S.current_term[slot];                                     /* :29 */
   a->leader_id = slot % P;                                            /* :30 */
   a->last_included_index = S.dummy_index[slot];                       /* :31 */
-  a->last_included_term = S.log_term[(int64_t)slot * e->L];           /* :32 dummyTerm */
+  a->last_included_term = term_at(e, slot, S.dummy_index[slot]);      /* :32 dummyTerm */
   return MRAFT_ITEM_OK;
 }
 
@@ -489,7 +506,6 @@ int ora_gather_install_snapshot_args(ora_engine *e, const int32_t *slots, const 
 /* HandleInstallSnapshot, raft_snapshot.go:15-54 */
 static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, mraft_is_reply *r,
                              int *installed) {
-  const int64_t row = (int64_t)f * e->L;
   *installed = 0;
   r->success = 0;
   r->term = 0;
@@ -516,20 +532,24 @@ static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, m
   if (lii <= S.commit_index[f]) return MRAFT_ITEM_OK;                 /* :31-33 outdated */
   CR(A_LAST, f);
   if (lii > S.last_index[f]) {                                        /* :35-37 */
-    S.log_term[row] = a->last_included_term;
+    const int64_t at = (int64_t)f * e->L + S.log_head[f];             /* logs = [dummy] */
+    S.log_term[at] = a->last_included_term;
     S.last_index[f] = lii;
     S.dummy_index[f] = lii;
-    CW(A_LOG, row); CW(A_LAST, f);
+    CW(A_LOG, at); CW(A_LAST, f);
   } else {                                                            /* :38-40 */
     CR(A_DUMMY, f);
-    slice_from(e, f, lii);
-    S.log_term[row] = a->last_included_term;                          /* :45 setDummyTerm */
+    slice_from(e, f, lii);                                            /* O(1) ring rebase */
+    const int64_t at = lpos(e, f, lii);
+    S.log_term[at] = a->last_included_term;                           /* :45 setDummyTerm */
+    CW(A_LOG, at);
   }
   S.commit_index[f] = lii;                                            /* :42 */
   S.last_applied[f] = lii;                                            /* :43 */
   CW(A_DUMMY, f); CW(A_COMMIT, f); CW(A_APPLIED, f);
   persist(e, f, MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT);        /* :47 */
-  *installed = 1;                                                     /* :49-50 hasSnapshot */
+  S.has_snapshot[f] = 1;                                              /* :52 hasSnapshot */
+  *installed = 1;
   return MRAFT_ITEM_OK;
 }
 
@@ -640,7 +660,7 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
   for (int32_t p = 0; p < P; ++p) {
     if (ok[p] == 2) {                                                 /* InstallSnapshot */
       gather_is_one(e, ld, p, &isa[p]);
-      CR(A_LOG, (int64_t)ld * e->L);                                  /* dummyTerm */
+      CR(A_LOG, lpos(e, ld, S.dummy_index[ld]));                      /* dummyTerm */
       int inst = 0;
       if (handle_is_one(e, g * P + p, &isa[p], &isr[p], &inst)) {
         flags |= MRAFT_G_FOLLOWER_PANIC;                              /* message dropped */
@@ -653,13 +673,12 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
     if (!ok[p]) continue;
     gather_one(e, ld, p, &args[p]);                                   /* a3 */
     int32_t prev = args[p].prev_log_index;
-    CR(A_LOG, (int64_t)ld * e->L + prev - S.dummy_index[ld]);         /* PrevLogTerm */
+    CR(A_LOG, lpos(e, ld, prev));                                     /* PrevLogTerm */
     /* Go copies the entries into the args (raft_append_entry.go:50-54). */
-    memcpy(scratch, S.log_term + args[p].entries_offset,
-           sizeof(int32_t) * (size_t)args[p].n_entries);
+    copy_terms(e, ld, prev + 1, args[p].n_entries, scratch);
     int fc = 0;
     int32_t err = handle_ae_one(e, g * P + p, &args[p], scratch,      /* a4 */
-                                args[p].entries_offset, &rep[p], &fc);
+                                ld, &rep[p], &fc);
     if (err) { flags |= MRAFT_G_LOG_FULL; continue; }
     have[p] = 1;
     if (fc) flags |= MRAFT_G_FOLLOWER_COMMIT;
@@ -697,7 +716,7 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
       if (j != lp) CR(A_MATCH, (int64_t)ld * P + j);
     int32_t top = imin(mstar, S.last_index[ld]);
     for (int32_t i = top; i > commit0; --i) {
-      CR(A_LOG, (int64_t)ld * e->L + i - S.dummy_index[ld]);
+      CR(A_LOG, lpos(e, ld, i));
       if (term_at(e, ld, i) == term0) break;
     }
   }
@@ -768,7 +787,7 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
     int32_t last = S.last_index[s], dummy = S.dummy_index[s];
     if ((int64_t)last + k - dummy > (int64_t)e->L - 1) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
     for (int32_t j = 1; j <= k; ++j)                                  /* :96-100 */
-      S.log_term[(int64_t)s * e->L + (last + j - dummy)] = S.current_term[s];
+      S.log_term[lpos(e, s, last + j)] = S.current_term[s];
     S.last_index[s] = last + k;
     persist(e, s, MRAFT_PERSIST_STATE);                               /* :101 */
     out_index[i] = last + 1; out_term[i] = S.current_term[s]; out_is_leader[i] = 1;  /* :103 */
@@ -777,9 +796,16 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
   return MRAFT_OK;
 }
 
-int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to) {
+int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to, int32_t *out_snap_index,
+                      int32_t *out_snap_term) {
   int64_t gp = (int64_t)e->G * e->P;
   for (int64_t s = 0; s < gp; ++s) {
+    if (out_snap_index) {                                             /* :168-177 SnapshotValid first */
+      const int hs = S.has_snapshot[s] != 0;
+      out_snap_index[s] = hs ? S.dummy_index[s] : -1;                 /* SnapshotIndex = dummyIndex */
+      out_snap_term[s] = hs ? term_at(e, s, S.dummy_index[s]) : 0;    /* SnapshotTerm = dummyTerm */
+      S.has_snapshot[s] = 0;                                          /* rf.hasSnapshot = false */
+    }
     int32_t la = S.last_applied[s], ci = S.commit_index[s];
     out_from[s] = la + 1;                                             /* :179-190 */
     out_to[s] = ci;
@@ -1038,8 +1064,7 @@ int ora_read_persistent(ora_engine *e, const int32_t *slots, int64_t n, mraft_pe
   if (!out_terms || terms_cap < off) return MRAFT_E_INVAL;
   for (int64_t i = 0; i < n; ++i) {
     const int64_t cnt = (int64_t)out[i].last_index - out[i].dummy_index + 1;
-    memcpy(out_terms + out[i].terms_offset, S.log_term + (int64_t)out[i].slot * e->L,
-           sizeof(int32_t) * (size_t)cnt);
+    copy_terms(e, out[i].slot, out[i].dummy_index, (int32_t)cnt, out_terms + out[i].terms_offset);
   }
   return MRAFT_OK;
 }
@@ -1064,6 +1089,8 @@ int ora_restore(ora_engine *e, const mraft_persistent *in, int64_t n, const int3
     S.current_term[s] = r->current_term;                              /* :231 */
     S.voted_for[s] = r->voted_for;                                    /* :232 */
     memcpy(S.log_term + s * e->L, terms + r->terms_offset, sizeof(int32_t) * (size_t)cnt);  /* :233 */
+    S.log_head[s] = 0;                                                /* a fresh raftLog */
+    S.has_snapshot[s] = 0;                                            /* Make: no snapshot pending */
     S.dummy_index[s] = r->dummy_index;
     S.last_index[s] = r->last_index;
     S.commit_index[s] = r->dummy_index;                               /* :79 */

@@ -63,7 +63,8 @@ int ora_replicate_tick_mt(ora_engine *e, const int32_t *leader_peer,
 int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
               int64_t n, int32_t *out_index, int32_t *out_term,
               int32_t *out_is_leader, int32_t *item_err);
-int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to);
+int ora_collect_apply(ora_engine *e, int32_t *out_from, int32_t *out_to, int32_t *out_snap_index,
+                      int32_t *out_snap_term);
 
 int ora_snapshot(ora_engine *e, const int32_t *slots, const int32_t *index, int64_t n,
                  int32_t *item_err);

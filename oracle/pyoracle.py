@@ -151,6 +151,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
     matchIndex: List[int]
     grantedVotes: int = 0
     persisted: int = 0  # persist() (1) / SaveStateAndSnapshot() (1|2) ran since the last collect
+    hasSnapshot: bool = False  # raft.go:158, set by HandleInstallSnapshot (raft_snapshot.go:52)
 
     def persist(self, bits=1):  # raft.go:205-208; SaveStateAndSnapshot persister.go:58-63
         self.persisted |= bits
@@ -287,6 +288,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
             self.raftLog.logs[0].Index = args.LastIncludedIndex
             self.raftLog.logs[0].Term = args.LastIncludedTerm
             self.persist(3)  # SaveStateAndSnapshot, :47
+            self.hasSnapshot = True  # :52
             return True
         finally:
             reply.Term = self.currentTerm
@@ -356,7 +358,7 @@ class Raft:  # raft.go:16-40 (decision-relevant fields)
 # ---------------------------------------------------------------------------
 
 STATE_KEYS = ("current_term", "voted_for", "state", "commit_index", "last_applied",
-              "dummy_index", "last_index", "granted_votes", "log_term", "match_index", "next_index", "persist_dirty")
+              "dummy_index", "last_index", "granted_votes", "log_term", "match_index", "next_index", "persist_dirty", "log_head", "has_snapshot")
 
 
 def from_soa(st: dict, G: int, P: int, L: int) -> List[Raft]:
@@ -364,7 +366,8 @@ def from_soa(st: dict, G: int, P: int, L: int) -> List[Raft]:
     for s in range(G * P):
         d = int(st["dummy_index"][s]); last = int(st["last_index"][s])
         row = st["log_term"][s * L:(s + 1) * L]
-        logs = [Entry(d + k, int(row[k])) for k in range(last - d + 1)]
+        h = int(st["log_head"][s]) if "log_head" in st else 0   # the engine's ring (include/mraft.h)
+        logs = [Entry(d + k, int(row[(h + k) % L])) for k in range(last - d + 1)]
         rafts.append(Raft(me=s % P, npeers=P, currentTerm=int(st["current_term"][s]),
                           votedFor=int(st["voted_for"][s]), state=int(st["state"][s]),
                           raftLog=RaftLog(logs), commitIndex=int(st["commit_index"][s]),
@@ -372,13 +375,16 @@ def from_soa(st: dict, G: int, P: int, L: int) -> List[Raft]:
                           nextIndex=[int(x) for x in st["next_index"][s * P:(s + 1) * P]],
                           matchIndex=[int(x) for x in st["match_index"][s * P:(s + 1) * P]],
                           grantedVotes=int(st["granted_votes"][s]),
-                          persisted=int(st["persist_dirty"][s]) if "persist_dirty" in st else 0))
+                          persisted=int(st["persist_dirty"][s]) if "persist_dirty" in st else 0,
+                          hasSnapshot=bool(st["has_snapshot"][s]) if "has_snapshot" in st else False))
     return rafts
 
 
 def to_soa(rafts: List[Raft], st: dict, G: int, P: int, L: int) -> dict:
     """Write objects back into a copy of st (log slots beyond lastIndex keep
-    their previous contents, like the device arrays)."""
+    their previous contents, like the device arrays). The object model has no
+    ring: each log is written from the replica's existing log_head, so the
+    result equals the engine's logically (tests compare logical logs)."""
     out = {k: np.array(v, copy=True) for k, v in st.items()}
     for s, rf in enumerate(rafts):
         out["current_term"][s] = rf.currentTerm
@@ -392,10 +398,14 @@ def to_soa(rafts: List[Raft], st: dict, G: int, P: int, L: int) -> dict:
         if "persist_dirty" not in out:
             out["persist_dirty"] = np.zeros(len(rafts), dtype=np.int32)
         out["persist_dirty"][s] = rf.persisted
+        if "has_snapshot" not in out:
+            out["has_snapshot"] = np.zeros(len(rafts), dtype=np.int32)
+        out["has_snapshot"][s] = int(rf.hasSnapshot)
         if len(rf.raftLog.logs) > L:
             raise ValueError("log exceeds capacity")
+        h = int(out["log_head"][s]) if "log_head" in out else 0
         for k, e in enumerate(rf.raftLog.logs):
-            out["log_term"][s * L + k] = e.Term
+            out["log_term"][s * L + (h + k) % L] = e.Term
         out["match_index"][s * P:(s + 1) * P] = rf.matchIndex
         out["next_index"][s * P:(s + 1) * P] = rf.nextIndex
     return out

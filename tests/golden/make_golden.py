@@ -31,7 +31,7 @@ def one_group(P, L, slots):
     st = {k: np.zeros(n, dtype=np.int64) for k, n in {
         "current_term": P, "voted_for": P, "state": P, "commit_index": P, "last_applied": P,
         "dummy_index": P, "last_index": P, "granted_votes": P, "log_term": P * L,
-        "match_index": P * P, "next_index": P * P, "persist_dirty": P}.items()}
+        "match_index": P * P, "next_index": P * P, "persist_dirty": P, "log_head": P, "has_snapshot": P}.items()}
     st["voted_for"][:] = -1
     st["state"][:] = FOLLOWER
     for p in range(P):
@@ -305,8 +305,9 @@ def check_kat(k, out):
                                                    st["persist_dirty"][int(s_)], v)
     for key, slot in (("slot1", 1), ("slot0", 0), ("slot2", 2)):
         for f, v in e.get(key, {}).items():
-            if f == "log":
-                got = list(st["log_term"][slot * L: slot * L + len(v)])
+            if f == "log":  # in Index order from the dummy (the engine's ring, include/mraft.h)
+                h = int(st["log_head"][slot]) if "log_head" in st else 0
+                got = [st["log_term"][slot * L + (h + j) % L] for j in range(len(v))]
                 assert got == v, (k["name"], got, v)
             else:
                 assert st[f][slot] == v, (k["name"], f, st[f][slot], v)

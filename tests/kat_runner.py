@@ -20,6 +20,8 @@ def load_kats():
 def kat_state(k):
     st = {kk: np.array(v, dtype=np.int32) for kk, v in k["state"].items()}
     st.setdefault("persist_dirty", np.zeros(k["G"] * k["P"], np.int32))
+    st.setdefault("log_head", np.zeros(k["G"] * k["P"], np.int32))
+    st.setdefault("has_snapshot", np.zeros(k["G"] * k["P"], np.int32))
     return st
 
 

@@ -37,7 +37,7 @@ def lib():
             "ora_replicate_tick": [E, vp, vp],
             "ora_replicate_tick_mt": [E, vp, vp, i32],
             "ora_start": [E, vp, vp, i64, vp, vp, vp, vp],
-            "ora_collect_apply": [E, vp, vp],
+            "ora_collect_apply": [E, vp, vp, vp, vp],
             "ora_start_election": [E, vp, i64, vp, vp],
             "ora_handle_request_vote": [E, vp, i64, vp, vp],
             "ora_process_vote_replies": [E, vp, i64, vp, i64, vp, vp],
@@ -75,6 +75,8 @@ class Oracle:
     def __init__(self, G: int, P: int, L: int, st: dict):
         self.G, self.P, self.L = G, P, L
         self.st = copy_state(st)
+        self.st.setdefault("log_head", np.zeros(G * P, np.int32))  # fixtures made before the ring
+        self.st.setdefault("has_snapshot", np.zeros(G * P, np.int32))
         self._e = OraEngine(G, P, L, soa_of(self.st))
 
     def state(self) -> dict:
@@ -140,11 +142,13 @@ class Oracle:
         lib().ora_start(ctypes.byref(self._e), ptr(slots), ptr(c), n, ptr(idx), ptr(term), ptr(isl), ptr(err))
         return idx, term, isl, err
 
-    def collect_apply(self):
+    def collect_apply(self, snapshots: bool = False):
         gp = self.G * self.P
         fr, to = np.zeros(gp, np.int32), np.zeros(gp, np.int32)
-        lib().ora_collect_apply(ctypes.byref(self._e), ptr(fr), ptr(to))
-        return fr, to
+        si = np.zeros(gp, np.int32) if snapshots else None
+        stm = np.zeros(gp, np.int32) if snapshots else None
+        lib().ora_collect_apply(ctypes.byref(self._e), ptr(fr), ptr(to), ptr(si), ptr(stm))
+        return (fr, to, si, stm) if snapshots else (fr, to)
 
     def store_state(self):
         return copy_state(self.st)
@@ -249,23 +253,50 @@ class Oracle:
         return commit, tl
 
 
-def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = ""):
-    """Compare two state images. Log slots beyond lastIndex are dead and may
-    differ (the reference's slice has no such slots), so only live slots
-    [0, last-dummy] of every replica are compared."""
+def logical_logs(st: dict, G: int, P: int, L: int):
+    """[G*P, L] view of every replica's log in Index order: row r, column k =
+    the term of Index dummy + k (the ring of include/mraft.h unrolled from
+    log_head); columns past last - dummy are dead slots."""
+    lt = st["log_term"].reshape(G * P, L)
+    h = st["log_head"] if "log_head" in st else np.zeros(G * P, np.int32)
+    cols = (h[:, None].astype(np.int64) + np.arange(L)[None, :]) % L
+    return np.take_along_axis(lt, cols, axis=1)
+
+
+def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = "", heads: bool = True):
+    """Compare two state images. Logs are compared in Index order over the
+    live entries [dummy, last] of every replica (slots past lastIndex are dead:
+    the reference's slice has no such slots). heads=False skips the ring
+    positions themselves (the Python restatement has no ring)."""
     for k in a:
-        if k == "log_term":
+        if k == "log_term" or (k == "log_head" and not heads) or k not in b:
             continue
         if not np.array_equal(a[k], b[k]):
             bad = np.nonzero(a[k] != b[k])[0][:8]
             raise AssertionError(f"{ctx}: {k} differs at {bad}: {a[k][bad]} vs {b[k][bad]}")
-    la = a["log_term"].reshape(G * P, L)
-    lb = b["log_term"].reshape(G * P, L)
+    la = logical_logs(a, G, P, L)
+    lb = logical_logs(b, G, P, L)
     live = a["last_index"] - a["dummy_index"]
     mask = np.arange(L)[None, :] <= live[:, None]
     if not np.array_equal(np.where(mask, la, 0), np.where(mask, lb, 0)):
         rows = np.nonzero((np.where(mask, la, 0) != np.where(mask, lb, 0)).any(axis=1))[0][:8]
         raise AssertionError(f"{ctx}: log_term differs in replicas {rows}")
+
+
+def rotate_rings(st: dict, G: int, P: int, L: int, rng, frac: float = 1.0) -> dict:
+    """The same logical state with every replica's ring started at a random
+    head (a fraction `frac` of the replicas): row contents rotated so Index
+    dummy + k sits at (head + k) mod L. Exercises the wrap in every kernel."""
+    out = {k: np.array(v, copy=True) for k, v in st.items()}
+    logs = logical_logs(st, G, P, L)
+    h = rng.integers(0, L, G * P).astype(np.int32)
+    h[rng.random(G * P) >= frac] = 0
+    cols = (h[:, None].astype(np.int64) + np.arange(L)[None, :]) % L
+    lt = np.empty_like(logs)
+    np.put_along_axis(lt, cols, logs, axis=1)
+    out["log_term"] = lt.reshape(-1)
+    out["log_head"] = h
+    return out
 
 
 class GoShaped:

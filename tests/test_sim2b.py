@@ -1,10 +1,13 @@
-"""Config #1: the reference's 2A/2B test scenarios (src/raft/test_test.go),
-replayed by the deterministic harness in tests/sim2b.py through the engine's
-C ABI. The CPU run (oracle backend) checks the harness + oracle; the GPU run
-checks libmraft_hip.so; both must satisfy the reference tests' assertions
-(indices 1,2,3; no commit without a majority; index2 in [2,3]; convergence
-after divergent partitions; at most one leader per term; agreement on every
-committed index)."""
+"""Config #1: the reference's 2A/2B/2C/2D test scenarios
+(src/raft/test_test.go), replayed by the deterministic harness in
+tests/sim2b.py through the engine's C ABI. The CPU run (oracle backend) checks
+the harness + oracle; the GPU run checks libmraft_hip.so; both must satisfy
+the reference tests' assertions (indices 1,2,3; no commit without a majority;
+index2 in [2,3]; convergence after divergent partitions; at most one leader
+per term; agreement and in-order apply on every committed index; the RPC
+budgets of TestCount2B; committed client values after churn; snapshots every
+10 entries with InstallSnapshot to lagging or restarted followers, persisted
+log size under MAXLOGSIZE, no index regression after a full crash)."""
 import pytest
 
 from oracle_lib import Oracle
@@ -23,7 +26,7 @@ def _gpu(G, P, L, st):
 
 
 @pytest.mark.parametrize("name", list(SCENARIOS))
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", [1, 2])
 def test_scenario_oracle(name, seed):
     SCENARIOS[name](_oracle, seed=seed)
 
