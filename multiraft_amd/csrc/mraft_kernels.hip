@@ -243,33 +243,41 @@ __global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mr
       // alike and every vector read stays inside its buffer.
       const long long eo = a.entries_offset - (long long)(prev + 1);    // entry Index x -> ent[eo + x]
       const LinRow src{ent, eo};
-      const RingRow fr[1] = {RingRow{s.log, (long long)f * L, fhead - fdummy, L}};  // follower ring
       const int plo = prev + 1, phi = prev + nn, nend = prev + nn + 1;
-      const int start[1] = {plo}, cend[1] = {min(phi, flast) + 1};
-      const int capok[1] = {(int64_t)prev + nn - fdummy <= (int64_t)L - 1};
-      int mode[1] = {M_CMP}, cfrom[1] = {0}, fullmask = 0, found = -1;
-      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)fr[0].at(plo);
+      Fol<1> fo;  // the receiving follower's ring
+      fo.log = s.log;
+      fo.slot0 = f;
+      fo.skip = 1;
+      fo.L = L;
+      fo.base[0] = fhead - fdummy;
+      fo.start[0] = plo;
+      fo.cend[0] = min(phi, flast) + 1;
+      fo.cfrom[0] = 0;
+      fo.cmp = 1;
+      fo.copy = 0;
+      fo.capok = (int64_t)prev + nn - fdummy <= (int64_t)L - 1 ? 1 : 0;
+      fo.full = 0;
+      int found = -1;
+      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)fo.at(0, plo);
       const bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0 && ((ea ^ fa) & 15) == 0 &&
                        (ea & ~(uintptr_t)15) >= (uintptr_t)ent &&
                        ((uintptr_t)(ent + eo + phi) | 15) < (uintptr_t)(ent + n_ent);
       if (vec) {
         int c = plo - (int)((ea >> 2) & 31);                           // 128-B aligned chunks
-        for (; c <= phi && mode[0] == M_CMP; c += 256)
-          pass_chunk<1, 1, true, false>(src, fr, start, cend, nend, mode, cfrom, capok, fullmask, 1, 0, 0, found,
-                                        c, plo, phi);
-        copy_loop<1, 1, true, false>(src, fr, mode, c, nend, plo, phi, 1, 0, 0, found);
+        for (; c <= phi && fo.cmp; c += 256)
+          pass_chunk<1, 1, true, false>(src, fo, nend, 1, 0, 0, found, c, plo, phi);
+        copy_loop<1, true, false>(src, fo, c, nend, plo, phi, 1, 0, 0, found);
       } else {
         int c = plo;
-        for (; c <= phi && mode[0] == M_CMP; c += 256)
-          pass_chunk<1, 1, false, false>(src, fr, start, cend, nend, mode, cfrom, capok, fullmask, 1, 0, 0, found,
-                                         c, plo, phi);
-        copy_loop<1, 1, false, false>(src, fr, mode, c, nend, plo, phi, 1, 0, 0, found);
+        for (; c <= phi && fo.cmp; c += 256)
+          pass_chunk<1, 1, false, false>(src, fo, nend, 1, 0, 0, found, c, plo, phi);
+        copy_loop<1, false, false>(src, fo, c, nend, plo, phi, 1, 0, 0, found);
       }
       int last_after = flast;
-      if (fullmask) {
+      if (fo.full) {
         write_state = false;                                           // engine capacity
         if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_LOG_FULL; }
-      } else if (cfrom[0] > 0) {                                       // truncated and appended
+      } else if (fo.cfrom[0] > 0) {                                       // truncated and appended
         newlast = prev + nn;
         last_after = newlast;
       }

@@ -37,10 +37,6 @@ struct RingRow {
   }
 };
 
-#ifndef MRAFT_COPY_PIPE
-#define MRAFT_COPY_PIPE 1  // software-pipelined copy-only loop (0: the plain loop, for A/B runs)
-#endif
-
 #ifndef MRAFT_TICK_NT
 #define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
 #endif
@@ -74,6 +70,39 @@ __device__ __forceinline__ void st1(int32_t *p, int a) {
   else *p = a;
 }
 
+// The followers a pass serves, with as little wave-uniform state as the pass
+// needs (it is live across the whole streaming loop; at 8 waves per SIMD every
+// scalar held here is one the compiler would otherwise spill): follower q's
+// replica slot is slot0 + q, skipping `skip` (the leader's peer index in the
+// tick), so no 64-bit row offsets are held; its mode is two bits (cmp: still
+// comparing; copy: copying from cfrom on; neither: done); capok (the append
+// fits the capacity) and full (rejected as MRAFT_ITEM_LOG_FULL) are bits too.
+template <int NI>
+struct Fol {
+  int32_t *log;
+  long long slot0;
+  int skip, L;
+  int base[NI];   // ring base: head - dummy (include/mraft.h)
+  int start[NI];  // first compared Index (prev + 1)
+  int cend[NI];   // compared while the follower has the Index: [start, cend)
+  int cfrom[NI];  // first mismatching Index (copy from here)
+  int cmp, copy, capok, full;
+  __device__ __forceinline__ int32_t *at(int q, int idx) const {
+    const long long row = (slot0 + q + (q >= skip ? 1 : 0)) * (long long)L;
+    const int k = idx + base[q];  // >= 0 for every lane that loads or stores (see RingRow)
+    return log + row + (k >= L ? k - L : k);
+  }
+  __device__ __forceinline__ bool is_cmp(int q) const { return (cmp >> q) & 1; }
+  __device__ __forceinline__ bool is_copy(int q) const { return (copy >> q) & 1; }
+  // follower q's first mismatch is at im: copy from there if the append fits
+  __device__ __forceinline__ void mismatch(int q, int im) {
+    cfrom[q] = im;
+    cmp &= ~(1 << q);
+    if ((capok >> q) & 1) copy |= 1 << q;
+    else full |= 1 << q;  // MRAFT_ITEM_LOG_FULL: no state change
+  }
+};
+
 // One chunk of the streaming pass over the leader's log. The pass serves
 // (1) every follower q's entry merge: compare entries [start_q, cend_q) with
 // the follower's log, then (from the first mismatch) copy entries up to `hi`
@@ -81,13 +110,10 @@ __device__ __forceinline__ void st1(int32_t *p, int a) {
 // whose term equals T (kept in `found`, the pass ascends).
 // VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
 // otherwise lane j owns c+64(4v+u)+j. Entry idx is at src.at(idx), follower
-// q's term of Index idx at fr[q].at(idx).
+// q's term of Index idx at fo.at(q, idx).
 template <int NI, int V, bool VEC, bool COUNT, class Src>
-__device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[NI], const int (&start)[NI],
-                                           const int (&cend)[NI], int nend, int (&mode)[NI],
-                                           int (&cfrom)[NI], const int (&capok)[NI],
-                                           int &fullmask, int slo, int shi, int T, int &found,
-                                           int c, int plo, int phi) {
+__device__ __forceinline__ void pass_chunk(const Src &src, Fol<NI> &fo, int nend, int slo, int shi, int T,
+                                           int &found, int c, int plo, int phi) {
   constexpr int CW = 256 * V;
   const int lane = lane_id();
   int idx[V][4], e[V][4];
@@ -115,18 +141,18 @@ __device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[N
     for (int v = 0; v < V; ++v)
 #pragma unroll
       for (int u = 0; u < 4; ++u) f[q][v][u] = 0;
-    if (mode[q] != M_CMP || start[q] > c + CW - 1 || cend[q] <= c) continue;
+    if (!fo.is_cmp(q) || fo.start[q] > c + CW - 1 || fo.cend[q] <= c) continue;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       if (VEC) {
-        if (idx[v][3] >= start[q] && idx[v][0] < cend[q]) {
-          const int4 x = ld4(fr[q].at(idx[v][0]));
+        if (idx[v][3] >= fo.start[q] && idx[v][0] < fo.cend[q]) {
+          const int4 x = ld4(fo.at(q, idx[v][0]));
           f[q][v][0] = x.x; f[q][v][1] = x.y; f[q][v][2] = x.z; f[q][v][3] = x.w;
         }
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (idx[v][u] >= start[q] && idx[v][u] < cend[q]) f[q][v][u] = ld1(fr[q].at(idx[v][u]));
+          if (idx[v][u] >= fo.start[q] && idx[v][u] < fo.cend[q]) f[q][v][u] = ld1(fo.at(q, idx[v][u]));
       }
     }
   }
@@ -160,10 +186,10 @@ __device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[N
   }
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
-    if (mode[q] == M_DONE || start[q] > c + CW - 1) continue;
-    if (mode[q] == M_CMP) {
+    if ((!fo.is_cmp(q) && !fo.is_copy(q)) || fo.start[q] > c + CW - 1) continue;
+    if (fo.is_cmp(q)) {
       int im = -1;  // first mismatching entry index in this chunk
-      if (cend[q] > c) {
+      if (fo.cend[q] > c) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
           if (im >= 0) break;
@@ -171,7 +197,7 @@ __device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[N
             int first = 4;
 #pragma unroll
             for (int u = 3; u >= 0; --u)
-              if (idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]) first = u;
+              if (idx[v][u] >= fo.start[q] && idx[v][u] < fo.cend[q] && e[v][u] != f[q][v][u]) first = u;
             const unsigned long long m = __ballot(first < 4);
             if (m) {
               const int l = first_lane(m);
@@ -181,65 +207,55 @@ __device__ __forceinline__ void pass_chunk(const Src &src, const RingRow (&fr)[N
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const unsigned long long m =
-                  __ballot(idx[v][u] >= start[q] && idx[v][u] < cend[q] && e[v][u] != f[q][v][u]);
+                  __ballot(idx[v][u] >= fo.start[q] && idx[v][u] < fo.cend[q] && e[v][u] != f[q][v][u]);
               if (m && im < 0) im = c + 64 * (4 * v + u) + first_lane(m);
             }
           }
         }
       }
-      if (im < 0 && cend[q] <= c + CW - 1) {
+      if (im < 0 && fo.cend[q] <= c + CW - 1) {
         // Compared region ends in this chunk without a mismatch: either every
         // entry matched (no truncation: the non-FIFO guard, :146-155) or the
         // follower's log ends before the entries do ("beyond the end").
-        if (cend[q] < nend) im = cend[q];
-        else mode[q] = M_DONE;
+        if (fo.cend[q] < nend) im = fo.cend[q];
+        else fo.cmp &= ~(1 << q);
       }
-      if (im >= 0) {
-        cfrom[q] = im;
-        if (capok[q]) {
-          mode[q] = M_COPY;
-        } else {
-          mode[q] = M_DONE;  // MRAFT_ITEM_LOG_FULL: no state change
-          fullmask |= 1 << q;
-        }
-      }
+      if (im >= 0) fo.mismatch(q, im);
     }
-    if (mode[q] == M_COPY) {
+    if (fo.is_copy(q)) {
       if (!COUNT) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-          if (VEC && idx[v][0] >= cfrom[q] && idx[v][3] < nend) {
-            st4(fr[q].at(idx[v][0]), e[v][0], e[v][1], e[v][2], e[v][3]);
+          if (VEC && idx[v][0] >= fo.cfrom[q] && idx[v][3] < nend) {
+            st4(fo.at(q, idx[v][0]), e[v][0], e[v][1], e[v][2], e[v][3]);
           } else {
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (idx[v][u] >= cfrom[q] && idx[v][u] < nend) st1(fr[q].at(idx[v][u]), e[v][u]);
+              if (idx[v][u] >= fo.cfrom[q] && idx[v][u] < nend) st1(fo.at(q, idx[v][u]), e[v][u]);
           }
         }
       }
-      if (c + CW >= nend) mode[q] = M_DONE;
+      if (c + CW >= nend) fo.copy &= ~(1 << q);
     }
   }
 }
 
 // Copy-only tail of the pass, once no follower is still comparing: every
-// follower in M_COPY receives the leader's entries [c, nend) (its copy start
-// is already behind c), VC dwordx4 loads per lane in flight per iteration,
-// and the commit scan [slo, shi] continues on the same loads.
-template <int NI, int VC, bool VEC, bool COUNT, class Src>
-__device__ __forceinline__ void copy_loop(const Src &src, const RingRow (&fr)[NI], const int (&mode)[NI], int c,
-                                          int nend, int plo, int phi, int slo, int shi, int T, int &found) {
-  constexpr int CW = 256 * VC;
+// follower still copying receives the leader's entries [c, nend) (its copy
+// start is already behind c), and the commit scan [slo, shi] continues on the
+// same loads. Software-pipelined: chunk c+256 is loaded before chunk c is
+// stored, so a wave never waits for its own stores before issuing the next
+// load (gfx9's vmcnt counts both in order). The next chunk is loaded only when
+// the loop will run for it: no extra traffic. (Two chunks ahead,
+// MRAFT_COPY_PIPE=2, measured no faster: the copy is memory-system-bound at 8
+// waves per SIMD, profiles/r2_experiments.)
+template <int NI, bool VEC, bool COUNT, class Src>
+__device__ __forceinline__ void copy_loop(const Src &src, const Fol<NI> &fo, int c, int nend, int plo, int phi,
+                                          int slo, int shi, int T, int &found) {
+  constexpr int CW = 256;
   const int lane = lane_id();
-  int cmask = 0;
-#pragma unroll
-  for (int q = 0; q < NI; ++q) cmask |= (mode[q] == M_COPY) ? (1 << q) : 0;
-#if MRAFT_COPY_PIPE
-  if constexpr (VEC && VC == 1) {
-    // Software-pipelined: chunk c+256 is loaded before chunk c is stored, so
-    // a wave never waits for its own stores before issuing the next load
-    // (vmcnt counts both in order). The next chunk is loaded only when the
-    // loop will run for it (same exit rule as below): no extra traffic.
+  int cmask = fo.copy;
+  if constexpr (VEC) {
     if (c > phi || (!cmask && !(slo <= shi && c <= shi))) return;
     int4 cur = make_int4(0, 0, 0, 0);
     if (c + 4 * lane + 3 >= plo && c + 4 * lane <= phi) cur = ld4(src.at(c + 4 * lane));
@@ -267,12 +283,12 @@ __device__ __forceinline__ void copy_loop(const Src &src, const RingRow (&fr)[NI
         for (int q = 0; q < NI; ++q) {
           if (!((cmask >> q) & 1)) continue;
           if (i0 + 3 < nend) {
-            st4(fr[q].at(i0), cur.x, cur.y, cur.z, cur.w);
+            st4(fo.at(q, i0), cur.x, cur.y, cur.z, cur.w);
           } else {
             const int e[4] = {cur.x, cur.y, cur.z, cur.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              if (i0 + u < nend) st1(fr[q].at(i0 + u), e[u]);
+              if (i0 + u < nend) st1(fo.at(q, i0 + u), e[u]);
           }
         }
       }
@@ -281,200 +297,36 @@ __device__ __forceinline__ void copy_loop(const Src &src, const RingRow (&fr)[NI
       c = cn;
       cur = nxt;
     }
-  }
-#endif
-  for (; c <= phi; c += CW) {
-    const bool scan = slo <= shi && c <= shi && c + CW - 1 >= slo;
-    if (!cmask && !(slo <= shi && c <= shi)) break;
-    int idx[VC][4], e[VC][4];
+  } else {
+    for (; c <= phi; c += 64 * 4) {
+      if (!cmask && !(slo <= shi && c <= shi)) break;
+      int idx[4], e[4];
 #pragma unroll
-    for (int v = 0; v < VC; ++v)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) idx[v][u] = VEC ? c + 256 * v + 4 * lane + u : c + 64 * (4 * v + u) + lane;
-#pragma unroll
-    for (int v = 0; v < VC; ++v) {
-      if (VEC) {
-        int4 x = make_int4(0, 0, 0, 0);
-        if (idx[v][3] >= plo && idx[v][0] <= phi) x = ld4(src.at(idx[v][0]));
-        e[v][0] = x.x; e[v][1] = x.y; e[v][2] = x.z; e[v][3] = x.w;
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src.at(idx[v][u])) : 0;
+      for (int u = 0; u < 4; ++u) {
+        idx[u] = c + 64 * u + lane;
+        e[u] = (idx[u] >= plo && idx[u] <= phi) ? ld1(src.at(idx[u])) : 0;
       }
-    }
-    if (scan) {
-      int hit = -1;
+      if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+        int hit = -1;
 #pragma unroll
-      for (int v = VC - 1; v >= 0; --v) {
-        if (hit >= 0) break;
-        if (VEC) {
-          int lu = -1;
+        for (int u = 3; u >= 0; --u) {
+          if (hit >= 0) break;
+          const unsigned long long m = __ballot(idx[u] >= slo && idx[u] <= shi && e[u] == T);
+          if (m) hit = c + 64 * u + 63 - __clzll((long long)m);
+        }
+        if (hit >= 0) found = hit;
+      }
+      if (!COUNT) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) {
+          if (!((cmask >> q) & 1)) continue;
 #pragma unroll
           for (int u = 0; u < 4; ++u)
-            if (idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T) lu = u;
-          const unsigned long long m = __ballot(lu >= 0);
-          if (m) {
-            const int l = 63 - __clzll((long long)m);
-            hit = c + 256 * v + 4 * l + __shfl(lu, l, 64);
-          }
-        } else {
-#pragma unroll
-          for (int u = 3; u >= 0; --u) {
-            if (hit >= 0) break;
-            const unsigned long long m =
-                __ballot(idx[v][u] >= slo && idx[v][u] <= shi && e[v][u] == T);
-            if (m) hit = c + 64 * (4 * v + u) + 63 - __clzll((long long)m);
-          }
+            if (idx[u] < nend) st1(fo.at(q, idx[u]), e[u]);
         }
       }
-      if (hit >= 0) found = hit;
+      if (c + CW >= nend) cmask = 0;
     }
-    if (!COUNT) {
-#pragma unroll
-      for (int q = 0; q < NI; ++q) {
-        if (!((cmask >> q) & 1)) continue;
-#pragma unroll
-        for (int v = 0; v < VC; ++v) {
-          if (VEC && idx[v][3] < nend) {
-            st4(fr[q].at(idx[v][0]), e[v][0], e[v][1], e[v][2], e[v][3]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (idx[v][u] < nend) st1(fr[q].at(idx[v][u]), e[v][u]);
-          }
-        }
-      }
-    }
-    if (c + CW >= nend) cmask = 0;
-  }
-}
-
-// The whole streaming pass as ONE software-pipelined loop (VEC layout, one
-// dwordx4 per lane and stream per 256-entry chunk): compare chunk c, then
-// issue chunk c+256's loads (the leader's and every still-comparing
-// follower's), then chunk c's stores. gfx9's vmcnt counts loads and stores in
-// one in-order counter, so in pass_chunk + copy_loop a compare chunk waited
-// for the previous chunk's stores before its own loads returned (a store round
-// trip plus a load round trip per chunk); here the next loads are in flight
-// before the stores issue. Same results, loads and stores as pass_chunk
-// followed by copy_loop: chunk c+256 is loaded only when the loop runs for it,
-// and every load stays inside the row it streams (lanes whose 4 entries end
-// before plo / start do not load).
-template <int NI, bool COUNT, class Src>
-__device__ __forceinline__ void stream_pass(const Src &src, const RingRow (&fr)[NI],
-                                            const int (&start)[NI], const int (&cend)[NI], int nend,
-                                            int (&mode)[NI], int (&cfrom)[NI], const int (&capok)[NI],
-                                            int &fullmask, int slo, int shi, int T, int &found, int c,
-                                            int plo, int phi) {
-  constexpr int CW = 256;
-  const int lane = lane_id();
-  auto runs = [&](int cc) {
-    if (cc > phi) return false;
-    bool a = slo <= shi && cc <= shi;
-#pragma unroll
-    for (int q = 0; q < NI; ++q) a = a || mode[q] != M_DONE;
-    return a;
-  };
-  auto load_leader = [&](int cc) {
-    const int i0 = cc + 4 * lane;
-    int4 x = make_int4(0, 0, 0, 0);
-    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src.at(i0));
-    return x;
-  };
-  auto load_follower = [&](int q, int cc) {
-    const int i0 = cc + 4 * lane;
-    int4 x = make_int4(0, 0, 0, 0);
-    if (mode[q] == M_CMP && start[q] <= cc + CW - 1 && cend[q] > cc && i0 + 3 >= start[q] && i0 < cend[q])
-      x = ld4(fr[q].at(i0));
-    return x;
-  };
-  if (!runs(c)) return;
-  int4 e = load_leader(c);
-  int4 f[NI];
-#pragma unroll
-  for (int q = 0; q < NI; ++q) f[q] = load_follower(q, c);
-  for (;;) {
-    const int i0 = c + 4 * lane;
-    const int ev[4] = {e.x, e.y, e.z, e.w};
-    // Commit scan: highest index of this chunk in [slo, shi] with term T.
-    if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
-      int lu = -1;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (i0 + u >= slo && i0 + u <= shi && ev[u] == T) lu = u;
-      const unsigned long long m = __ballot(lu >= 0);
-      if (m) {
-        const int l = 63 - __clzll((long long)m);
-        found = c + 4 * l + __shfl(lu, l, 64);
-      }
-    }
-    // Compare: first mismatch of every follower still comparing.
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (mode[q] != M_CMP || start[q] > c + CW - 1) continue;
-      int im = -1;
-      if (cend[q] > c) {
-        const int fv[4] = {f[q].x, f[q].y, f[q].z, f[q].w};
-        int first = 4;
-#pragma unroll
-        for (int u = 3; u >= 0; --u)
-          if (i0 + u >= start[q] && i0 + u < cend[q] && ev[u] != fv[u]) first = u;
-        const unsigned long long m = __ballot(first < 4);
-        if (m) {
-          const int l = first_lane(m);
-          im = c + 4 * l + __shfl(first, l, 64);
-        }
-      }
-      if (im < 0 && cend[q] <= c + CW - 1) {
-        // Compared region ends in this chunk without a mismatch: every entry
-        // matched (no truncation: the non-FIFO guard, :146-155) or the
-        // follower's log ends before the entries do ("beyond the end").
-        if (cend[q] < nend) im = cend[q];
-        else mode[q] = M_DONE;
-      }
-      if (im >= 0) {
-        cfrom[q] = im;
-        if (capok[q]) {
-          mode[q] = M_COPY;
-        } else {
-          mode[q] = M_DONE;  // MRAFT_ITEM_LOG_FULL: no state change
-          fullmask |= 1 << q;
-        }
-      }
-    }
-    // This chunk's copies, and who still needs the next chunk.
-    int cmask = 0;
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (mode[q] != M_COPY) continue;
-      cmask |= 1 << q;
-      if (c + CW >= nend) mode[q] = M_DONE;
-    }
-    const int cn = c + CW;
-    const bool more = runs(cn);
-    int4 en = make_int4(0, 0, 0, 0);
-    int4 fn[NI];
-    if (more) en = load_leader(cn);
-#pragma unroll
-    for (int q = 0; q < NI; ++q) fn[q] = more ? load_follower(q, cn) : make_int4(0, 0, 0, 0);
-    if (!COUNT) {
-#pragma unroll
-      for (int q = 0; q < NI; ++q) {
-        if (!((cmask >> q) & 1)) continue;
-        if (i0 >= cfrom[q] && i0 + 3 < nend) {
-          st4(fr[q].at(i0), e.x, e.y, e.z, e.w);
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (i0 + u >= cfrom[q] && i0 + u < nend) st1(fr[q].at(i0 + u), ev[u]);
-        }
-      }
-    }
-    if (!more) return;
-    c = cn;
-    e = en;
-#pragma unroll
-    for (int q = 0; q < NI; ++q) f[q] = fn[q];
   }
 }
 

@@ -82,6 +82,23 @@ __device__ __forceinline__ long long interval_len(long long a, long long b) {
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// The state pointers again, read afresh from the kernel-argument segment (the
+// tick's first argument is the Dev struct). Phase C/D use this copy, so the
+// entry copy of the ~14 array pointers dies after the header instead of being
+// held (and spilled) across the streaming pass; the segment pointer is passed
+// through an empty asm so the loads are new scalar loads, not the entry ones.
+__device__ __forceinline__ Dev reload_dev() {
+  const __attribute__((address_space(4))) Dev *kp =
+      (const __attribute__((address_space(4))) Dev *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  Dev d;
+  d.term = kp->term; d.voted = kp->voted; d.role = kp->role; d.commit = kp->commit;
+  d.applied = kp->applied; d.dummy = kp->dummy; d.last = kp->last; d.votes = kp->votes;
+  d.log = kp->log; d.match = kp->match; d.next = kp->next; d.pdirty = kp->pdirty;
+  d.head = kp->head; d.hsnap = kp->hsnap; d.G = kp->G; d.P = kp->P; d.L = kp->L;
+  return d;
+}
+
 // Reply fold of one group (processAppendEntriesReply, :66-88, in peer order),
 // wave-uniform. Inputs per follower slot q come from lane q. The fold keeps
 // only what the rest of the tick needs (bit q of gate_m: the reply passed the
@@ -156,9 +173,6 @@ struct Fold {
 #ifndef MRAFT_TICK_MINW
 #define MRAFT_TICK_MINW 8  // __launch_bounds__ minimum waves per SIMD
 #endif
-#ifndef MRAFT_TICK_VC
-#define MRAFT_TICK_VC 1    // dwordx4 vectors per lane in the copy-only loop
-#endif
 #ifndef MRAFT_TICK_EXP
 #define MRAFT_TICK_EXP 0   // traffic experiments only (wrong results): 1 = no pass, 2 = no pass, no scans,
                            // 3 = as 2 and no log[prev] / log[last] header loads
@@ -166,11 +180,11 @@ struct Fold {
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
 #endif
+#ifndef MRAFT_TICK_RELOAD
+#define MRAFT_TICK_RELOAD 1  // phase C/D re-read the state pointers (not held across the pass)
+#endif
 #ifndef MRAFT_TICK_HDR_EXTRA
 #define MRAFT_TICK_HDR_EXTRA 0  // experiment: extra dependent header round trips (wrong only in timing)
-#endif
-#ifndef MRAFT_TICK_STREAM
-#define MRAFT_TICK_STREAM 0  // 1: one software-pipelined streaming loop (stream_pass; spills: slower)
 #endif
 #ifndef MRAFT_TICK_TRACE
 #define MRAFT_TICK_TRACE 0  // diagnostic build: s_memrealtime stamps per group (tools/trace_tick.py)
@@ -392,26 +406,32 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 
   // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
-  RingRow fr[NI];
-  int start[NI], cend[NI], mode[NI], cfrom[NI], capok[NI];
+  Fol<NI> fo;
+  fo.log = s.log;
+  fo.slot0 = (long long)g * P;
+  fo.skip = lp;
+  fo.L = L;
+  fo.cmp = merge_m;
+  fo.copy = 0;
+  fo.capok = 0;
+  fo.full = 0;
   int mlo = last + 1, maybe_full = 0;
   const RingRow lsrc{s.log, lrow, lb, L};
   bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
-    const int qp = q < lp ? q : q + 1;
     const int sp = uni(__shfl(prev, q, 64)), sd = uni(__shfl(fdummy, q, 64)),
               sl = uni(__shfl(flast, q, 64)), sh = uni(__shfl(fhead, q, 64));
-    fr[q] = RingRow{s.log, ((long long)g * P + qp) * L, sh - sd, L};
-    start[q] = sp + 1;
-    cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
-    cfrom[q] = 0;
-    capok[q] = (long long)last - sd <= (long long)L - 1;
-    mode[q] = ((merge_m >> q) & 1) ? M_CMP : M_DONE;
-    if (mode[q] == M_CMP) {
-      mlo = min(mlo, start[q]);
-      vec = vec && (((fr[q].base - lb) & 3) == 0);  // 4-entry groups aligned alike in both rings
-      maybe_full |= !capok[q];
+    fo.base[q] = sh - sd;
+    fo.start[q] = sp + 1;
+    fo.cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
+    fo.cfrom[q] = 0;
+    const bool capok = (long long)last - sd <= (long long)L - 1;
+    fo.capok |= capok ? 1 << q : 0;
+    if ((merge_m >> q) & 1) {
+      mlo = min(mlo, fo.start[q]);
+      vec = vec && (((fo.base[q] - lb) & 3) == 0);  // 4-entry groups aligned alike in both rings
+      maybe_full |= !capok;
     }
   }
 
@@ -434,50 +454,38 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       }
     }
   }
-  int fullmask = 0, found = -1;
+  int found = -1;
   TICK_STAMP(1);
   if (MRAFT_TICK_EXP == 0 && (merge_m || slo <= shi)) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
-    constexpr int VC = MRAFT_TICK_VC;
     // Chunks start on a 128-B line of the leader's row (physical position of
     // plo rounded down; the ring wraps at a multiple of 4 entries, so every
     // lane's dwordx4 stays contiguous).
-    const int c0a = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
-    if (vec && MRAFT_TICK_STREAM) {
-      stream_pass<NI, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi, T, found,
-                             c0a, plo, phi);
-    } else if (vec) {
-      int c = c0a;
-      for (; c <= phi; c += 256 * V) {
-        bool cmp = false;
-#pragma unroll
-        for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
-        if (!cmp) break;
-        pass_chunk<NI, V, true, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi,
-                                       T, found, c, plo, phi);
-      }
-      copy_loop<NI, VC, true, COUNT>(lsrc, fr, mode, c, last + 1, plo, phi, slo, shi, T, found);
+    if (vec) {
+      int c = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
+      for (; c <= phi && fo.cmp; c += 256 * V)
+        pass_chunk<NI, V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+      copy_loop<NI, true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     } else {
       int c = plo;
-      for (; c <= phi; c += 256 * V) {
-        bool cmp = false;
-#pragma unroll
-        for (int q = 0; q < NI; ++q) cmp |= mode[q] == M_CMP;
-        if (!cmp) break;
-        pass_chunk<NI, V, false, COUNT>(lsrc, fr, start, cend, last + 1, mode, cfrom, capok, fullmask, slo, shi,
-                                        T, found, c, plo, phi);
-      }
-      copy_loop<NI, VC, false, COUNT>(lsrc, fr, mode, c, last + 1, plo, phi, slo, shi, T, found);
+      for (; c <= phi && fo.cmp; c += 256 * V)
+        pass_chunk<NI, V, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+      copy_loop<NI, false, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     }
   }
   TICK_STAMP(2);
+#if MRAFT_TICK_RELOAD
+  const Dev s2 = reload_dev();
+#else
+  const Dev &s2 = s;
+#endif
   int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
     if (lane == q && icls == IC_MERGE) {
-      mk = (cfrom[q] > 0 || ((fullmask >> q) & 1)) ? cfrom[q] - start[q] : -1;
-      if ((fullmask >> q) & 1) icls = IC_FULL;
+      mk = (fo.cfrom[q] > 0 || ((fo.full >> q) & 1)) ? fo.cfrom[q] - fo.start[q] : -1;
+      if ((fo.full >> q) & 1) icls = IC_FULL;
     }
   }
   if (!maybe_full) {
@@ -486,15 +494,15 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     const int have1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
     const int succ1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
 #pragma unroll
-    for (int j = 0; j < P; ++j) mm[j] = uni(s.match[ld * P + j]);  // re-read: not kept live across the pass
+    for (int j = 0; j < P; ++j) mm[j] = uni(s2.match[ld * P + j]);  // re-read: not kept live across the pass
     fd.run(T, lp, mm, have1, succ1, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        if (uni(s.log[lrow + ring(top + lb, L)]) == T) {
+        if (uni(s2.log[lrow + ring(top + lb, L)]) == T) {
           commit = top;
         } else {
-          const int i = wave_scan_down_eq(s.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
+          const int i = wave_scan_down_eq(s2.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
           if (i > c0) commit = i;
         }
       }
@@ -505,13 +513,13 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   int fcadv = 0;
   long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
   if (icls >= IC_STALE && icls <= IC_HB) {
-    if (!COUNT) mark_persist(s, f, MRAFT_PERSIST_STATE);                 // deferred :111
+    if (!COUNT) mark_persist(s2, f, MRAFT_PERSIST_STATE);                 // deferred :111
     if (icls == IC_STALE) {
       cR = 1;
     } else {
       if (!COUNT) {
-        if (adopt) { s.term[f] = T; s.voted[f] = -1; }
-        s.role[f] = kFollower;                                           // :120
+        if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
+        s2.role[f] = kFollower;                                           // :120
       }
       cR = 2;                                                            // term, dummy
       cW = (adopt ? 2 : 0) + 1;                                          // role
@@ -525,7 +533,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
           cR += (mk < 0) ? n : (mk < kc ? mk + 1 : mk);                 // compared follower terms
           if (mk >= 0) {
             newlast = prev + n;
-            if (!COUNT) s.last[f] = newlast;
+            if (!COUNT) s2.last[f] = newlast;
             cW += (n - mk) + 1;
           }
         }
@@ -533,7 +541,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         if (c0 > fcommit) {
           fcadv = 1;
           cW += 1;
-          if (!COUNT) s.commit[f] = min(c0, newlast);
+          if (!COUNT) s2.commit[f] = min(c0, newlast);
         }
       }
     }
@@ -541,12 +549,12 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   if (icls >= IC_IS_STALE && icls <= IC_IS_INSTALL) {
     cR = 1;                                                              // term
     if (!COUNT)
-      mark_persist(s, f, (adopt ? MRAFT_PERSIST_STATE : 0) |            // raft_snapshot.go:26
+      mark_persist(s2, f, (adopt ? MRAFT_PERSIST_STATE : 0) |            // raft_snapshot.go:26
                              (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
     if (icls != IC_IS_STALE) {
       if (!COUNT) {
-        if (adopt) { s.term[f] = T; s.voted[f] = -1; }
-        s.role[f] = kFollower;                                           // :28
+        if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
+        s2.role[f] = kFollower;                                           // :28
       }
       cR += 1;                                                           // commit
       cW = (adopt ? 2 : 0) + 1;
@@ -556,15 +564,15 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         // ring: the head moves to the entry at LastIncludedIndex, no term
         // moves; a new log ([dummy] only, :35-37) keeps its head.
         // (head and dummy re-read here rather than kept live across the pass)
-        const int fh = s.head[f], nh = newlog ? fh : ring(fh + (ldummy - s.dummy[f]), L);
+        const int fh = s2.head[f], nh = newlog ? fh : ring(fh + (ldummy - s2.dummy[f]), L);
         if (!COUNT) {
-          s.log[f * L + nh] = lit;                                       // :44-45 dummy term
-          if (newlog) s.last[f] = ldummy;
-          else s.head[f] = nh;
-          s.hsnap[f] = 1;                                                // raft_snapshot.go:52 hasSnapshot
-          s.dummy[f] = ldummy;
-          s.commit[f] = ldummy;                                          // :42
-          s.applied[f] = ldummy;                                         // :43
+          s2.log[f * L + nh] = lit;                                       // :44-45 dummy term
+          if (newlog) s2.last[f] = ldummy;
+          else s2.head[f] = nh;
+          s2.hsnap[f] = 1;                                                // raft_snapshot.go:52 hasSnapshot
+          s2.dummy[f] = ldummy;
+          s2.commit[f] = ldummy;                                          // :42
+          s2.applied[f] = ldummy;                                         // :43
         }
         cR += 1;                                                         // last
         cW += 3;
@@ -588,12 +596,12 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   if (!COUNT) {
     if (lane == 0) {
       if (fd.stepped) {
-        s.term[ld] = fd.term;
-        s.voted[ld] = -1;
-        s.role[ld] = kFollower;
-        mark_persist(s, ld, MRAFT_PERSIST_STATE);                        // :72, snapshot :64
+        s2.term[ld] = fd.term;
+        s2.voted[ld] = -1;
+        s2.role[ld] = kFollower;
+        mark_persist(s2, ld, MRAFT_PERSIST_STATE);                        // :72, snapshot :64
       }
-      if (commit != c0) s.commit[ld] = commit;
+      if (commit != c0) s2.commit[ld] = commit;
       if (gflags) gflags[g] = flags;
       ex.put(g, commit, fd.stepped ? fd.term : T, fd.stepped ? kFollower : kLeader);
     }
@@ -604,8 +612,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (lane < NI && ((fd.gate_m >> lane) & 1)) {
       const bool isr = ((is_m >> lane) & 1) != 0, ok = ((fd.rs_m >> lane) & 1) != 0;
       const int mv = isr ? ldummy : prev + n;
-      s.next[ld * P + p] = ok ? mv + 1 : rci;
-      if (ok) s.match[ld * P + p] = mv;
+      s2.next[ld * P + p] = ok ? mv + 1 : rci;
+      if (ok) s2.match[ld * P + p] = mv;
     }
   } else {
     // Leader-side words, wave-uniform.

@@ -1,14 +1,19 @@
 #!/bin/bash
 # Builds tick-kernel variants as tools/variants/libmraft_hip_<tag>.so (same
 # sources, different compile-time knobs); tools/tune.sh times them.
-# Each argument is  tag=DEFINES  e.g.  "v2=-DMRAFT_TICK_V=2 -DMRAFT_TICK_MINW=6"
+# Each argument is  tag[@SRCDIR]=DEFINES  e.g.  "v2=-DMRAFT_TICK_V=2 -DMRAFT_TICK_MINW=6"
+# or "head@/tmp/head/multiraft_amd/csrc=" (another source tree, e.g. git archive HEAD).
 set -e
 cd "$(dirname "$0")/../multiraft_amd/csrc"
-mkdir -p ../../tools/variants
-rm -f ../../tools/variants/*.so
+OUT=$(cd ../../tools && pwd)/variants
+HERE=$(pwd)
+mkdir -p "$OUT"
+rm -f "$OUT"/*.so
 for spec in "$@"; do
+  cd "$HERE"
   tag=${spec%%=*}
   defs=${spec#*=}
+  case "$tag" in *@*) cd "${tag#*@}"; tag=${tag%%@*};; esac
   mkdir -p build_$tag
   for f in mraft_abi mraft_kernels mraft_tick mraft_elect; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
@@ -17,7 +22,7 @@ for spec in "$@"; do
   g++ -O3 -std=c++17 -fPIC -c mraft_persist.cpp -o build_$tag/mraft_persist.o &
   g++ -O3 -std=c++17 -fPIC -c mraft_router.cpp -o build_$tag/mraft_router.o &
   wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../tools/variants/libmraft_hip_$tag.so build_$tag/*.o \
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT"/libmraft_hip_$tag.so build_$tag/*.o \
     -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   rm -rf build_$tag
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
