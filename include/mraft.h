@@ -310,9 +310,13 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * entries' terms (n_entry_terms words; pass NULL to read entries by reference
  * from the engine's own log, as produced by mraft_gather_append_args: every
  * item then sees the log as it was before the call, like the reference's copy
- * of args.Entries at gather time, raft_append_entry.go:50-54; items whose
- * source row wraps or is written by the same call are staged first, which
- * costs one host round trip). */
+ * of args.Entries at gather time, raft_append_entry.go:50-54). By reference,
+ * consecutive items reading the same entries (one leader's messages to its
+ * followers, as the gather lays them out) are served together, reading the
+ * entries once; items that read a row this call also writes, and the items
+ * writing such rows, run after the others, the former from a staged copy.
+ * The call then blocks the host until the batch plan is known (the GPU keeps
+ * working meanwhile). */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,

@@ -27,7 +27,12 @@ struct mraft_engine {
   hipStream_t fanin_own = nullptr, fanin_masked = nullptr, tick_masked = nullptr;
   hipEvent_t fanin_ev = nullptr;
   unsigned long long *claim = nullptr;
+  uint32_t *srcmark = nullptr;             // per slot: epoch of the last call that read its row while writing it
   uint32_t epoch = 0;
+  unsigned long long *plan_host = nullptr;  // pinned, device-written: the AppendEntries plan's totals
+  unsigned long long *plan_host_dev = nullptr;
+  unsigned long long *plan_dev = nullptr;   // the plan's accumulators (0-3) and published totals (4-6)
+  unsigned long long plan_seq = 0;
   std::vector<void *> scratch_ptr;
   std::vector<size_t> scratch_cap;
 };
@@ -153,9 +158,13 @@ int ensure_claim(mraft_engine *h) {
     size_t b = (size_t)gp_of(h) * sizeof(unsigned long long);
     if (hipMalloc(&h->claim, b) != hipSuccess) return fail(MRAFT_E_NOMEM, "claim alloc failed");
     HIP_TRY(hipMemsetAsync(h->claim, 0, b, h->stream));
+    if (hipMalloc(&h->srcmark, (size_t)gp_of(h) * sizeof(uint32_t)) != hipSuccess)
+      return fail(MRAFT_E_NOMEM, "srcmark alloc failed");
+    HIP_TRY(hipMemsetAsync(h->srcmark, 0, (size_t)gp_of(h) * sizeof(uint32_t), h->stream));
   }
   if (++h->epoch == 0) {  // wrapped: reset
     HIP_TRY(hipMemsetAsync(h->claim, 0, (size_t)gp_of(h) * sizeof(unsigned long long), h->stream));
+    HIP_TRY(hipMemsetAsync(h->srcmark, 0, (size_t)gp_of(h) * sizeof(uint32_t), h->stream));
     h->epoch = 1;
   }
   return MRAFT_OK;
@@ -234,6 +243,9 @@ int mraft_destroy(mraft_engine *h) {
   for (void *p : h->scratch_ptr)
     if (p) (void)hipFree(p);
   if (h->claim) (void)hipFree(h->claim);
+  if (h->srcmark) (void)hipFree(h->srcmark);
+  if (h->plan_host) (void)hipHostFree(h->plan_host);
+  if (h->plan_dev) (void)hipFree(h->plan_dev);
   if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
   if (h->fanin_masked) (void)hipStreamSynchronize(h->fanin_masked);
   for (hipStream_t s : {h->own_stream, h->fanin_own, h->fanin_masked, h->tick_masked})
@@ -400,34 +412,64 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
   const int32_t *src = en ? (const int32_t *)en : h->dev.log_term;
   const int64_t src_n = en ? n_entry_terms : gp_of(h) * h->L;
-  mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h),
-                      h->P, h->claim, h->epoch, (int32_t *)e, h->stream);
-  void *soff = nullptr, *stage = nullptr;
-  int64_t n_stage = 0;
-  if (!en) {
-    // Entries by reference into the engine's log: stage those whose range
-    // wraps around the source ring or whose source row this batch also
-    // writes (the reference's copy at gather time, raft_append_entry.go:50-54);
-    // the rest are read in place. Sizing the staging buffer costs one host
-    // round trip on this path.
-    void *tot;
-    TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
-    TRY(scratch(h, 15, sizeof(unsigned long long), &tot));
-    HIP_TRY(hipMemsetAsync(tot, 0, sizeof(unsigned long long), h->stream));
-    mraft::launch_ae_stage_plan((const mraft_ae_args *)a, n, src_n, h->L, h->dev.log_head, h->claim, h->epoch,
-                                (const int32_t *)e, (int64_t *)soff, (unsigned long long *)tot, h->stream);
-    unsigned long long ht = 0;
-    HIP_TRY(hipMemcpyAsync(&ht, tot, sizeof ht, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    if (ht > 0) {
-      n_stage = (int64_t)ht;
-      TRY(scratch(h, 16, sizeof(int32_t) * (size_t)ht, &stage));
+  const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
+  if (en) {  // entries in a host-supplied buffer: one message per wave
+    mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h), h->P,
+                        h->claim, h->epoch, (int32_t *)e, h->stream);
+    mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, nullptr, nullptr, 0,
+                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
+    return sg.finish();
+  }
+  // Entries by reference into the engine's log: messages reading the same
+  // entries form sets served by one wave each (the main launch); items that
+  // read or write a row another item of this batch writes or reads are
+  // deferred to a second launch, the readers' entries staged first (the
+  // reference's copy at gather time, raft_append_entry.go:50-54). The plan's
+  // totals reach the host (pinned words the plan kernel writes) while the
+  // main launch runs.
+  if (!h->plan_host) {
+    HIP_TRY(hipHostMalloc((void **)&h->plan_host, 4 * sizeof(unsigned long long),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer((void **)&h->plan_host_dev, h->plan_host, 0));
+    h->plan_host[3] = 0;
+    if (hipMalloc(&h->plan_dev, 8 * sizeof(unsigned long long)) != hipSuccess)
+      return fail(MRAFT_E_NOMEM, "plan counters alloc failed");
+    HIP_TRY(hipMemsetAsync(h->plan_dev, 0, 8 * sizeof(unsigned long long), h->stream));
+  }
+  void *soff, *sets, *defer, *stage = nullptr;
+  TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
+  TRY(scratch(h, 17, sizeof(int64_t) * (size_t)n, &sets));
+  TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
+  mraft::launch_claim_ae((const mraft_ae_args *)a, n, src_n, h->L, gp_of(h), h->claim, h->srcmark, h->epoch,
+                         (int32_t *)e, h->stream);
+  mraft::launch_ae_set_plan((const mraft_ae_args *)a, n, src_n, h->L, ni, h->claim, h->srcmark, h->epoch,
+                            (const int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev,
+                            h->plan_host_dev, ++h->plan_seq, h->stream);
+  // main launch: grid sized by the upper bound n, the set count read on the device
+  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, (const int64_t *)soff,
+                          (const int64_t *)sets, n, h->plan_dev + 5, ni, (mraft_ae_reply *)r, (int32_t *)e,
+                          h->stream);
+  // The plan's last workgroup writes the totals, then the sequence word.
+  volatile unsigned long long *ph = h->plan_host;
+  for (unsigned spin = 1; ph[3] != h->plan_seq; ++spin) {
+    if ((spin & 4095) == 0) {  // the stream drained (or failed) without the word: stop polling
+      const hipError_t q = hipStreamQuery(h->stream);
+      if (q == hipErrorNotReady) continue;
+      HIP_TRY(q);
+      if (ph[3] != h->plan_seq) return fail(MRAFT_E_HIP, "append plan did not publish its totals");
+    }
+  }
+  const unsigned long long staged = ph[0], n_defer = ph[2];
+  if (n_defer > 0) {
+    if (staged > 0) {
+      TRY(scratch(h, 16, sizeof(int32_t) * (size_t)staged, &stage));
       mraft::launch_ae_stage_copy(h->dev.log_term, h->dev.log_head, h->L, (const mraft_ae_args *)a, n,
                                   (const int64_t *)soff, (int32_t *)stage, h->stream);
     }
+    mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
+                            (int64_t)staged, (const int64_t *)soff, (const int64_t *)defer, (int64_t)n_defer,
+                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
   }
-  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
-                          n_stage, (const int64_t *)soff, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
   return sg.finish();
 }
 

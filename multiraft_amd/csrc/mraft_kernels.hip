@@ -116,40 +116,169 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
 // entries_offset = source slot * L + (Index - dummy) of the first entry, a
 // logical position in that replica's ring. The reference copies args.Entries
 // when it builds the message (appendOneRound, raft_append_entry.go:50-54),
-// before any handler runs. k_ae_stage_plan decides per item:
+// before any handler runs; here they are read in place from the source ring
+// (see below for rows this batch also writes: a stale second leader).
+//
+// Messages that read the same entries (same source row, same ring position of
+// Index 0, same last Index: the P-1 messages one leader's gather makes for
+// its followers, consecutive in the batch) form a *set*, up to NI messages,
+// served by one wave with one streaming pass over the shared entries, as the
+// fused tick serves a group (mraft_pass.h). A message whose run of same-entry
+// predecessors is NI or longer is a set of its own, so membership is decided
+// from at most NI neighbours on each side.
+//
+// Entries whose source row this batch also writes must be read as they were
+// before the call. k_ae_src_mark marks every source row that is also a
+// receiving slot (claim epoch set by k_claim); the items reading such a row
+// (staged: their entries are copied out first) and the items writing one are
+// *deferred*: handled by a second launch after the main one, which touches
+// neither kind of row. The host learns whether a deferred launch is needed
+// from a readback that overlaps the main launch.
+//
+// k_ae_set_plan decides per item:
 //   soff = -1      malformed reference (MRAFT_ITEM_BAD_SLOT);
-//   soff <= -2     read in place at log word (-soff - 2): the range is
-//                  contiguous in the ring and no item of this batch writes
-//                  the source row;
-//   soff >= 0      staged at stage[soff]: the range wraps around the ring, or
-//                  the source row is also a receiving slot of this batch (a
-//                  stale second leader of the group; claim epoch set by
-//                  k_claim) and would race with that item's writes.
-// k_ae_stage_copy then copies the staged ranges, unrolling the ring.
-__global__ void k_ae_stage_plan(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L,
-                                const int32_t *__restrict__ head,
-                                const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                const int32_t *__restrict__ err, int64_t *__restrict__ soff,
-                                unsigned long long *__restrict__ total) {
+//   soff = -2      read in place through the source ring;
+//   soff >= 0      staged at stage[soff];
+// and appends every main set's first item to `sets` (first * 8 + size - 1)
+// and every deferred item to `defer` (item * 8); total = {staged words,
+// main sets, deferred items}.
+struct AeKey {
+  int64_t row;  // source slot
+  int base;     // ring position of the entries, relative: (offset mod L) - (prev + 1)
+  int end;      // Index of the last entry
+};
+
+enum : int { AK_ERR = -2, AK_BAD = -1, AK_RING = 0, AK_STAGED = 1, AK_WRITER = 2 };
+
+__device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t n_log, int L,
+                                       const unsigned long long *__restrict__ claim,
+                                       const uint32_t *__restrict__ srcmark, uint32_t epoch, AeKey &key) {
+  if (e) return AK_ERR;
+  if (a.n_entries < 0 || a.entries_offset < 0 || a.entries_offset + a.n_entries > n_log ||
+      a.entries_offset % L + a.n_entries > L)
+    return AK_BAD;
+  key.row = a.entries_offset / L;
+  key.base = (int)(a.entries_offset % L) - (a.prev_log_index + 1);
+  key.end = a.prev_log_index + a.n_entries;
+  if (a.n_entries > 0 && (uint32_t)(claim[key.row] >> 32) == epoch) return AK_STAGED;
+  if (srcmark && srcmark[a.slot] == epoch) return AK_WRITER;
+  return AK_RING;
+}
+
+// k_claim_check for AppendEntries by reference, marking the source rows
+// this batch also writes (every claim is in place: k_claim ran before).
+__global__ void k_claim_check_mark(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L,
+                                   const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                   int32_t *__restrict__ err, uint32_t *__restrict__ srcmark) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || err[i]) return;
   const mraft_ae_args a = args[i];
-  int64_t o = -1;
-  if (!err[i] && a.n_entries >= 0 && a.entries_offset >= 0 && a.entries_offset + a.n_entries <= n_log &&
-      a.entries_offset % L + a.n_entries <= L) {
-    if (a.n_entries == 0) {
-      o = -2;
-    } else {
-      const int64_t r = a.entries_offset / L;
-      const int k0 = (int)(a.entries_offset % L);
-      const int p0 = ring(k0 + head[r], L);
-      if (p0 + a.n_entries > L || (uint32_t)(claim[r] >> 32) == epoch)
-        o = (int64_t)atomicAdd(total, (unsigned long long)a.n_entries);
-      else
-        o = -(r * L + p0) - 2;
+  if (claim[a.slot] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i))) {
+    err[i] = MRAFT_ITEM_DUP_SLOT;
+    return;
+  }
+  AeKey k;
+  if (ae_kind(a, 0, n_log, L, claim, nullptr, epoch, k) == AK_STAGED) srcmark[k.row] = epoch;
+}
+
+// Appends `va` (when `wa`) to la and `vb` (when `wb`) to lb, with one
+// 64-bit atomic per workgroup on `count` (la's count in the low word).
+template <int NW>
+__device__ __forceinline__ void block_append2(bool wa, int64_t va, int64_t *__restrict__ la, bool wb, int64_t vb,
+                                              int64_t *__restrict__ lb, unsigned long long *__restrict__ count,
+                                              int *lds) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const unsigned long long ma = __ballot(wa), mb = __ballot(wb);
+  if (lane == 0) { lds[w] = __popcll(ma); lds[NW + 1 + w] = __popcll(mb); }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int ta = 0, tb = 0;
+    for (int j = 0; j < NW; ++j) {
+      const int ca = lds[j], cb = lds[NW + 1 + j];
+      lds[j] = ta; lds[NW + 1 + j] = tb;
+      ta += ca; tb += cb;
+    }
+    const unsigned long long inc = ((unsigned long long)tb << 32) | (unsigned)ta;
+    const unsigned long long base = inc ? atomicAdd(count, inc) : 0;
+    lds[NW] = (int)(base & 0xFFFFFFFFu);
+    lds[2 * NW + 1] = (int)(base >> 32);
+  }
+  __syncthreads();
+  if (wa) la[(int64_t)lds[NW] + lds[w] + __popcll(ma & ((1ull << lane) - 1))] = va;
+  if (wb) lb[(int64_t)lds[2 * NW + 1] + lds[NW + 1 + w] + __popcll(mb & ((1ull << lane) - 1))] = vb;
+}
+
+// One workgroup of kAePlanT threads plans kAeOwn items: every thread
+// classifies one item (its own or a neighbour within kAeHalo on either side)
+// into LDS, then each owned item finds its place in its run from LDS.
+constexpr int kAePlanT = 1024, kAeHalo = 7, kAeOwn = kAePlanT - 2 * kAeHalo;
+
+__global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *__restrict__ args, int64_t n,
+                                                     int64_t n_log, int L, int ni,
+                                                     const unsigned long long *__restrict__ claim,
+                                                     const uint32_t *__restrict__ srcmark, uint32_t epoch,
+                                                     const int32_t *__restrict__ err, int64_t *__restrict__ soff,
+                                                     int64_t *__restrict__ sets, int64_t *__restrict__ defer,
+                                                     unsigned long long *__restrict__ total,
+                                                     volatile unsigned long long *__restrict__ host_total,
+                                                     unsigned long long seq) {
+  constexpr int NW = kAePlanT / 64;
+  __shared__ int lds[2 * NW + 2];
+  __shared__ int kd[kAePlanT], kb[kAePlanT], ke[kAePlanT];
+  __shared__ long long kr[kAePlanT];
+  const int t = threadIdx.x;
+  const int64_t i = blockIdx.x * (int64_t)kAeOwn - kAeHalo + t;
+  AeKey k{-1, 0, 0};
+  const int kind = (i >= 0 && i < n) ? ae_kind(args[i], err[i], n_log, L, claim, srcmark, epoch, k) : -3;
+  kd[t] = kind; kr[t] = k.row; kb[t] = k.base; ke[t] = k.end;
+  __syncthreads();
+  const bool own = t >= kAeHalo && t < kAeHalo + kAeOwn && i < n;
+  if (own) {
+    int64_t o = -1;
+    if (kind == AK_STAGED) o = (int64_t)atomicAdd(&total[0], (unsigned long long)args[i].n_entries);
+    else if (kind >= AK_RING) o = -2;
+    soff[i] = o;
+  }
+  int64_t head = -1;  // first * 8 + (size - 1) when item i starts a main set
+  if (own && kind < AK_STAGED) {
+    int pos = 0;  // this item's place in its run of same-entry messages (up to ni back)
+    if (kind == AK_RING)
+      for (int d = 1; d <= ni && kd[t - d] == AK_RING && kr[t - d] == k.row && kb[t - d] == k.base &&
+                      ke[t - d] == k.end; ++d)
+        ++pos;
+    if (kind != AK_RING || pos >= ni) {
+      head = i * 8;
+    } else if (pos == 0) {
+      int cnt = 1;  // the set's size (up to ni forward)
+      for (int d = 1; d < ni && kd[t + d] == AK_RING && kr[t + d] == k.row && kb[t + d] == k.base &&
+                      ke[t + d] == k.end; ++d)
+        ++cnt;
+      head = i * 8 + (cnt - 1);
     }
   }
-  soff[i] = o;
+  block_append2<NW>(head >= 0, head, sets, own && kind >= AK_STAGED, i * 8, defer, &total[1], lds);
+  // The last workgroup to finish publishes the totals (total[4..6]: read by
+  // the handler launches; and to the host's pinned words, so the host needs
+  // no copy after this kernel) and re-arms the accumulators for the next call.
+  // No fence: the totals are device-coherent atomics, this workgroup's were
+  // performed before its `done` increment (their results were awaited), and
+  // the handler reads the lists after this kernel ends. (A device-scope fence
+  // here writes back the XCD's L2 per workgroup: +23 us.)
+  if (threadIdx.x == 0) {
+    if (atomicAdd(&total[3], 1ull) == gridDim.x - 1) {
+      const unsigned long long staged = atomicAdd(&total[0], 0ull), both = atomicAdd(&total[1], 0ull);
+      const unsigned long long v[3] = {staged, both & 0xFFFFFFFFull, both >> 32};
+      for (int j = 0; j < 3; ++j) {
+        total[4 + j] = v[j];
+        host_total[j] = v[j];
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the totals' stores complete before the sequence word's
+      host_total[3] = seq;            // the host polls this word
+      total[0] = 0;
+      total[1] = 0;
+      total[3] = 0;
+    }
+  }
 }
 
 __global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const int32_t *__restrict__ head, int L,
@@ -164,137 +293,241 @@ __global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const int32_t *
   wave_copy_from_ring(log + r * L, 0, head[r], L, (int)(a.entries_offset % L), stage + o, a.n_entries);
 }
 
-__global__ __launch_bounds__(64 * MRAFT_AE_WPB) void k_handle_ae(Dev s, const mraft_ae_args *__restrict__ args,
-                                                   int64_t n, const int32_t *__restrict__ ent0,
-                                                   int64_t n_ent0, const int32_t *__restrict__ stage,
-                                                   int64_t n_stage, const int64_t *__restrict__ soff,
-                                                   mraft_ae_reply *__restrict__ rep,
-                                                   int32_t *__restrict__ err) {
-  int64_t gb = blockIdx.x;
-  if (MRAFT_AE_XCD) {
-    const int64_t nb = gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
-    gb = x * per + min(x, rem) + (gb >> 3);
-  }
-  const int64_t i = gb * MRAFT_AE_WPB + (threadIdx.x >> 6);
-  if (i >= n) return;
+// a4, HandleAppendEntries (raft_append_entry.go:108-162, matchLog
+// raft_log.go:92-96) for one set of messages per wave: lane q < size takes
+// message first+q's prologue (its args, the receiving follower's scalars,
+// log[prev]); conflict scans run wave-wide one message at a time; every
+// merging message joins one streaming pass over the shared entries
+// (mraft_pass.h). `sets` NULL: message i = workgroup i, a set of one (entries
+// from a host buffer).
+enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE };
+
+#ifndef MRAFT_AE_MINW
+#define MRAFT_AE_MINW 8  // __launch_bounds__ minimum waves per SIMD of the handler
+#endif
+#ifndef MRAFT_AE_SPB
+#define MRAFT_AE_SPB 4  // main launch: grid = the item count / this (sets per workgroup at most)
+#endif
+#ifndef MRAFT_AE_STASH
+#define MRAFT_AE_STASH 1  // park the per-lane reply inputs in LDS across the pass
+#endif
+
+template <int NI>
+__device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__restrict__ args,
+                                           const int32_t *__restrict__ ent0, int64_t n_ent0,
+                                           const int32_t *__restrict__ stage, int64_t n_stage,
+                                           const int64_t *__restrict__ soff, int64_t first, int size,
+                                           mraft_ae_reply *__restrict__ rep, int32_t *__restrict__ err) {
   const int lane = lane_id();
-  mraft_ae_reply r = {0, 0, 0, 0};
-  // Three round trips before the merge: the item (error word and args
-  // together), the follower's scalars (one load per lane), log[prev].
-  const int e = err[i];
+  const bool mine = lane < size;
+  const int64_t i = first + (mine ? lane : 0);
+  // Three round trips before the pass: the item (error word, args, plan),
+  // the follower's scalars, log[prev].
+  const int e = mine ? err[i] : 1;
   mraft_ae_args a = args[i];
   const int64_t so = soff ? soff[i] : -1;
-  // All loads in flight before the branch (else the compiler sinks the args
-  // load behind the error check: one more round trip).
   asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
                "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so));
-  const int32_t *__restrict__ ent = ent0;
+  const int L = s.L;
+  // Where the entries are: Index x of this lane's message at src.at(x).
+  RingRow src{ent0, 0, 0, INT32_MAX};
   int64_t n_ent = n_ent0;
-  if (soff) {  // entries by reference: where k_ae_stage_plan put them
-    if (so >= 0) {
-      ent = stage;
-      n_ent = n_stage;
-      a.entries_offset = so;
-    } else if (so <= -2) {
-      a.entries_offset = -so - 2;
+  bool ok = true;
+  if (e) {
+  } else if (!soff) {   // host buffer
+    src.row = a.entries_offset - (a.prev_log_index + 1);
+  } else if (so >= 0) { // staged copy
+    src.p = stage;
+    n_ent = n_stage;
+    src.row = so - (a.prev_log_index + 1);
+    a.entries_offset = so;
+  } else if (so == -2) { // in place through the source ring
+    const int64_t r = a.entries_offset / L;
+    src.p = s.log;
+    src.row = r * L;
+    src.L = L;
+    src.base = s.head[r] + (int)(a.entries_offset % L) - (a.prev_log_index + 1);
+    n_ent = INT64_MAX;
+  } else {
+    ok = false;          // malformed reference
+  }
+  int cls = e ? AE_NONE : AE_DONE;
+  if (!e && (!ok || a.n_entries < 0 || a.entries_offset < 0 ||
+             (a.n_entries > 0 && so != -2 && a.entries_offset + a.n_entries > n_ent)))
+    cls = AE_BAD;
+  int f = a.slot;
+  const int prev = a.prev_log_index, nn = a.n_entries;
+  const bool live = cls == AE_DONE;
+  int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
+  if (live) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
+  mraft_ae_reply r = {0, 0, 0, 0};
+  int ftp = 0;
+  if (live) {
+    if (a.term < fterm) {                                              // :112-115
+      cls = AE_STALE;
+      r.term = fterm;
+    } else if (prev < fdummy) {                                        // :123-127
+      cls = AE_BELOW;
+      r.conflict_index = fdummy + 1;
     } else {
-      a.n_entries = -1;  // malformed reference: MRAFT_ITEM_BAD_SLOT below
+      ftp = prev > flast ? 0 : s.log[(int64_t)f * L + ring(prev - fdummy + fhead, L)];
+      if (prev > flast || ftp != a.prev_log_term) {                    // matchLog, raft_log.go:92-96
+        cls = AE_MISS;
+        r.term = a.term;
+        if (prev > flast) r.conflict_index = flast + 1;                // :131-133
+        else r.conflict_index = prev;                                  // :136-142 below when prev > dummy + 1
+      } else {
+        cls = AE_MERGE;
+      }
     }
   }
-  if (e) {
-    if (lane == 0) rep[i] = r;
-    return;
+  // :136-142, the ConflictIndex scan, wave-wide for one message at a time
+  for (unsigned long long m = __ballot(cls == AE_MISS && prev <= flast && prev > fdummy + 1); m; m &= m - 1) {
+    const int q = first_lane(m);
+    const int qf = __shfl(f, q, 64), qd = __shfl(fdummy, q, 64), qh = __shfl(fhead, q, 64),
+              qp = __shfl(prev, q, 64), qa = __shfl(ftp, q, 64);
+    const int ci = wave_conflict_scan(s.log + (int64_t)uni(qf) * L, uni(qd), uni(qh), L, uni(qp), uni(qa));
+    if (lane == q) r.conflict_index = ci;
   }
-  const int L = s.L;
-  if (a.n_entries < 0 || a.entries_offset < 0 ||
-      (a.n_entries > 0 && a.entries_offset + a.n_entries > n_ent)) {
-    if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_BAD_SLOT; }
-    return;
-  }
-  const int f = a.slot, prev = a.prev_log_index, nn = a.n_entries;
-  const int32_t *sa = lane == 0 ? s.term : lane == 1 ? s.dummy : lane == 2 ? s.last : lane == 3 ? s.commit : s.head;
-  const int sv = lane < 5 ? sa[f] : 0;
-  const int fterm = __builtin_amdgcn_readlane(sv, 0), fdummy = __builtin_amdgcn_readlane(sv, 1),
-            flast = __builtin_amdgcn_readlane(sv, 2), fc = __builtin_amdgcn_readlane(sv, 3),
-            fhead = __builtin_amdgcn_readlane(sv, 4);
-  if (a.term < fterm) {                                                // :112-115
-    r.term = fterm;
-    if (lane == 0) { rep[i] = r; mark_persist(s, f, MRAFT_PERSIST_STATE); }  // deferred :111
-    return;
-  }
-  const bool adopt = a.term > fterm;                                   // :116-118
-  const int32_t *frow = s.log + (int64_t)f * L;
-  bool write_state = true;
+  // :146-155 through the streaming pass the tick uses: compare entries with
+  // every merging follower's terms, truncate-and-append from the first
+  // mismatch. All messages of a set end at the same Index (AeKey).
   int newlast = -1, fcommit_new = -1;
-  if (prev < fdummy) {                                                 // :123-127
-    r.term = 0; r.conflict_index = fdummy + 1;
-  } else {
-    const int ftp = prev > flast ? 0 : frow[ring(prev - fdummy + fhead, L)];
-    if (prev > flast || ftp != a.prev_log_term) {                      // matchLog, raft_log.go:92-96
-      r.term = a.term;
-      if (prev > flast) r.conflict_index = flast + 1;                  // :131-133
-      else if (prev > fdummy + 1)
-        r.conflict_index = wave_conflict_scan(frow, fdummy, fhead, L, prev, ftp);  // :136-142
-      else r.conflict_index = prev;
+  const int merge_m = (int)(__ballot(cls == AE_MERGE) & ((1ull << NI) - 1));
+  if (merge_m) {
+    Fol<NI, true> fo;
+    fo.log = s.log;
+    fo.slot0 = 0;
+    fo.skip = NI;
+    fo.L = L;
+    fo.cmp = merge_m;
+    fo.copy = 0;
+    fo.capok = (int)(__ballot(cls == AE_MERGE && (int64_t)prev + nn - fdummy <= (int64_t)L - 1) & ((1ull << NI) - 1));
+    fo.full = 0;
+    const int phi = uni(__shfl(prev + nn, first_lane((unsigned long long)merge_m), 64)), nend = phi + 1;
+    int plo = phi + 1;
+    // the source as the first merging message sees it (the same for every message of a set)
+    const int q0 = first_lane((unsigned long long)merge_m);
+    RingRow ss;
+    {
+      const uint64_t pa = (uint64_t)(uintptr_t)src.p;
+      const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)pa, q0, 64), hi = (uint32_t)__shfl((int)(pa >> 32), q0, 64);
+      ss.p = (const int32_t *)(uintptr_t)(((uint64_t)uni((int)hi) << 32) | (uint32_t)uni((int)lo));
+      const uint64_t ra = (uint64_t)src.row;
+      const uint32_t rlo = (uint32_t)__shfl((int)(uint32_t)ra, q0, 64), rhi = (uint32_t)__shfl((int)(ra >> 32), q0, 64);
+      ss.row = (long long)(((uint64_t)uni((int)rhi) << 32) | (uint32_t)uni((int)rlo));
+      ss.base = uni(__shfl(src.base, q0, 64));
+      ss.L = uni(__shfl(src.L, q0, 64));
+    }
+    bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      fo.slot[q] = uni(__shfl(f, q, 64));
+      const int sp = uni(__shfl(prev, q, 64)), sl = uni(__shfl(flast, q, 64));
+      fo.base[q] = uni(__shfl(fhead - fdummy, q, 64));
+      fo.start[q] = sp + 1;
+      fo.cend[q] = min(phi, sl) + 1;
+      fo.cfrom[q] = 0;
+      if ((merge_m >> q) & 1) {
+        plo = min(plo, sp + 1);
+        // dwordx4 when the entries and this follower's row are 16-B aligned alike
+        vec = vec && ((((uintptr_t)ss.at(sp + 1) ^ (uintptr_t)fo.at(q, sp + 1)) & 15) == 0);
+      }
+    }
+    if (ss.L == INT32_MAX)  // a flat buffer: every dwordx4 read must stay inside it
+      vec = vec && (((uintptr_t)ss.at(plo)) & ~(uintptr_t)15) >= (uintptr_t)ss.p &&
+            (((uintptr_t)ss.at(phi)) | 15) < (uintptr_t)(ss.p + n_ent);
+    int found = -1;
+#if MRAFT_AE_STASH
+    // This lane's reply inputs wait in LDS during the pass (the pass needs
+    // the registers: at 8 waves per SIMD they would spill to scratch).
+    __shared__ int stash[8][64];
+    {
+      volatile int *st = &stash[0][0];
+      st[0 * 64 + lane] = cls; st[1 * 64 + lane] = f; st[2 * 64 + lane] = fterm; st[3 * 64 + lane] = flast;
+      st[4 * 64 + lane] = fc; st[5 * 64 + lane] = a.term; st[6 * 64 + lane] = a.leader_commit;
+      st[7 * 64 + lane] = r.conflict_index;
+    }
+#endif
+    if (vec) {
+      int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
+      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+      copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
     } else {
-      // :146-155 through the streaming pass the tick uses (mraft_pass.h):
-      // compare entries with the follower's terms, truncate-and-append from
-      // the first mismatch; dwordx4 when entries and row are 16-B aligned
-      // alike and every vector read stays inside its buffer.
-      const long long eo = a.entries_offset - (long long)(prev + 1);    // entry Index x -> ent[eo + x]
-      const LinRow src{ent, eo};
-      const int plo = prev + 1, phi = prev + nn, nend = prev + nn + 1;
-      Fol<1> fo;  // the receiving follower's ring
-      fo.log = s.log;
-      fo.slot0 = f;
-      fo.skip = 1;
-      fo.L = L;
-      fo.base[0] = fhead - fdummy;
-      fo.start[0] = plo;
-      fo.cend[0] = min(phi, flast) + 1;
-      fo.cfrom[0] = 0;
-      fo.cmp = 1;
-      fo.copy = 0;
-      fo.capok = (int64_t)prev + nn - fdummy <= (int64_t)L - 1 ? 1 : 0;
-      fo.full = 0;
-      int found = -1;
-      const uintptr_t ea = (uintptr_t)(ent + eo + plo), fa = (uintptr_t)fo.at(0, plo);
-      const bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0 && ((ea ^ fa) & 15) == 0 &&
-                       (ea & ~(uintptr_t)15) >= (uintptr_t)ent &&
-                       ((uintptr_t)(ent + eo + phi) | 15) < (uintptr_t)(ent + n_ent);
-      if (vec) {
-        int c = plo - (int)((ea >> 2) & 31);                           // 128-B aligned chunks
-        for (; c <= phi && fo.cmp; c += 256)
-          pass_chunk<1, 1, true, false>(src, fo, nend, 1, 0, 0, found, c, plo, phi);
-        copy_loop<1, true, false>(src, fo, c, nend, plo, phi, 1, 0, 0, found);
+      int c = plo;
+      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+      copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
+    }
+#if MRAFT_AE_STASH
+    {
+      volatile int *st = &stash[0][0];
+      cls = st[0 * 64 + lane]; f = st[1 * 64 + lane]; fterm = st[2 * 64 + lane]; flast = st[3 * 64 + lane];
+      fc = st[4 * 64 + lane]; a.term = st[5 * 64 + lane]; a.leader_commit = st[6 * 64 + lane];
+      r.conflict_index = st[7 * 64 + lane];
+    }
+#endif
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (lane != q || cls != AE_MERGE) continue;
+      if ((fo.full >> q) & 1) {
+        cls = AE_DONE;                                                 // engine capacity: no state change
+        err[i] = MRAFT_ITEM_LOG_FULL;
+        rep[i] = r;
       } else {
-        int c = plo;
-        for (; c <= phi && fo.cmp; c += 256)
-          pass_chunk<1, 1, false, false>(src, fo, nend, 1, 0, 0, found, c, plo, phi);
-        copy_loop<1, false, false>(src, fo, c, nend, plo, phi, 1, 0, 0, found);
-      }
-      int last_after = flast;
-      if (fo.full) {
-        write_state = false;                                           // engine capacity
-        if (lane == 0) { rep[i] = r; err[i] = MRAFT_ITEM_LOG_FULL; }
-      } else if (fo.cfrom[0] > 0) {                                       // truncated and appended
-        newlast = prev + nn;
-        last_after = newlast;
-      }
-      if (write_state) {
+        int last_after = flast;
+        if (fo.cfrom[q] > 0) newlast = last_after = phi;               // truncated and appended
         if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160
         r.term = a.term; r.success = 1;                                // :161
       }
     }
   }
-  if (!write_state) return;
-  if (lane == 0) {
-    if (adopt) { s.term[f] = a.term; s.voted[f] = -1; }
+  if (cls == AE_NONE) {
+    if (mine) rep[i] = r;
+  } else if (cls == AE_BAD) {
+    rep[i] = r;
+    err[i] = MRAFT_ITEM_BAD_SLOT;
+  } else if (cls == AE_STALE) {
+    rep[i] = r;
+    mark_persist(s, f, MRAFT_PERSIST_STATE);                           // deferred :111
+  } else if (cls >= AE_BELOW) {
+    if (a.term > fterm) { s.term[f] = a.term; s.voted[f] = -1; }      // :116-118
     s.role[f] = kFollower;                                             // :120
     if (newlast >= 0) s.last[f] = newlast;
     if (fcommit_new >= 0) s.commit[f] = fcommit_new;
     mark_persist(s, f, MRAFT_PERSIST_STATE);                           // deferred :111
     rep[i] = r;
+  }
+}
+
+// The grid may be sized by an upper bound: set_count holds the number of
+// sets on the device, and a workgroup serves sets blockIdx, blockIdx + grid,
+// ... (grid a multiple of 8: each XCD keeps its contiguous range of sets,
+// neighbouring sets share one L2).
+template <int NI>
+__global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(Dev s, const mraft_ae_args *__restrict__ args,
+                                                                  int64_t n, const int32_t *__restrict__ ent0,
+                                                                  int64_t n_ent0, const int32_t *__restrict__ stage,
+                                                                  int64_t n_stage, const int64_t *__restrict__ soff,
+                                                                  const int64_t *__restrict__ sets, int64_t n_sets,
+                                                                  const unsigned long long *__restrict__ set_count,
+                                                                  mraft_ae_reply *__restrict__ rep,
+                                                                  int32_t *__restrict__ err) {
+  const int64_t nb = sets ? (set_count ? (int64_t)*set_count : n_sets) : n;
+  for (int64_t v = blockIdx.x;; v += gridDim.x) {
+    int64_t gb = v;
+    if (MRAFT_AE_XCD) {
+      const int64_t x = v & 7, per = nb >> 3, rem = nb & 7, j = v >> 3;
+      if (j >= per + (x < rem ? 1 : 0)) return;
+      gb = x * per + min(x, rem) + j;
+    } else if (v >= nb) {
+      return;
+    }
+    if (sets) {
+      const int64_t h = sets[gb];
+      handle_one<NI>(s, args, ent0, n_ent0, stage, n_stage, soff, h >> 3, (int)(h & 7) + 1, rep, err);
+    } else {
+      handle_one<NI>(s, args, ent0, n_ent0, stage, n_stage, soff, gb, 1, rep, err);
+    }
   }
 }
 
@@ -1003,11 +1236,25 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
                      out, err);
 }
 
-void launch_ae_stage_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, const int32_t *head,
-                          const unsigned long long *claim, uint32_t epoch, const int32_t *err,
-                          int64_t *soff, unsigned long long *total, hipStream_t st) {
-  hipLaunchKernelGGL(k_ae_stage_plan, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, head, claim,
-                     epoch, err, soff, total);
+void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp,
+                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_claim, dim3(blocks_for(n)), dim3(kBlock), 0, st, (const char *)args, n,
+                     (int)sizeof(mraft_ae_args), (int)offsetof(mraft_ae_args, slot), (const int64_t *)nullptr, gp, 0,
+                     claim, epoch, err);
+  hipLaunchKernelGGL(k_claim_check_mark, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, claim, epoch,
+                     err, srcmark);
+}
+
+void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
+                        const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
+                        const int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
+                        unsigned long long *total, unsigned long long *host_total, unsigned long long seq,
+                        hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_ae_set_plan, dim3(blocks_for(n, kAeOwn)), dim3(kAePlanT), 0, st, args, n, n_log, L,
+                     ni < 1 ? 1 : ni > kAeHalo ? kAeHalo : ni, claim, srcmark, epoch, err, soff, sets, defer, total,
+                     host_total, seq);
 }
 
 void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
@@ -1016,12 +1263,31 @@ void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const 
                      stage);
 }
 
-void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent,
-                      int64_t n_ent, const int32_t *stage, int64_t n_stage, const int64_t *soff,
-                      mraft_ae_reply *rep, int32_t *err, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_handle_ae, dim3(blocks_for(n, MRAFT_AE_WPB)), dim3(64 * MRAFT_AE_WPB), 0, st, s, args, n,
-                     ent, n_ent, stage, n_stage, soff, rep, err);
+template <int NI>
+static void launch_set(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
+                       const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
+                       int64_t n_sets, const unsigned long long *set_count, mraft_ae_reply *rep, int32_t *err,
+                       hipStream_t st) {
+  // with the count on the device, n_sets is an upper bound: a workgroup per
+  // MRAFT_AE_SPB sets of the bound (grid a multiple of 8, see k_handle_set)
+  int64_t nb = sets ? n_sets : n;
+  if (set_count) nb = ((nb + MRAFT_AE_SPB - 1) / MRAFT_AE_SPB + 7) / 8 * 8;
+  hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, s, args, n, ent, n_ent, stage, n_stage,
+                     soff, sets, n_sets, set_count, rep, err);
+}
+
+void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
+                      const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
+                      int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
+                      int32_t *err, hipStream_t st) {
+  if (n <= 0 || (sets && n_sets <= 0)) return;
+#define MRAFT_SET_CASE(k) \
+  case k: launch_set<k>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, st); break;
+  switch (sets ? ni : 1) {
+    MRAFT_SET_CASE(1) MRAFT_SET_CASE(2) MRAFT_SET_CASE(3) MRAFT_SET_CASE(4) MRAFT_SET_CASE(5) MRAFT_SET_CASE(6)
+    default: launch_set<7>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, st);
+  }
+#undef MRAFT_SET_CASE
 }
 
 #if MRAFT_FOLD_TRACE

@@ -28,10 +28,10 @@ struct LinRow {
 // it), so idx + base >= 0 there and only the upper wrap is needed; masked
 // lanes may form any address, they never dereference it.
 struct RingRow {
-  int32_t *p;
+  const int32_t *p;
   long long row;
   int base, L;
-  __device__ __forceinline__ int32_t *at(int idx) const {
+  __device__ __forceinline__ const int32_t *at(int idx) const {
     const int k = idx + base;
     return p + row + (k >= L ? k - L : k);
   }
@@ -72,23 +72,26 @@ __device__ __forceinline__ void st1(int32_t *p, int a) {
 
 // The followers a pass serves, with as little wave-uniform state as the pass
 // needs (it is live across the whole streaming loop; at 8 waves per SIMD every
-// scalar held here is one the compiler would otherwise spill): follower q's
-// replica slot is slot0 + q, skipping `skip` (the leader's peer index in the
-// tick), so no 64-bit row offsets are held; its mode is two bits (cmp: still
+// scalar held here is one the compiler would otherwise spill): in the tick,
+// follower q's replica slot is slot0 + q, skipping `skip` (the leader's peer
+// index), so no 64-bit row offsets are held; the message handler (SLOTS)
+// names each receiving slot. A follower's mode is two bits (cmp: still
 // comparing; copy: copying from cfrom on; neither: done); capok (the append
 // fits the capacity) and full (rejected as MRAFT_ITEM_LOG_FULL) are bits too.
-template <int NI>
+template <int NI, bool SLOTS = false>
 struct Fol {
+  static constexpr int kNI = NI;
   int32_t *log;
   long long slot0;
   int skip, L;
+  int slot[SLOTS ? NI : 1];  // SLOTS: follower q's replica slot
   int base[NI];   // ring base: head - dummy (include/mraft.h)
   int start[NI];  // first compared Index (prev + 1)
   int cend[NI];   // compared while the follower has the Index: [start, cend)
   int cfrom[NI];  // first mismatching Index (copy from here)
   int cmp, copy, capok, full;
   __device__ __forceinline__ int32_t *at(int q, int idx) const {
-    const long long row = (slot0 + q + (q >= skip ? 1 : 0)) * (long long)L;
+    const long long row = (SLOTS ? (long long)slot[SLOTS ? q : 0] : slot0 + q + (q >= skip ? 1 : 0)) * (long long)L;
     const int k = idx + base[q];  // >= 0 for every lane that loads or stores (see RingRow)
     return log + row + (k >= L ? k - L : k);
   }
@@ -111,9 +114,10 @@ struct Fol {
 // VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
 // otherwise lane j owns c+64(4v+u)+j. Entry idx is at src.at(idx), follower
 // q's term of Index idx at fo.at(q, idx).
-template <int NI, int V, bool VEC, bool COUNT, class Src>
-__device__ __forceinline__ void pass_chunk(const Src &src, Fol<NI> &fo, int nend, int slo, int shi, int T,
+template <int V, bool VEC, bool COUNT, class Src, class F>
+__device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int slo, int shi, int T,
                                            int &found, int c, int plo, int phi) {
+  constexpr int NI = F::kNI;
   constexpr int CW = 256 * V;
   const int lane = lane_id();
   int idx[V][4], e[V][4];
@@ -249,9 +253,10 @@ __device__ __forceinline__ void pass_chunk(const Src &src, Fol<NI> &fo, int nend
 // the loop will run for it: no extra traffic. (Two chunks ahead,
 // MRAFT_COPY_PIPE=2, measured no faster: the copy is memory-system-bound at 8
 // waves per SIMD, profiles/r2_experiments.)
-template <int NI, bool VEC, bool COUNT, class Src>
-__device__ __forceinline__ void copy_loop(const Src &src, const Fol<NI> &fo, int c, int nend, int plo, int phi,
+template <bool VEC, bool COUNT, class Src, class F>
+__device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, int nend, int plo, int phi,
                                           int slo, int shi, int T, int &found) {
+  constexpr int NI = F::kNI;
   constexpr int CW = 256;
   const int lane = lane_id();
   int cmask = fo.copy;

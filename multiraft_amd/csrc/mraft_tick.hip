@@ -465,13 +465,13 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (vec) {
       int c = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
       for (; c <= phi && fo.cmp; c += 256 * V)
-        pass_chunk<NI, V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      copy_loop<NI, true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
+        pass_chunk<V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+      copy_loop<true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     } else {
       int c = plo;
       for (; c <= phi && fo.cmp; c += 256 * V)
-        pass_chunk<NI, V, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      copy_loop<NI, false, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
+        pass_chunk<V, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+      copy_loop<false, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     }
   }
   TICK_STAMP(2);

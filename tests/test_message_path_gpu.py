@@ -98,3 +98,61 @@ def test_stale_second_leader_by_reference_gpu():
     with Engine(G, P, L) as e:
         e.load_state(st)
         _message_round(e, o, st, slots, peers, G, P, L, "reference", assert_states_equal)
+
+
+def _cross_group_runs(args, ok, G, P, rng, run):
+    """By-reference messages whose entries are shared by long runs: each
+    gathered message is repeated `run` times, each copy addressed to a distinct
+    receiving slot of another group (longer than a set: the plan must split
+    the run), the batch then interleaved with messages of other sources."""
+    a = args[ok]
+    used = set(a["slot"].tolist())
+    free = [s for s in rng.permutation(G * P).tolist() if s not in used]
+    out = []
+    for k in range(0, len(a), 5):
+        for j in range(run):
+            if not free:
+                break
+            m = a[k].copy()
+            m["slot"] = free.pop()
+            out.append(m)
+    return np.array(out, dtype=args.dtype)
+
+
+@pytest.mark.parametrize("order", ["gathered", "shuffled", "long_runs", "with_errors"])
+def test_handle_sets_gpu(order):
+    """Message sets (messages reading the same entries, one wave each) in
+    every arrangement the plan must cut correctly: the gather's own order
+    (one set per leader), shuffled (sets of one), runs longer than a set,
+    and runs broken by duplicate-slot and malformed messages."""
+    G, P, L = 512, 5, 256
+    rng = np.random.default_rng(7 + len(order))
+    st, lp, _ = synth_tick_state(G, P, L, seed=303)
+    slots, peers = all_follower_items(lp, G, P)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        args, gerr = e.gather_append_args(slots, peers)
+        ok = gerr == 0
+        if order == "gathered":
+            batch = args[ok]
+        elif order == "shuffled":
+            batch = args[ok][rng.permutation(int(ok.sum()))]
+        elif order == "long_runs":
+            batch = _cross_group_runs(args, ok, G, P, rng, 11)
+        else:
+            batch = args[ok].copy()
+            dup = rng.choice(len(batch), len(batch) // 9, replace=False)
+            for j in dup:
+                batch[j]["slot"] = batch[(j + 2) % len(batch)]["slot"]   # a duplicate receiving slot
+            bad = rng.choice(len(batch), len(batch) // 13, replace=False)
+            batch["entries_offset"][bad] = -5                              # malformed reference
+            zero = rng.choice(len(batch), len(batch) // 11, replace=False)
+            batch["n_entries"][zero] = 0
+        rep, herr = e.handle_append_entries(batch, None)
+        orep, oherr = o.handle_append_entries(batch, None)
+        assert np.array_equal(herr, oherr)
+        assert np.array_equal(rep, orep)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"sets ({order})")
+        if order == "with_errors":
+            assert (herr != 0).any() and (herr == 0).any()
