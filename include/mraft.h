@@ -132,9 +132,9 @@ typedef struct {
   int32_t *persist_dirty; /* MRAFT_PERSIST_* bits: persist() call sites run
                              since the last mraft_collect_persist (below)  */
   int32_t *log_head;      /* ring position of the dummy entry, in [0, L)    */
-  int32_t *has_snapshot;  /* hasSnapshot (raft.go:158,168-177): set by an
+  int32_t *has_snapshot;  /* hasSnapshot (raft.go:36,157,168-177): set by an
                              installing HandleInstallSnapshot
-                             (raft_snapshot.go:52), consumed by the applier */
+                             (raft_snapshot.go:49), consumed by the applier */
 } mraft_soa;
 
 /* Persistence (SURVEY.md §5 "Checkpoint / resume", §8f #4). The reference
@@ -371,7 +371,7 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts,
 /* Applier (raft.go:153-203): for every slot, in the order the reference
  * sends them on applyCh,
  *   1. when hasSnapshot is set (an InstallSnapshot installed since the last
- *      call, raft_snapshot.go:52): the SnapshotValid message (:168-177),
+ *      call, raft_snapshot.go:49): the SnapshotValid message (:168-177),
  *      out_snap_index = SnapshotIndex = dummyIndex, out_snap_term =
  *      SnapshotTerm = dummyTerm, and hasSnapshot is cleared; otherwise
  *      out_snap_index = -1 (the host delivers the snapshot bytes it saved);
