@@ -59,6 +59,149 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
+    """The survey's other configurations, measured in the same run so they are
+    on the driver's record (rank 0, one GPU, after the headline's timed
+    region; never part of `value`):
+      * the message-level path at config #3 (gather -> handle by reference ->
+        fold) on a fresh copy per step, with the handler's
+        roofline from its algorithmic bytes (tools/msg_words.py);
+      * config #5, the election storm (65,536 x 7, 64 rounds per launch);
+      * config #2 (1,024 x 3 x 256: cache-resident, launch-bound).
+    Each timed with HIP events on the engine's stream; `copy` is a state copy
+    the headline already used, restored from `master` before every step."""
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, _abi, synth_election_state, synth_seed, synth_tick_state
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from msg_words import handle_words
+
+    out = {}
+    lib = _abi.lib()
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    def ck(rc, what):
+        assert rc == 0, (what, _abi.last_error())
+
+    # -- message-level path, config #3
+    eng = Engine(G, P, L, device=dev.index or 0, alloc=False)
+    eng.set_stream(stream.cuda_stream)
+    ldr = (np.arange(G) * P + lp).repeat(P - 1).astype(np.int32)
+    q = np.tile(np.arange(P - 1), G)
+    peers = np.where(q < np.repeat(lp, P - 1), q, q + 1).astype(np.int32)
+    keep = np.repeat(lp >= 0, P - 1)
+    ldr, peers = ldr[keep], peers[keep]
+    n = len(ldr)
+    slots_d, peers_d = torch.from_numpy(ldr).to(dev), torch.from_numpy(peers).to(dev)
+    args = torch.zeros((n, 10), dtype=torch.int32, device=dev)
+    gerr, herr, ferr, flags = (torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(4))
+    rep = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+    res = torch.zeros((n, 8), dtype=torch.int32, device=dev)
+    seg = torch.from_numpy(np.concatenate([[0], np.cumsum(np.bincount(ldr // P, minlength=G)[lp >= 0])])
+                           .astype(np.int64)).to(dev)
+    t_call = {"gather": [], "handle": [], "fold": []}
+    hw = None
+    for i in range(steps + 1):
+        for k, v in master.items():
+            copy[k].copy_(v)
+        eng.bind(copy)
+        e = [ev() for _ in range(6)]
+        e[0].record(stream)
+        ck(lib.mraft_gather_append_args(eng._h, slots_d.data_ptr(), peers_d.data_ptr(), n, args.data_ptr(),
+                                        gerr.data_ptr(), DEVICE), "gather")
+        e[1].record(stream)
+        e[2].record(stream)
+        ck(lib.mraft_handle_append_entries(eng._h, args.data_ptr(), n, None, 0, rep.data_ptr(), herr.data_ptr(),
+                                           DEVICE), "handle")
+        e[3].record(stream)
+        res[:, 0], res[:, 1], res[:, 2], res[:, 3], res[:, 4] = slots_d, peers_d, args[:, 1], args[:, 3], args[:, 6]
+        res[:, 5:8] = rep[:, 0:3]
+        e[4].record(stream)
+        ck(lib.mraft_process_append_replies(eng._h, res.data_ptr(), n, seg.data_ptr(), len(seg) - 1,
+                                            flags.data_ptr(), ferr.data_ptr(), DEVICE), "fold")
+        e[5].record(stream)
+        torch.cuda.synchronize()
+        if i == 0:  # the first pass is warm-up; its inputs give the algorithmic bytes
+            assert int(gerr.abs().sum()) == 0 and int(herr.abs().sum()) == 0 and int(ferr.abs().sum()) == 0
+            host = {k: v.cpu().numpy() for k, v in master.items()}
+            hw = handle_words(host, args.cpu().numpy().view(_abi.AE_ARGS).reshape(-1),
+                              rep.cpu().numpy().view(_abi.AE_REPLY).reshape(-1), herr.cpu().numpy(), G, P, L)
+            del host
+            continue
+        t_call["gather"].append(e[0].elapsed_time(e[1]))
+        t_call["handle"].append(e[2].elapsed_time(e[3]))
+        t_call["fold"].append(e[4].elapsed_time(e[5]))
+    ms = {k: float(np.mean(v)) for k, v in t_call.items()}
+    step_ms = sum(ms.values())
+    hb = 4 * hw["words"]
+    out["message_path_config3"] = {
+        "workload": "config #3 message-level path: gather -> HandleAppendEntries (entries by reference, "
+                    "message sets) -> processAppendEntriesReply + advanceCommitIndex, fresh copy per step",
+        "messages": n, "steps": steps, "ms_per_call": {k: round(v, 4) for k, v in ms.items()},
+        "decisions_per_s": G / (step_ms / 1e3),
+        "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
+                     "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
+                     "sets": hw["sets"], "merges": hw["merges"]}}
+    eng.close()
+
+    # -- config #5 election storm
+    Ge, Pe, R = 65536, 7, 64
+    st5, mask = synth_election_state(Ge, Pe, 8, seed=synth_seed(5), rounds=R)
+    m5 = {k: torch.from_numpy(v).to(dev) for k, v in st5.items()}
+    c5 = {k: v.clone() for k, v in m5.items()}
+    mask_d = torch.from_numpy(mask).to(dev)
+    e5 = Engine(Ge, Pe, 8, device=dev.index or 0, alloc=False)
+    e5.set_stream(stream.cuda_stream)
+    gf5 = torch.zeros(Ge, dtype=torch.int32, device=dev)
+    t5 = []
+    for i in range(steps + 1):
+        for k, v in m5.items():
+            c5[k].copy_(v)
+        e5.bind(c5)
+        a, b = ev(), ev()
+        a.record(stream)
+        e5.election_rounds(mask_d, gf5, where=DEVICE)
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i:
+            t5.append(a.elapsed_time(b))
+    out["election_storm_config5"] = {
+        "workload": "config #5: 65,536 groups x 7 peers, 64 election rounds per launch (mraft_election_rounds)",
+        "kernel_ms_mean": float(np.mean(t5)), "group_rounds_per_s": Ge * R / (float(np.mean(t5)) / 1e3),
+        "groups_with_new_leader": int(((gf5.cpu().numpy() & 128) != 0).sum()), "bound": "valu"}
+    e5.close()
+
+    # -- config #2
+    G2, P2, L2 = 1024, 3, 256
+    st2, lp2, _ = synth_tick_state(G2, P2, L2, seed=synth_seed(2))
+    m2 = {k: torch.from_numpy(v).to(dev) for k, v in st2.items()}
+    c2 = {k: v.clone() for k, v in m2.items()}
+    lp2_d = torch.from_numpy(lp2).to(dev)
+    e2 = Engine(G2, P2, L2, device=dev.index or 0, alloc=False)
+    e2.set_stream(stream.cuda_stream)
+    gf2 = torch.zeros(G2, dtype=torch.int32, device=dev)
+    t2 = []
+    for i in range(4 * steps + 1):
+        for k, v in m2.items():
+            c2[k].copy_(v)
+        e2.bind(c2)
+        a, b = ev(), ev()
+        a.record(stream)
+        e2.replicate_tick(lp2_d, gf2, where=DEVICE)
+        b.record(stream)
+        torch.cuda.synchronize()
+        if i:
+            t2.append(a.elapsed_time(b))
+    out["tick_config2"] = {
+        "workload": "config #2: 1,024 groups x 3 peers x 256-entry logs (cache-resident, launch-bound)",
+        "kernel_ms_mean": float(np.mean(t2)), "decisions_per_s": G2 / (float(np.mean(t2)) / 1e3)}
+    e2.close()
+    return out
+
+
 def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     """The reference's tick timed on this host's cores, two restatements:
     the Go-shaped one (oracle/mraft_goshape.c: int64 Raft structs, 40-byte
@@ -237,6 +380,8 @@ def main():
     ap.add_argument("--log", type=int, default=4096, help="log capacity L")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary lines (message path, configs #5 and #2) of a one-GPU run")
     ap.add_argument("--pmc-json", default="",
                     help="PMC traffic summary (default: profiles/pmc_traffic.json for 65,536 groups "
                          "per GPU, profiles/pmc_traffic_g<G>.json otherwise)")
@@ -530,6 +675,8 @@ def main():
     }
     if world > 1:
         out["roofline"]["kernel_ms_mean_max_over_ranks"] = ker_max_ms
+    if world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096:
+        out["secondary"] = secondary(master, clones[0], lp, G, P, L, stream, dev)  # reuses a spent copy
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 only (the other ranks wait at the barrier below); a shorter
         # sample with more than one rank
