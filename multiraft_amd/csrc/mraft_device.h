@@ -59,13 +59,14 @@ __device__ __forceinline__ int first_lane(unsigned long long m) { return __ffsll
 // row whose Index `base` (the dummy) sits at `head` (row length L); returns
 // lo - 1 when every term in the range equals a. Wave-uniform arguments; the
 // term of lo must be readable when lo <= hi (lanes past lo re-read it).
+template <int U = kUnroll>
 __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base, int head,
                                                  int L, int lo, int hi, int a) {
   const int lane = lane_id();
-  for (int top = hi; top >= lo; top -= kChunk) {
-    int v[kUnroll];
+  for (int top = hi; top >= lo; top -= kWave * U) {
+    int v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int idx = top - lane - kWave * u;
       const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the loads issue back to back
       v[u] = idx >= lo ? w : a;
@@ -74,7 +75,7 @@ __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row
     // behind the previous compare: one round trip per 64 terms).
     int r = lo - 1;
 #pragma unroll
-    for (int u = kUnroll - 1; u >= 0; --u) {
+    for (int u = U - 1; u >= 0; --u) {
       const unsigned long long m = __ballot(v[u] != a);
       r = m ? top - kWave * u - first_lane(m) : r;
     }

@@ -311,6 +311,9 @@ enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE
 #ifndef MRAFT_AE_STASH
 #define MRAFT_AE_STASH 1  // park the per-lane reply inputs in LDS across the pass
 #endif
+#ifndef MRAFT_AE_PIPE
+#define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
+#endif
 
 template <int NI>
 __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__restrict__ args,
@@ -451,7 +454,11 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
 #endif
     if (vec) {
       int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
-      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+      if (MRAFT_AE_PIPE) {
+        if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+      } else {
+        for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+      }
       copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
     } else {
       int c = plo;

@@ -13,6 +13,15 @@ namespace {
 
 enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the pass
 
+// base + k for a wave-uniform row base and a per-lane k >= 0 (for every lane
+// that dereferences it), as a 32-bit unsigned byte offset: the loads and
+// stores then use the SGPR-base + 32-bit VGPR-offset form, one VGPR per
+// stream instead of a 64-bit address pair.
+template <class T>
+__device__ __forceinline__ T *at_u(T *base, int k) {
+  return reinterpret_cast<T *>(reinterpret_cast<char *>(const_cast<int32_t *>(base)) + (uint32_t)k * 4u);
+}
+
 // Where the term of Index idx of a stream lives. Entries come from a
 // contiguous buffer (a network batch or staged copy: LinRow) or from the
 // leader's own ring (the fused tick: RingRow); followers are always rings
@@ -20,7 +29,7 @@ enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the 
 struct LinRow {
   const int32_t *p;
   long long off;
-  __device__ __forceinline__ const int32_t *at(int idx) const { return p + off + idx; }
+  __device__ __forceinline__ const int32_t *at(int idx) const { return at_u(p + off, idx); }
 };
 // Every lane that loads or stores in the pass holds an Index at or above the
 // row's dummy (loads and stores are masked to [plo, phi] / [start, cend) /
@@ -33,7 +42,7 @@ struct RingRow {
   int base, L;
   __device__ __forceinline__ const int32_t *at(int idx) const {
     const int k = idx + base;
-    return p + row + (k >= L ? k - L : k);
+    return at_u(p + row, k >= L ? k - L : k);
   }
 };
 
@@ -93,7 +102,7 @@ struct Fol {
   __device__ __forceinline__ int32_t *at(int q, int idx) const {
     const long long row = (SLOTS ? (long long)slot[SLOTS ? q : 0] : slot0 + q + (q >= skip ? 1 : 0)) * (long long)L;
     const int k = idx + base[q];  // >= 0 for every lane that loads or stores (see RingRow)
-    return log + row + (k >= L ? k - L : k);
+    return at_u(log + row, k >= L ? k - L : k);
   }
   __device__ __forceinline__ bool is_cmp(int q) const { return (cmp >> q) & 1; }
   __device__ __forceinline__ bool is_copy(int q) const { return (copy >> q) & 1; }
@@ -241,6 +250,99 @@ __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int 
       }
       if (c + CW >= nend) fo.copy &= ~(1 << q);
     }
+  }
+}
+
+// The compare chunks of the pass (VEC, 256 entries per chunk) software-
+// pipelined: chunk c is compared, then chunk c+256's loads (the leader's
+// entries and the words of every follower still comparing after chunk c) are
+// issued, then chunk c's stores, so the wave waits for the next loads without
+// waiting for its own stores (vmcnt counts both, in order). No word is loaded
+// that pass_chunk would not load. Runs while some follower compares; returns
+// the first chunk not processed (the copy-only loop continues there).
+template <bool COUNT, class Src, class F>
+__device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int slo, int shi, int T, int &found,
+                                         int c, int plo, int phi) {
+  constexpr int NI = F::kNI;
+  constexpr int CW = 256;
+  const int lane = lane_id();
+  int e[4], f[NI][4];
+  auto load = [&](int cc, int (&ee)[4], int (&ff)[NI][4]) {
+    const int i0 = cc + 4 * lane;
+    int4 x = make_int4(0, 0, 0, 0);
+    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src.at(i0));
+    ee[0] = x.x; ee[1] = x.y; ee[2] = x.z; ee[3] = x.w;
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      ff[q][0] = ff[q][1] = ff[q][2] = ff[q][3] = 0;
+      if (!fo.is_cmp(q) || fo.start[q] > cc + CW - 1 || fo.cend[q] <= cc) continue;
+      if (i0 + 3 >= fo.start[q] && i0 < fo.cend[q]) {
+        const int4 y = ld4(fo.at(q, i0));
+        ff[q][0] = y.x; ff[q][1] = y.y; ff[q][2] = y.z; ff[q][3] = y.w;
+      }
+    }
+  };
+  load(c, e, f);
+  for (;;) {
+    const int i0 = c + 4 * lane;
+    // compare: first mismatch of every follower still comparing
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (!fo.is_cmp(q) || fo.start[q] > c + CW - 1) continue;
+      int im = -1;
+      if (fo.cend[q] > c) {
+        int first = 4;
+#pragma unroll
+        for (int u = 3; u >= 0; --u)
+          if (i0 + u >= fo.start[q] && i0 + u < fo.cend[q] && e[u] != f[q][u]) first = u;
+        const unsigned long long m = __ballot(first < 4);
+        if (m) {
+          const int l = first_lane(m);
+          im = c + 4 * l + __shfl(first, l, 64);
+        }
+      }
+      if (im < 0 && fo.cend[q] <= c + CW - 1) {
+        if (fo.cend[q] < nend) im = fo.cend[q];
+        else fo.cmp &= ~(1 << q);
+      }
+      if (im >= 0) fo.mismatch(q, im);
+    }
+    // commit scan on this chunk's entries
+    if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
+      int lu = -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u >= slo && i0 + u <= shi && e[u] == T) lu = u;
+      const unsigned long long m = __ballot(lu >= 0);
+      if (m) {
+        const int l = 63 - __clzll((long long)m);
+        found = c + 4 * l + __shfl(lu, l, 64);
+      }
+    }
+    const int cn = c + CW;
+    const bool more = cn <= phi && fo.cmp;
+    int en[4];
+    if (more) load(cn, en, f);
+    if (!COUNT) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if (!fo.is_copy(q) || fo.start[q] > c + CW - 1) continue;
+        if (i0 >= fo.cfrom[q] && i0 + 3 < nend) {
+          st4(fo.at(q, i0), e[0], e[1], e[2], e[3]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + u >= fo.cfrom[q] && i0 + u < nend) st1(fo.at(q, i0 + u), e[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NI; ++q)
+      if (fo.is_copy(q) && fo.start[q] <= c + CW - 1 && cn >= nend) fo.copy &= ~(1 << q);
+    if (!more) return cn;
+    c = cn;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = en[u];
   }
 }
 

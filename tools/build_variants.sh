@@ -3,19 +3,27 @@
 # sources, different compile-time knobs); tools/tune.sh times them.
 # Each argument is  tag[@SRCDIR]=DEFINES  e.g.  "v2=-DMRAFT_TICK_V=2 -DMRAFT_TICK_MINW=6"
 # or "head@/tmp/head/multiraft_amd/csrc=" (another source tree, e.g. git archive HEAD).
+# TICK_ONLY=1: recompile only mraft_tick.hip per variant (the rest from build/).
 set -e
 cd "$(dirname "$0")/../multiraft_amd/csrc"
 OUT=$(cd ../../tools && pwd)/variants
 HERE=$(pwd)
 mkdir -p "$OUT"
 rm -f "$OUT"/*.so
-for spec in "$@"; do
+build_one() {
+  local spec="$1"
   cd "$HERE"
   tag=${spec%%=*}
   defs=${spec#*=}
   case "$tag" in *@*) cd "${tag#*@}"; tag=${tag%%@*};; esac
   mkdir -p build_$tag
-  for f in mraft_abi mraft_kernels mraft_tick mraft_elect; do
+  srcs="mraft_abi mraft_kernels mraft_tick mraft_elect"
+  if [ -n "$TICK_ONLY" ] && [ "$(pwd)" = "$HERE" ]; then
+    # only the tick differs: the other objects come from the in-tree build
+    srcs="mraft_tick"
+    for f in mraft_abi mraft_kernels mraft_elect; do cp build/$f.o build_$tag/; done
+  fi
+  for f in $srcs; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
       $defs -c $f.hip -o build_$tag/$f.o 2>/dev/null &
   done
@@ -28,4 +36,8 @@ for spec in "$@"; do
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
       $defs -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
       grep -A9 "k_tick_groupILi5ELb0" | grep -E "VGPRs:|Scratch|Occupancy" | sed -E "s/.*(VGPRs|ScratchSize|Occupancy)[^:]*: ([0-9]+).*/\1=\2/" | tr "\n" " "; echo
-done
+}
+# variants build in parallel (one compiler process per source file each)
+for spec in "$@"; do build_one "$spec" > "$OUT/.log_${spec%%[=@]*}" 2>&1 & done
+wait
+cat "$OUT"/.log_*; rm -f "$OUT"/.log_*

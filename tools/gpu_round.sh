@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-dev}
 mkdir -p gpurun_out
-echo "== pytest -m gpu" && { timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ]; } &&
+echo "== pytest -m gpu" && { timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -4 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ]; } &&
 echo "== profile" && bash tools/profile_round.sh > gpurun_out/profile.log 2>&1 &&
 python tools/pmc_summary.py "$TAG" > gpurun_out/pmc_summary.log 2>&1 && cp profiles/pmc_traffic.json profiles/${TAG}_*.csv gpurun_out/ &&
 echo "== bench" && { timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 20 --warmup 3} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?; tail -2 gpurun_out/bench.err; cat gpurun_out/bench.json; [ $rc -eq 0 ]; } &&
