@@ -13,13 +13,16 @@ namespace {
 
 enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the pass
 
-// base + k for a wave-uniform row base and a per-lane k >= 0 (for every lane
-// that dereferences it), as a 32-bit unsigned byte offset: the loads and
-// stores then use the SGPR-base + 32-bit VGPR-offset form, one VGPR per
-// stream instead of a 64-bit address pair.
+// base + k for a wave-uniform row base and a per-lane k, as a 32-bit unsigned
+// byte offset from base - 32 entries: the loads and stores then use the
+// SGPR-base + 32-bit VGPR-offset form, one VGPR per stream instead of a 64-bit
+// address pair. Valid for k >= -32 on every lane that dereferences it: a
+// dwordx4 group that holds the first entry of a range may begin up to 3
+// entries before it (a flat entries buffer indexed from its first Index: k < 0
+// there while the address is inside the buffer).
 template <class T>
 __device__ __forceinline__ T *at_u(T *base, int k) {
-  return reinterpret_cast<T *>(reinterpret_cast<char *>(const_cast<int32_t *>(base)) + (uint32_t)k * 4u);
+  return reinterpret_cast<T *>(reinterpret_cast<char *>(const_cast<int32_t *>(base - 32)) + (uint32_t)(k + 32) * 4u);
 }
 
 // Where the term of Index idx of a stream lives. Entries come from a

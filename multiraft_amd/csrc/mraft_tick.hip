@@ -191,9 +191,15 @@ struct Fold {
 #endif
 #if MRAFT_TICK_TRACE
 __device__ unsigned long long g_tick_trace[65536 * 4];
+// the XCD (XCC) this wave runs on, kept in the top bits of the entry stamp
+__device__ __forceinline__ unsigned long long tick_xcc() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return (unsigned long long)(v & 15);
+}
 #define TICK_STAMP(k)                                                                        \
   do {                                                                                       \
-    if (!COUNT && g < 65536 && lane == 0) g_tick_trace[g * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (!COUNT && g < 65536 && lane == 0) g_tick_trace[g * 4 + (k)] = __builtin_amdgcn_s_memrealtime() | ((k) == 0 ? tick_xcc() << 60 : 0ull); \
   } while (0)
 #else
 #define TICK_STAMP(k) do {} while (0)
