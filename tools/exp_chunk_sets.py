@@ -86,10 +86,23 @@ def main():
             best = min(best, a.elapsed_time(b))
         return best
 
+    probe = None
+    if os.environ.get("PROBE", "0") == "1":
+        probe = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprobe_place.so"))
+        probe.probe_place.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.POINTER(ctypes.c_float)]
+        sink = torch.zeros(16, dtype=torch.int32, device=dev)
     print(f"pool of {pool_n} chunks of {gran} B; {nch} per image", flush=True)
     for idx in images:
         va = image(idx)
-        print(f"image {idx}: tick {tick(va):.4f} ms", flush=True)
+        t = tick(va)
+        extra = ""
+        if probe is not None:
+            torch.cuda.synchronize()
+            ms = ctypes.c_float()
+            assert probe.probe_place(va, G, P, L, sink.data_ptr(), ctypes.byref(ms)) == 0
+            extra = f"  probe {ms.value:.4f} ms"
+        print(f"image {idx}: tick {t:.4f} ms{extra}", flush=True)
     eng.close()
 
 
