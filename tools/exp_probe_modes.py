@@ -1,4 +1,4 @@
-"""Placement experiment: on N plain (hipMalloc) log images, the tick's time
+"""Placement experiment: on N plain (torch / hipMalloc) log images, the tick's time
 and the synthetic traffic probe (tools/probe_place.hip) under different
 group -> XCD orders: which orders are fast on every image?"""
 import ctypes
@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     import torch
-    from multiraft_amd import DEVICE, Engine, LogImage, synth_seed, synth_tick_state
+    from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
     G, P, L = 65536, 5, 4096
     N = int(os.environ.get("COPIES", 8))
     modes = [int(m) for m in os.environ.get("MODES", "0,1,2,3,4,5,6").split(",")]
@@ -29,10 +29,9 @@ def main():
     lp_d = torch.from_numpy(lp).to(dev)
     gf = torch.zeros(G, dtype=torch.int32, device=dev)
     small = {k: v.clone() for k, v in master.items() if k != "log_term"}
-    imgs = [LogImage(G, P, L, plain=True) for _ in range(N)]
+    imgs = [torch.empty_like(master["log_term"]) for _ in range(N)]  # plain allocations
     print("modes " + " ".join(str(m) for m in modes), flush=True)
-    for i, img in enumerate(imgs):
-        t = img.tensor()
+    for i, t in enumerate(imgs):
         best = 1e9
         for _ in range(2):
             t.copy_(master["log_term"])
@@ -51,13 +50,10 @@ def main():
         pr = []
         for m in modes:
             ms = ctypes.c_float()
-            assert probe.probe_place(img.ptr, G, P, L, sink.data_ptr(), ctypes.byref(ms), m) == 0
+            assert probe.probe_place(t.data_ptr(), G, P, L, sink.data_ptr(), ctypes.byref(ms), m) == 0
             pr.append(ms.value)
         print(f"image {i}: tick {best:.4f} ms | probe " + " ".join(f"{x:.4f}" for x in pr), flush=True)
-        del t
     eng.close()
-    for img in imgs:
-        img.free()
 
 
 if __name__ == "__main__":

@@ -27,10 +27,48 @@ __device__ __forceinline__ int probe_group(int b, int nb, int mode) {
   }
 }
 
+// traffic patterns (mode / 16): 0 the tick's shape (below); 1 reads only (row 0
+// half + rows 1-2 quarter); 2 writes only (rows 3-4 half); 3 one 16-KB row per
+// group read (row 0 whole), nothing else; 4 row 0 read whole, row 1 written whole.
 __global__ __launch_bounds__(64) void k_probe(int *__restrict__ log, int G, int P, int L, int *__restrict__ sink,
                                               int mode) {
-  const int g = probe_group((int)blockIdx.x, (int)gridDim.x, mode);
+  const int g = probe_group((int)blockIdx.x, (int)gridDim.x, mode & 15);
   if (g >= G) return;
+  const int pat = mode >> 4;
+  if (pat >= 1) {
+    const int lane0 = threadIdx.x;
+    int *r0 = log + (long long)g * P * L;
+    int acc0 = 0;
+    const int lo = pat >= 3 ? 0 : L / 2;
+    for (int c = lo; c < L; c += 256) {
+      const int i = c + 4 * lane0;
+      if (pat == 1 || pat >= 3) {
+        const int4 *s = reinterpret_cast<const int4 *>(r0 + i);
+        int4 v;
+        v.x = __builtin_nontemporal_load(&s->x); v.y = __builtin_nontemporal_load(&s->y);
+        v.z = __builtin_nontemporal_load(&s->z); v.w = __builtin_nontemporal_load(&s->w);
+        acc0 ^= v.x ^ v.w;
+        if (pat == 4) {
+          int4 *d = reinterpret_cast<int4 *>(r0 + L + i);
+          __builtin_nontemporal_store(v.x, &d->x); __builtin_nontemporal_store(v.y, &d->y);
+          __builtin_nontemporal_store(v.z, &d->z); __builtin_nontemporal_store(v.w, &d->w);
+        }
+      }
+      if (pat == 1 && c < 3 * L / 4)
+        for (int q = 1; q < 3; ++q) {
+          const int4 *s = reinterpret_cast<const int4 *>(r0 + q * L + i);
+          acc0 ^= __builtin_nontemporal_load(&s->x) ^ __builtin_nontemporal_load(&s->w);
+        }
+      if (pat == 2)
+        for (int q = 3; q < 5; ++q) {
+          int4 *d = reinterpret_cast<int4 *>(r0 + q * L + i);
+          __builtin_nontemporal_store(c, &d->x); __builtin_nontemporal_store(i, &d->y);
+          __builtin_nontemporal_store(q, &d->z); __builtin_nontemporal_store(g, &d->w);
+        }
+    }
+    if (acc0 == 0x7fffffff) sink[0] = acc0;
+    return;
+  }
   const int lane = threadIdx.x;
   int *r = log + (long long)g * P * L;
   int acc = 0;
