@@ -670,6 +670,11 @@ def main():
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "algorithmic_bytes_per_decision": algo_bytes / max(active, 1),
                      "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms)),
+                     "kernel_ms_median": float(np.median(ker_ms)),
+                     "kernel_ms_steps": [round(float(x), 4) for x in ker_ms],
+                     "note": ("each step ticks its own fresh state copy; copies whose log image sits in "
+                              "physical memory that takes streaming writes ~10 % slower run ~13 % slower "
+                              "(DESIGN.md §5 placement lottery): kernel_ms_steps shows both populations"),
                      "scope": "rank 0's GPU" if world > 1 else "the GPU"},
         "cpu_baseline": None,
     }
