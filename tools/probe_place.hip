@@ -35,6 +35,23 @@ __global__ __launch_bounds__(64) void k_probe(int *__restrict__ log, int G, int 
   const int g = probe_group((int)blockIdx.x, (int)gridDim.x, mode & 15);
   if (g >= G) return;
   const int pat = mode >> 4;
+  if (pat >= 5) {
+    // write-order patterns over rows 1..4 (whole rows): 5 row 4 only; 6 the
+    // four rows interleaved per 1-KB chunk (the tick's copy); 7 row after row;
+    // 8 interleaved per 4-KB block
+    const int ln = threadIdx.x;
+    int *r0 = log + (long long)g * P * L;
+    const int rows_lo = pat == 5 ? 4 : 1;
+    const int blk = pat == 6 ? 256 : pat == 8 ? 1024 : L;
+    for (int c0 = 0; c0 < L; c0 += blk)
+      for (int q = rows_lo; q < 5; ++q)
+        for (int c = c0; c < c0 + blk && c < L; c += 256) {
+          int4 *d = reinterpret_cast<int4 *>(r0 + q * L + c + 4 * ln);
+          __builtin_nontemporal_store(c, &d->x); __builtin_nontemporal_store(q, &d->y);
+          __builtin_nontemporal_store(g, &d->z); __builtin_nontemporal_store(ln, &d->w);
+        }
+    return;
+  }
   if (pat >= 1) {
     const int lane0 = threadIdx.x;
     int *r0 = log + (long long)g * P * L;
