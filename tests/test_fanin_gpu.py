@@ -11,7 +11,7 @@ import pytest
 from oracle_lib import Oracle
 
 from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
-from multiraft_amd.router import GroupStatusView, RcclFanIn, unpack_status
+from multiraft_amd.router import GroupStatusView, RcclFanIn, ShardCtrlerState, key2shard, unpack_status
 
 pytestmark = pytest.mark.gpu
 
@@ -54,5 +54,17 @@ def test_one_rank_rccl_gather_equals_export(mode):
             assert np.array_equal(gc.numpy(), oc) and np.array_equal(gt.numpy(), otl)
             view = GroupStatusView(gc.numpy(), gt.numpy())
             assert int(view.is_leader.sum()) == int(((otl & 1) != 0).sum())
+            # the shard router on the gathered words: shardctrler Join of
+            # three replica groups (gid k served by Raft group 100 k), then
+            # every key routed to its shard's group reads that group's
+            # GetState words (shardkv/client.go:68-100 polls these)
+            ctl = ShardCtrlerState()
+            ctl.join({1: ["a"], 2: ["b"], 3: ["c"]})
+            shard_to_group = np.array([100 * int(x) for x in ctl.query().shards])
+            assert set(ctl.query().shards.tolist()) == {1, 2, 3}
+            for key in ("", "a", "k17", "zz", "\x07x"):
+                g, c_, t_, ldr = view.route(key, shard_to_group)
+                assert g == 100 * int(ctl.query().shards[key2shard(key)])
+                assert (c_, t_, ldr) == (int(oc[g]), int(otl[g]) >> 1, bool(otl[g] & 1))
         finally:
             fan.close()
