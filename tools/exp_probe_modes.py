@@ -52,7 +52,17 @@ def main():
             ms = ctypes.c_float()
             assert probe.probe_place(t.data_ptr(), G, P, L, sink.data_ptr(), ctypes.byref(ms), m) == 0
             pr.append(ms.value)
-        print(f"image {i}: tick {best:.4f} ms | probe " + " ".join(f"{x:.4f}" for x in pr), flush=True)
+        extra = ""
+        if os.environ.get("RANGES", "0") == "1":
+            # plain streaming writes over each 1-GiB piece of the image (TB/s)
+            probe.probe_write_range.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.POINTER(ctypes.c_float)]
+            nbytes, gib, rates = t.numel() * 4, 1 << 30, []
+            for off in range(0, nbytes - gib + 1, gib):
+                ms = ctypes.c_float()
+                assert probe.probe_write_range(t.data_ptr() + off, gib, ctypes.byref(ms)) == 0
+                rates.append(gib / (ms.value * 1e-3) / 1e12)
+            extra = " | write TB/s per GiB " + " ".join(f"{x:.2f}" for x in rates)
+        print(f"image {i}: tick {best:.4f} ms | probe " + " ".join(f"{x:.4f}" for x in pr) + extra, flush=True)
     eng.close()
 
 

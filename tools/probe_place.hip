@@ -131,3 +131,30 @@ extern "C" int probe_place(void *log, int G, int P, int L, void *sink, float *ms
   *ms = best;
   return 0;
 }
+
+// Plain streaming write over [p, p + bytes): grid-stride, 16 B per lane, non-temporal.
+__global__ void k_write_range(int4 *__restrict__ b, long long n4) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    __builtin_nontemporal_store((int)i, &b[i].x); __builtin_nontemporal_store(1, &b[i].y);
+    __builtin_nontemporal_store(2, &b[i].z); __builtin_nontemporal_store(3, &b[i].w);
+  }
+}
+
+extern "C" int probe_write_range(void *p, long long bytes, float *ms) {
+  hipEvent_t a, b;
+  if (hipEventCreate(&a) || hipEventCreate(&b)) return -3;
+  float best = 1e30f;
+  for (int r = 0; r < 3; ++r) {
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL(k_write_range, dim3(16384), dim3(256), 0, 0, (int4 *)p, bytes / 16);
+    (void)hipEventRecord(b, 0);
+    if (hipEventSynchronize(b)) return -3;
+    float t;
+    (void)hipEventElapsedTime(&t, a, b);
+    if (r && t < best) best = t;
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *ms = best;
+  return 0;
+}
