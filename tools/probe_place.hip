@@ -23,6 +23,10 @@ __device__ __forceinline__ int probe_group(int b, int nb, int mode) {
     case 4: return ((j >> 6) * 8 + x) * 64 + (j & 63);
     case 5: { const int nblk = per >> 10; return x * per + (nblk - 1 - (j >> 10)) * 1024 + (j & 1023); }
     case 6: return x * per + (j + x * (per / 8)) % per;
+    case 7: return x * per + (j & 1) * (per / 2) + (j >> 1);                 // range halves walked together
+    case 8: return x * per + (j & 3) * (per / 4) + (j >> 2);                 // range quarters walked together
+    case 9: return ((j >> 10) * 8 + x) * 1024 + (j & 1023);                  // 1,024-group chunks dealt round-robin
+    case 10: return ((j >> 8) * 8 + x) * 256 + (j & 255);                    // 256-group chunks dealt round-robin
     default: return x * per + j;
   }
 }
