@@ -202,6 +202,33 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
     return out
 
 
+def placement_probe(copies, G, P, L, dev):
+    """After the timed region (the copies are spent): the data-free traffic
+    probe (tools/probe_place.hip: the tick's XCD-aware order, writes only)
+    on every step's state copy, so the record shows that the slow steps are
+    the copies whose memory takes the eight XCDs' writes slowly (DESIGN.md §5
+    placement lottery). None if the probe library is not built."""
+    import ctypes
+
+    import torch
+    path = os.path.join(ROOT, "tools", "libprobe_place.so")
+    if not os.path.exists(path) or P < 5:
+        return None
+    lib = ctypes.CDLL(path)
+    lib.probe_place.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    sink = torch.zeros(16, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ms = []
+    for c in copies:
+        t = ctypes.c_float()
+        if lib.probe_place(c["log_term"].data_ptr(), G, P, L, sink.data_ptr(), ctypes.byref(t), 32) != 0:
+            return None
+        ms.append(round(t.value, 4))
+    return {"what": "writes-only probe (tools/probe_place.hip mode 32) on each step's state copy after the "
+                    "timed region, ms per copy, in step order", "ms": ms}
+
+
 def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     """The reference's tick timed on this host's cores, two restatements:
     the Go-shaped one (oracle/mraft_goshape.c: int64 Raft structs, 40-byte
@@ -680,6 +707,25 @@ def main():
     }
     if world > 1:
         out["roofline"]["kernel_ms_mean_max_over_ranks"] = ker_max_ms
+    if world == 1 and not restore:
+        pp = placement_probe(clones[:K], G, P, L, dev)
+        if pp is not None:
+            # the two populations the probe separates (largest gap in its sorted
+            # times), each with its mean kernel time and HBM fraction; `frac`
+            # above stays the mean over every step
+            pm = np.array(pp["ms"])
+            order = np.sort(pm)
+            if len(order) > 1 and np.diff(order).max() > 0.05 * order[0]:
+                cut = order[int(np.argmax(np.diff(order)))]
+                km = np.array(ker_ms)
+                pops = {}
+                for name, sel in (("fast_memory", pm <= cut), ("slow_memory", pm > cut)):
+                    kms = float(km[sel].mean())
+                    pops[name] = {"steps": int(sel.sum()), "kernel_ms_mean": round(kms, 4),
+                                  "frac": algo_bytes / (kms / 1e3) / HBM_PEAK}
+                pp["populations"] = pops
+                pp["corr_with_kernel_ms"] = float(np.corrcoef(pm, km)[0, 1])
+            out["roofline"]["placement_probe"] = pp
     if world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096:
         out["secondary"] = secondary(master, clones[0], lp, G, P, L, stream, dev)  # reuses a spent copy
     if rank == 0 and not args.no_cpu_baseline:
