@@ -710,13 +710,17 @@ def main():
     if world == 1 and not restore:
         pp = placement_probe(clones[:K], G, P, L, dev)
         if pp is not None:
-            # the two populations the probe separates (largest gap in its sorted
-            # times), each with its mean kernel time and HBM fraction; `frac`
-            # above stays the mean over every step
+            # the two populations the probe separates (two-means on its times),
+            # each with its mean kernel time and HBM fraction; `frac` above
+            # stays the mean over every step
             pm = np.array(pp["ms"])
-            order = np.sort(pm)
-            if len(order) > 1 and np.diff(order).max() > 0.05 * order[0]:
-                cut = order[int(np.argmax(np.diff(order)))]
+            lo_c, hi_c = float(pm.min()), float(pm.max())
+            for _ in range(20):
+                cut = (lo_c + hi_c) / 2
+                if not (pm <= cut).any() or not (pm > cut).any():
+                    break
+                lo_c, hi_c = float(pm[pm <= cut].mean()), float(pm[pm > cut].mean())
+            if (pm <= cut).any() and (pm > cut).any() and hi_c > 1.05 * lo_c:
                 km = np.array(ker_ms)
                 pops = {}
                 for name, sel in (("fast_memory", pm <= cut), ("slow_memory", pm > cut)):
