@@ -428,6 +428,13 @@ def main():
                     help="CUs reserved for the fan-in stream (mraft_fanin_reserve_cus; 0 = none): "
                          "without them the overlapped gather queues for CU slots behind the next "
                          "tick (0.31 ms vs 0.015 ms on one rank, profiles/r2_v1_fanin_cus*.json)")
+    ap.add_argument("--fanin-marks", default="chain", choices=["chain", "legacy"],
+                    help="timing/ordering markers on the tick stream: chain = one per tick, shared by "
+                         "the timing and the fan-in's wait (MRAFT_FANIN_ORDERED); legacy = round 2's "
+                         "start + end marks per tick plus the fan-in's own event (A/B only)")
+    ap.add_argument("--extra-marks", type=int, default=0,
+                    help="experiment: record this many extra (untimed) events on the tick stream "
+                         "after every tick")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch plumbing only (no GPU call): start the ranks, build every rank's "
                          "shard of the seeded workload, run the control plane and print the line "
@@ -566,10 +573,15 @@ def main():
     algo_bytes = 4 * (rd + wr)
 
     # Per-launch kernel timing on the engine's stream. With nothing else on the
-    # stream between ticks (no fan-in, no restores) one marker between
-    # consecutive ticks serves as the end of one and the start of the next.
-    chain = not dist_on and not restore
+    # stream between ticks (no restores) one marker between consecutive ticks
+    # serves as the end of one and the start of the next, and the fan-in
+    # stream waits on that same marker (MRAFT_FANIN_ORDERED): one marker
+    # packet per tick on the tick's queue. Every extra marker there costs the
+    # step a few microseconds of idle device (the round-2 fan-in runs recorded
+    # four per tick: ~20 us per step beyond the kernel).
+    chain = not restore and args.fanin_marks == "chain"
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
+    extra = [torch.cuda.Event() for _ in range(args.extra_marks)]
 
     # The all-gather, timed on its own stream (reported beside the step).
     ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if fan is not None else []
@@ -596,6 +608,8 @@ def main():
         eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
         if timed:
             mark_end(i).record(stream)
+        for x in extra:  # experiment: marker packets between ticks
+            x.record(stream)
         if dist_on:  # the shard router's fan-in
             if on_host:
                 t1 = time.perf_counter()
@@ -606,13 +620,18 @@ def main():
                 # RCCL all-gather of this tick's words (C ABI). Overlapped: on
                 # the fan-in stream after the tick, beside the next tick (which
                 # writes another block), so the next batch never waits for it.
-                if timed and overlap:
+                ordered = False
+                if overlap and timed and chain:
+                    # the fan-in stream waits on the tick's own end marker
+                    comm_stream.wait_event(mark_end(i))
+                    ordered = True
+                elif timed and overlap:
                     # the gather starts once the tick is done: its start mark
                     # waits for the tick on the fan-in stream as well
                     comm_stream.wait_stream(stream)
                 if timed:
                     ag_marks[2 * i].record(comm_stream)
-                fan.gather(status[j], gathered[j], overlap=overlap)
+                fan.gather(status[j], gathered[j], overlap=overlap, ordered=ordered)
                 if timed:
                     ag_marks[2 * i + 1].record(comm_stream)
 
@@ -686,7 +705,10 @@ def main():
                    "allgather_ms_mean": float(np.mean(ag_ms)) if ag_ms else None,
                    "allgather_bytes_per_rank": 8 * G if dist_on else 0,
                    "allgather_placement": (args.fanin if fan is not None else None),
-                   "fanin_reserved_cus": args.fanin_cus if fan is not None else 0},
+                   "fanin_reserved_cus": args.fanin_cus if fan is not None else 0,
+                   "tick_stream_marks_per_step": (1 if chain else 2) + args.extra_marks
+                   + (1 if fan is not None and not chain else 0),
+                   "step_minus_kernel_ms": dt / K * 1e3 - float(np.mean(ker_ms))},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,

@@ -563,7 +563,13 @@ enum {
    * on its stream (an event, no host wait): later work on the engine stream
    * (the next tick) does not wait for the gather. The caller must not reuse
    * `local`/`gathered` before mraft_fanin_synchronize or a later gather. */
-  MRAFT_FANIN_OVERLAP = 1
+  MRAFT_FANIN_OVERLAP = 1,
+  /* As OVERLAP, but the caller has already ordered the fan-in stream
+   * (mraft_fanin_stream) after the work that produces `local`, e.g. with
+   * hipStreamWaitEvent on an event of its own: the call records no event on
+   * the engine stream, so a host that already marks every tick (timing) adds
+   * no second marker packet per tick. */
+  MRAFT_FANIN_ORDERED = 2
 };
 
 /* All-gather of the [2*G] status words of every rank over `comm` (ncclAllGather,

@@ -30,6 +30,7 @@ G_SNAPSHOT_INSTALLED = 256
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
 ABI_VERSION = 3
 FANIN_OVERLAP = 1
+FANIN_ORDERED = 2
 COMM_ID_BYTES = 128
 SYN_MATCH, SYN_MISMATCH, SYN_BEYOND, SYN_STALE, SYN_BELOW_DUMMY, SYN_HEARTBEAT = range(6)
 

@@ -903,7 +903,9 @@ int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local, in
     return sg.finish();
   }
   hipStream_t st = h->stream;
-  if (flags & MRAFT_FANIN_OVERLAP) {
+  if (flags & MRAFT_FANIN_ORDERED) {
+    TRY(fanin_stream_of(h, &st));
+  } else if (flags & MRAFT_FANIN_OVERLAP) {
     TRY(fanin_stream_of(h, &st));
     if (!h->fanin_ev) HIP_TRY(hipEventCreateWithFlags(&h->fanin_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(h->fanin_ev, h->stream));

@@ -396,13 +396,16 @@ class Engine:
         return c.value
 
     def allgather_status(self, comm: int, local, gathered=None, where: int = DEVICE,
-                         overlap: bool = False):
+                         overlap: bool = False, ordered: bool = False):
         """All-gather this rank's [2*G] status block (commit | term<<1|leader)
-        into the [nranks*2*G] rank-major `gathered` buffer over RCCL."""
+        into the [nranks*2*G] rank-major `gathered` buffer over RCCL.
+        ordered: the caller has already made the fan-in stream wait for the
+        producer of `local` (MRAFT_FANIN_ORDERED: no event recorded here)."""
         if where == HOST:
             local = np.ascontiguousarray(local, dtype=np.int32)
         _ck(self._lib.mraft_allgather_status(self._h, comm, ptr(local), ptr(gathered), where,
-                                             _abi.FANIN_OVERLAP if overlap else 0),
+                                             _abi.FANIN_ORDERED if ordered else
+                                             (_abi.FANIN_OVERLAP if overlap else 0)),
             "mraft_allgather_status")
         return gathered
 

@@ -4,9 +4,11 @@ Each rank owns a contiguous range of groups; once per tick the GetState words
 of every group (commitIndex, currentTerm<<1 | isLeader — mraft_export_group_status)
 are all-gathered so every rank's router sees the whole deployment. This is the
 replacement for polling GetState()/commit progress
-(src/kvraft/server.go:114, src/shardkv/client.go:68-100). The collective is
-torch.distributed's all_gather_into_tensor: RCCL over xGMI for device tensors
-(backend "nccl"), gloo for host tensors (tests).
+(src/kvraft/server.go:114, src/shardkv/client.go:68-100). On the data path
+the collective is the library's own RCCL all-gather over xGMI through the C
+ABI (RcclFanIn: mraft_comm_init + mraft_allgather_status); the
+torch.distributed helpers below (allgather_status*) are the host-side
+rehearsal used by the gloo tests and the bench's check of the RCCL words.
 
 The shard -> group assignment is the shard controller's Config
 (src/shardctrler/common.go:27-132), applied as its state machine does
@@ -105,9 +107,10 @@ class RcclFanIn:
         self.eng, self.rank, self.world = eng, rank, world
         self.comm = eng.comm_init(world, rank, uid)
 
-    def gather(self, local, out, overlap: bool = True):
-        """local: [2*G] device block of this rank; out: [world*2*G] device."""
-        return self.eng.allgather_status(self.comm, local, out, overlap=overlap)
+    def gather(self, local, out, overlap: bool = True, ordered: bool = False):
+        """local: [2*G] device block of this rank; out: [world*2*G] device.
+        ordered: the caller already ordered the fan-in stream after the tick."""
+        return self.eng.allgather_status(self.comm, local, out, overlap=overlap, ordered=ordered)
 
     def close(self):
         from .engine import comm_destroy
