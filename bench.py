@@ -49,6 +49,22 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_share() -> dict:
+    """The host cores this process may use: its CPU affinity, capped by a
+    cgroup CPU quota when one is set (the GPU box's nproc shows the whole
+    machine). `threads` is what the CPU baseline runs on."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return {"threads": max(1, min(aff, quota) if quota else aff), "affinity": aff, "cgroup_quota": quota,
+            "nproc": os.cpu_count()}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -202,6 +218,95 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
     return out
 
 
+CONFIG4_ANCHOR = os.path.join(ROOT, "profiles", "config4_n1_anchor.json")
+
+
+def config4_one_gpu(dev, stream, steps=10):
+    """BASELINE config #4 on ONE GPU: all 262,144 groups (config #3's
+    generator and mix, the workload the N > 1 lines split N ways) in one tick
+    launch per step, each step on its own fresh HBM-resident copy (as many as
+    fit; ~21.5 GB each). The N = 1 point of the strong-scaling series, timed
+    exactly like the headline (one marker per tick on the engine stream)."""
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
+    G4, P, L = 262144, 5, 4096
+    t = time.perf_counter()
+    st, lp, _ = synth_tick_state(G4, P, L, seed=synth_seed(3), nthreads=cpu_share()["threads"])
+    gen_s = time.perf_counter() - t
+    master = {}
+    for k in list(st):
+        master[k] = torch.from_numpy(st.pop(k)).to(dev)
+    clone_bytes = sum(v.numel() * 4 for v in master.values())
+    free, _ = torch.cuda.mem_get_info(dev)
+    pool = max(1, min(steps, int(free * 0.92 // clone_bytes)))
+    clones = [{k: v.clone() for k, v in master.items()} for _ in range(pool)]
+    lp_d = torch.from_numpy(lp).to(dev)
+    gf = torch.zeros(G4, dtype=torch.int32, device=dev)
+    eng = Engine(G4, P, L, device=dev.index or 0, alloc=False)
+    eng.set_stream(stream.cuda_stream)
+    eng.bind(master)
+    rd, wr, active = eng.replicate_tick_count(lp_d, where=DEVICE)
+    algo = 4 * (rd + wr)
+    eng.bind(clones[-1])  # warm-up on a copy that is re-timed last
+    eng.replicate_tick(lp_d, gf, where=DEVICE)
+    torch.cuda.synchronize()
+    if pool > 1:  # the warm-up copy is spent: refresh it for the timed steps
+        for k in master:
+            clones[-1][k].copy_(master[k])
+    torch.cuda.synchronize()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(pool + 1)]
+    t0 = time.perf_counter()
+    marks[0].record(stream)
+    for i in range(pool):
+        eng.bind(clones[i])
+        eng.replicate_tick(lp_d, gf, where=DEVICE)
+        marks[i + 1].record(stream)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ker = [marks[i].elapsed_time(marks[i + 1]) for i in range(pool)]
+    eng.close()
+    del clones, master
+    torch.cuda.empty_cache()
+    km = float(np.mean(ker))
+    out = {"workload": "config #4 on one GPU: 262,144 groups x 5 peers x 4,096-entry logs (config #3's "
+                       "generator and mix; the N > 1 lines split it N ways), one tick launch per step, "
+                       "fresh copy per step",
+           "groups": G4, "steps": pool, "state_copy_gib": clone_bytes / 2**30, "generate_s": gen_s,
+           "ms_per_step": dt / pool * 1e3, "decisions_per_s": G4 * pool / dt,
+           "roofline": {"kernel": "k_tick_group<5,false>", "bound": "hbm", "algorithmic_bytes": algo,
+                        "achieved": algo / (km / 1e3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                        "frac": algo / (km / 1e3) / HBM_PEAK, "kernel_ms_mean": km,
+                        "kernel_ms_min": float(np.min(ker)), "kernel_ms_steps": [round(x, 4) for x in ker],
+                        "active_groups": active}}
+    pj = os.path.join(ROOT, "profiles", f"pmc_traffic_g{G4}.json")
+    if os.path.exists(pj):
+        pm = json.load(open(pj))
+        if pm.get("kernel_src_sha") == kernel_src_sha():
+            out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
+            out["roofline"]["traffic_source"] = f"profiles/{os.path.basename(pj)} ({pm.get('tag')})"
+    return out
+
+
+def strong_scaling_ref(strong, world, G_total) -> dict:
+    """For N > 1 strong-scaling lines of config #4: the N = 1 point of the
+    same series (all 262,144 groups on one GPU), as last measured by a
+    one-GPU bench run (secondary.config4_one_gpu -> tools/write_anchor.py)."""
+    if not (strong and world > 1 and G_total == 262144):
+        return {}
+    if not os.path.exists(CONFIG4_ANCHOR):
+        return {"strong_scaling_reference_ms": None,
+                "strong_scaling_reference": {"what": "no one-GPU config #4 anchor committed"}}
+    a = json.load(open(CONFIG4_ANCHOR))
+    return {"strong_scaling_reference_ms": a.get("ms_per_step"),
+            "strong_scaling_reference": {
+                "what": "N = 1 point of this series: config #4's 262,144 groups on one GPU "
+                        "(secondary.config4_one_gpu of a one-GPU bench.py run, same generator and timing)",
+                "source": f"profiles/{os.path.basename(CONFIG4_ANCHOR)} ({a.get('tag')})",
+                "ms_per_step": a.get("ms_per_step"), "kernel_ms_mean": a.get("kernel_ms_mean"),
+                "decisions_per_s": a.get("decisions_per_s")}}
+
+
 def placement_probe(copies, G, P, L, dev):
     """After the timed region (the copies are spent): the data-free traffic
     probe (tools/probe_place.hip: the tick's XCD-aware order, writes only)
@@ -241,7 +346,8 @@ def cpu_baseline(G_total, P, L, seed, budget_s, rank):
     from oracle_lib import GoShaped, Oracle  # test infrastructure: CPU baseline only
 
     from multiraft_amd import synth_tick_state
-    threads = max(1, min(16, os.cpu_count() or 1))
+    share = cpu_share()
+    threads = share["threads"]
 
     def timed(make, tick, budget, nt, groups):
         done, spent, w0, last = 0, 0.0, time.perf_counter(), time.perf_counter()
@@ -290,6 +396,9 @@ def cpu_baseline(G_total, P, L, seed, budget_s, rank):
               f"SoA {stt:.4g} ({s1:.4g} on 1)")
     return {"value": gt, "unit": "decisions/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "cores_source": (f"len(os.sched_getaffinity(0)) = {share['affinity']}"
+                             + (f", capped by the cgroup CPU quota ({share['cgroup_quota']})"
+                                if share["cgroup_quota"] else "")),
             "compiler": "gcc -O3 -march=x86-64-v3 (oracle/Makefile)",
             "sample": (f"oracle/mraft_goshape.c: the tick on the reference's data shapes (int64 Raft "
                        f"structs, 40-byte Entry slices, per-message entries copies, a1's "
@@ -515,7 +624,8 @@ def main():
                                                          dist_on, rccl, args.dist_backend),
                            "groups_per_gpu": G, "global_groups": G_total, "peers": P,
                            "log_capacity": L, "shard_of_rank0": [0, G],
-                           "leaders_in_shard_rank0": int((lp >= 0).sum())}}),
+                           "leaders_in_shard_rank0": int((lp >= 0).sum())},
+                **strong_scaling_ref(strong, world, G_total)}),
                 file=result_out, flush=True)
         if dist_on:
             dist.barrier()
@@ -729,6 +839,7 @@ def main():
     }
     if world > 1:
         out["roofline"]["kernel_ms_mean_max_over_ranks"] = ker_max_ms
+    out.update(strong_scaling_ref(strong, world, G_total))
     if world == 1 and not restore:
         pp = placement_probe(clones[:K], G, P, L, dev)
         if pp is not None:
@@ -752,8 +863,18 @@ def main():
                 pp["populations"] = pops
                 pp["corr_with_kernel_ms"] = float(np.corrcoef(pm, km)[0, 1])
             out["roofline"]["placement_probe"] = pp
-    if world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096:
+    if (world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096
+            and fan is None):
         out["secondary"] = secondary(master, clones[0], lp, G, P, L, stream, dev)  # reuses a spent copy
+        # config #4's N = 1 anchor: free config #3's copies, then all 262,144 groups on this GPU
+        eng.close()
+        del clones, master
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        c4 = config4_one_gpu(dev, stream)
+        out["secondary"]["config4_one_gpu"] = c4
+        log(rank, f"config #4 on one GPU: {c4['ms_per_step']:.4f} ms/step, tick {c4['roofline']['kernel_ms_mean']:.4f} ms "
+                  f"({c4['roofline']['frac']:.3f} of 8 TB/s) over {c4['steps']} fresh copies")
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 only (the other ranks wait at the barrier below); a shorter
         # sample with more than one rank

@@ -81,7 +81,9 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from oracle_lib import Oracle  # checker / CPU baseline only
         Gs = 8192
-        threads = max(1, min(16, os.cpu_count() or 1))
+        from bench import cpu_share  # affinity, capped by the cgroup quota
+        share = cpu_share()
+        threads = share["threads"]
         sst, smask = synth_election_state(G, P, L, seed=synth_seed(5), rounds=R, g_begin=0, g_end=Gs)
         o = Oracle(Gs, P, L, sst)
 
@@ -99,7 +101,9 @@ def main():
         v1, _ = run(1, min(2.0, a.cpu_seconds / 4))
         vt, spent = run(threads, a.cpu_seconds)
         out["cpu_baseline"] = {"value": vt, "unit": "group-rounds/s", "cores": threads,
-                               "kind": "port", "single_thread_value": v1,
+                               "kind": "port", "single_thread_value": v1, "nproc": os.cpu_count(),
+                               "cores_source": f"sched_getaffinity {share['affinity']}, cgroup quota "
+                                               f"{share['cgroup_quota']}",
                                "sample": f"oracle ora_election_rounds on groups 0..{Gs - 1}, {R} rounds, "
                                          f"fresh state per pass, {spent:.1f} s on {threads} threads; "
                                          f"1 thread: {v1:.4g} group-rounds/s"}

@@ -30,6 +30,8 @@ def test_gpus2_spawns_two_ranks_config4_default():
     c = out["config"]
     assert c["global_groups"] == 262144 and c["groups_per_gpu"] == 131072
     assert c["workload"].startswith("config #4: 262,144 groups")
+    # the N = 1 point of the strong-scaling series is named on every N > 1 line
+    assert "strong_scaling_reference_ms" in out and "what" in out["strong_scaling_reference"]
 
 
 def test_gpus1_defaults_to_config3():
@@ -37,6 +39,7 @@ def test_gpus1_defaults_to_config3():
     assert out["n_gpus"] == 1 and out["scaling"] == "weak"
     assert out["config"]["groups_per_gpu"] == 65536
     assert out["config"]["workload"].startswith("config #3")
+    assert "strong_scaling_reference_ms" not in out
 
 
 def test_gpus4_weak_when_groups_given():
