@@ -393,7 +393,10 @@ int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to,
  * (lastApplied, commitIndex] (:179-190). *out_n = the number of such slots;
  * the first min(*out_n, cap) are written and only those clear hasSnapshot and
  * advance lastApplied to commitIndex (:200), so a caller with a small buffer
- * calls again for the rest. */
+ * calls again for the rest. out_snap_index / out_snap_term may both be NULL:
+ * then, as in mraft_collect_apply, no SnapshotValid message is taken —
+ * only slots with commitIndex > lastApplied count and hasSnapshot stays set
+ * for a later call that passes them. */
 int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots,
                                 int32_t *out_snap_index, int32_t *out_snap_term,
                                 int32_t *out_from, int32_t *out_to,

@@ -11,7 +11,7 @@ ABI in include/mraft.h); this package is its host-side mirror:
     words (one RCCL all-gather per tick on multi-GPU).
 """
 from ._abi import (CANDIDATE, DEVICE, FOLLOWER, HOST, LEADER, synth_seed)  # noqa: F401
-from .engine import (Engine, MraftError, copy_state, decode_persistent,  # noqa: F401
+from .engine import (Engine, MraftError, copy_state, decode_persistent, entry_positions,  # noqa: F401
                      encode_persistent, new_state, state_sizes, synth_election_state,
                      synth_fold_batch, synth_tick_state)
 

@@ -545,8 +545,8 @@ int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *ou
                                 int32_t *out_snap_term, int32_t *out_from, int32_t *out_to, int64_t cap,
                                 int64_t *out_n, int32_t where) {
   TRY(check(h));
-  if (cap < 0 || !out_n ||
-      (cap > 0 && (!out_slots || !out_from || !out_to || !out_snap_index || !out_snap_term)))
+  if (cap < 0 || !out_n || (cap > 0 && (!out_slots || !out_from || !out_to)) ||
+      (!out_snap_index) != (!out_snap_term))
     return fail(MRAFT_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);

@@ -409,6 +409,9 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
     fo.full = 0;
     const int phi = uni(__shfl(prev + nn, first_lane((unsigned long long)merge_m), 64)), nend = phi + 1;
     int plo = phi + 1;
+#pragma unroll
+    for (int q = 0; q < NI; ++q)
+      if ((merge_m >> q) & 1) plo = min(plo, uni(__shfl(prev, q, 64)) + 1);
     // the source as the first merging message sees it (the same for every message of a set)
     const int q0 = first_lane((unsigned long long)merge_m);
     RingRow ss;
@@ -422,6 +425,14 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
       ss.base = uni(__shfl(src.base, q0, 64));
       ss.L = uni(__shfl(src.L, q0, 64));
     }
+    // A flat source (host buffer or staged copy) is addressed from the pass's
+    // first Index: the lane offset at_u forms is then Index - plo >= -3 for
+    // every lane that loads (32-bit byte offsets stay small whatever the Raft
+    // Index; with the absolute Index they would wrap past 2^30).
+    if (ss.L == INT32_MAX) {
+      ss.row += (long long)ss.base + plo;
+      ss.base = -plo;
+    }
     bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0;
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
@@ -432,7 +443,6 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
       fo.cend[q] = min(phi, sl) + 1;
       fo.cfrom[q] = 0;
       if ((merge_m >> q) & 1) {
-        plo = min(plo, sp + 1);
         // dwordx4 when the entries and this follower's row are 16-B aligned alike
         vec = vec && ((((uintptr_t)ss.at(sp + 1) ^ (uintptr_t)fo.at(q, sp + 1)) & 15) == 0);
       }
@@ -819,12 +829,15 @@ __global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__re
   }
 }
 
-// Compacted applier: slots with commitIndex > lastApplied, ascending, in
-// three launches (per-block counts, one-workgroup exclusive scan, emit).
-__global__ __launch_bounds__(256) void k_apply_count(Dev s, int32_t *__restrict__ bcnt) {
+// Compacted applier: slots with a message to send, ascending, in three
+// launches (per-block counts, one-workgroup exclusive scan, emit). `snaps`:
+// the caller takes SnapshotValid messages (hasSnapshot counts and is
+// cleared); without, only commitIndex > lastApplied counts and hasSnapshot
+// is left for a later call that takes them (as mraft_collect_apply does).
+__global__ __launch_bounds__(256) void k_apply_count(Dev s, int32_t *__restrict__ bcnt, int snaps) {
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const bool pend = i < gp && (s.hsnap[i] != 0 || s.commit[i] > s.applied[i]);
+  const bool pend = i < gp && ((snaps && s.hsnap[i] != 0) || s.commit[i] > s.applied[i]);
   const unsigned long long m = __ballot(pend);
   __shared__ int wc[4];
   if (lane_id() == 0) wc[threadIdx.x >> 6] = __popcll(m);
@@ -862,7 +875,7 @@ __global__ __launch_bounds__(256) void k_apply_emit(Dev s, const int32_t *__rest
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   int la = 0, ci = 0, hs = 0;
-  if (i < gp) { la = s.applied[i]; ci = s.commit[i]; hs = s.hsnap[i]; }
+  if (i < gp) { la = s.applied[i]; ci = s.commit[i]; hs = osi ? s.hsnap[i] : 0; }
   const bool pend = i < gp && (hs != 0 || ci > la);
   const unsigned long long m = __ballot(pend);
   __shared__ int wc[4];
@@ -874,9 +887,11 @@ __global__ __launch_bounds__(256) void k_apply_emit(Dev s, const int32_t *__rest
   off += __popcll(m & ((1ull << lane_id()) - 1));
   if (pend && off < cap) {
     oslot[off] = (int32_t)i;
-    osi[off] = hs ? s.dummy[i] : -1;                                   // raft.go:168-177
-    ost[off] = hs ? s.log[i * s.L + s.head[i]] : 0;                    // dummyTerm
-    if (hs) s.hsnap[i] = 0;
+    if (osi) {
+      osi[off] = hs ? s.dummy[i] : -1;                                 // raft.go:168-177
+      ost[off] = hs ? s.log[i * s.L + s.head[i]] : 0;                  // dummyTerm
+      if (hs) s.hsnap[i] = 0;
+    }
     ofrom[off] = la + 1;                                               // raft.go:179-190
     oto[off] = ci;
     if (ci > la) s.applied[i] = ci;                                    // :200
@@ -1343,7 +1358,8 @@ void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t c
                                   int64_t *total, hipStream_t st) {
   const int64_t gp = (int64_t)s.G * s.P;
   const int64_t nb = (gp + 255) / 256;
-  hipLaunchKernelGGL(k_apply_count, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt);
+  hipLaunchKernelGGL(k_apply_count, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt,
+                     osnap_index ? 1 : 0);
   hipLaunchKernelGGL(k_apply_scan, dim3(1), dim3(1024), 0, st, scratch_bcnt, nb, total);
   hipLaunchKernelGGL(k_apply_emit, dim3((unsigned)nb), dim3(256), 0, st, s, scratch_bcnt, cap, oslot,
                      osnap_index, osnap_term, ofrom, oto);

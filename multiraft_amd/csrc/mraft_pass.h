@@ -26,14 +26,10 @@ __device__ __forceinline__ T *at_u(T *base, int k) {
 }
 
 // Where the term of Index idx of a stream lives. Entries come from a
-// contiguous buffer (a network batch or staged copy: LinRow) or from the
-// leader's own ring (the fused tick: RingRow); followers are always rings
-// (include/mraft.h: row + (head + idx - dummy) mod L, base = head - dummy).
-struct LinRow {
-  const int32_t *p;
-  long long off;
-  __device__ __forceinline__ const int32_t *at(int idx) const { return at_u(p + off, idx); }
-};
+// contiguous buffer (a network batch or staged copy: L = INT32_MAX, never
+// wraps, base = -(the pass's first Index) so lane offsets stay small) or from
+// a ring (the leader's own row; followers are always rings; include/mraft.h:
+// row + (head + idx - dummy) mod L, base = head - dummy).
 // Every lane that loads or stores in the pass holds an Index at or above the
 // row's dummy (loads and stores are masked to [plo, phi] / [start, cend) /
 // [cfrom, nend), and a dwordx4 group aligned in the ring cannot begin below

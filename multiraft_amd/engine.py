@@ -46,6 +46,23 @@ def copy_state(st: dict) -> dict:
     return {k: np.array(v, copy=True) for k, v in st.items()}
 
 
+def entry_positions(log_head, L: int, entries_offset, n_entries) -> np.ndarray:
+    """Where, in a host copy of `log_term` ([G*P*L], include/mraft.h), the
+    entries an AppendEntries names by reference are: mraft_gather_append_args
+    sets entries_offset = slot * L + (prev + 1 - dummyIndex), the LOGICAL
+    position in that replica's ring, so entry k of item i is at
+    slot * L + (log_head[slot] + pos + k) mod L. Returns the flat indices of
+    every item's entries, item after item (a host shipping entries over the
+    network copies log_term[entry_positions(...)])."""
+    eo = np.asarray(entries_offset, dtype=np.int64)
+    n = np.maximum(np.asarray(n_entries, dtype=np.int64), 0)
+    slot, pos = eo // L, eo % L
+    item = np.repeat(np.arange(len(eo)), n)
+    within = np.arange(int(n.sum()), dtype=np.int64) - np.repeat(np.cumsum(n) - n, n)
+    head = np.asarray(log_head, dtype=np.int64)[slot][item]
+    return slot[item] * L + (head + pos[item] + within) % L
+
+
 def synth_tick_state(G: int, P: int, L: int, seed: int, g_begin: int = 0, g_end: int | None = None,
                      nthreads: int | None = None):
     """Seeded replication-tick workload (include/mraft_synth.h). Returns
@@ -138,6 +155,16 @@ class Engine:
 
     def store_state(self) -> dict:
         out = {f: np.empty(n, dtype=np.int32) for f, n in state_sizes(self.G, self.P, self.L).items()}
+        soa = soa_of(out)
+        _ck(self._lib.mraft_store_state(self._h, ctypes.byref(soa), HOST), "mraft_store_state")
+        return out
+
+    def scalar_state(self, fields=("current_term", "voted_for", "state", "commit_index", "last_applied",
+                                   "dummy_index", "last_index", "log_head", "has_snapshot")) -> dict:
+        """The per-replica scalar arrays only (no logs, no leader view): a
+        cheap host mirror of roles and terms (mraft_store_state with the
+        other arrays NULL)."""
+        out = {f: np.empty(self.G * self.P, dtype=np.int32) for f in fields}
         soa = soa_of(out)
         _ck(self._lib.mraft_store_state(self._h, ctypes.byref(soa), HOST), "mraft_store_state")
         return out
@@ -252,7 +279,11 @@ class Engine:
         cap = self.G * self.P if cap is None else cap
         sl, si, stm, fr, to = (np.zeros(max(cap, 1), np.int32) for _ in range(5))
         n = np.zeros(1, np.int64)
-        _ck(self._lib.mraft_collect_apply_compact(self._h, ptr(sl), ptr(si), ptr(stm), ptr(fr), ptr(to), cap,
+        # without snapshots the SnapshotValid outputs are NULL: hasSnapshot
+        # stays set (and snapshot-only slots do not count) until a call that
+        # takes them, as in collect_apply(snapshots=False)
+        _ck(self._lib.mraft_collect_apply_compact(self._h, ptr(sl), ptr(si) if snapshots else None,
+                                                  ptr(stm) if snapshots else None, ptr(fr), ptr(to), cap,
                                                   ptr(n), HOST), "mraft_collect_apply_compact")
         k = int(min(n[0], cap))
         if snapshots:

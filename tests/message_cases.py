@@ -4,6 +4,7 @@ gather -> handle -> fold path a host drives for network-delivered batches
 import numpy as np
 
 from multiraft_amd._abi import AE_RESULT, LEADER
+from multiraft_amd.engine import entry_positions
 
 
 def all_follower_items(lp, G, P):
@@ -16,11 +17,12 @@ def all_follower_items(lp, G, P):
     return ld[keep].astype(np.int32), peers[keep].astype(np.int32)
 
 
-def external_entries(args, ok, log_term, misalign=True):
-    """Copy every gathered item's entries (a view into the leader's log row,
-    entries_offset) into one external buffer, as the network would deliver
-    them; item j starts at a 16-B aligned position plus (j % 4) words when
-    `misalign`. Returns (args with rebased entries_offset, buffer)."""
+def external_entries(args, ok, st, L, misalign=True):
+    """Copy every gathered item's entries (a view into the leader's log ring,
+    entries_offset: a logical ring position, unrolled through log_head by
+    multiraft_amd.entry_positions) into one external buffer, as the network
+    would deliver them; item j starts at a 16-B aligned position plus (j % 4)
+    words when `misalign`. Returns (args with rebased entries_offset, buffer)."""
     a2 = args.copy()
     n = np.where(ok, args["n_entries"], 0).astype(np.int64)
     pad = (np.arange(len(args)) % 4) if misalign else np.zeros(len(args), np.int64)
@@ -30,9 +32,8 @@ def external_entries(args, ok, log_term, misalign=True):
     buf = np.zeros(total, np.int32)
     idx_item = np.repeat(np.arange(len(args)), n)
     within = np.arange(int(n.sum())) - np.repeat(np.cumsum(n) - n, n)
-    src = args["entries_offset"].astype(np.int64)[idx_item] + within
     dst = start[idx_item] + within
-    buf[dst] = log_term[src]
+    buf[dst] = st["log_term"][entry_positions(st["log_head"], L, args["entries_offset"], n)]
     a2["entries_offset"] = np.where(ok, start, 0)
     return a2, buf
 

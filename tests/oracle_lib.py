@@ -153,6 +153,10 @@ class Oracle:
     def store_state(self):
         return copy_state(self.st)
 
+    def scalar_state(self):
+        """The live state arrays (read-only use: the harness's mirror)."""
+        return self.st
+
     # ---- snapshots ---------------------------------------------------------
     def snapshot(self, slots, index):
         slots = np.ascontiguousarray(slots, dtype=np.int32)

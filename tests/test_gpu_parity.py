@@ -12,7 +12,7 @@ from kat_runner import kat_state, load_kats, run_kat  # noqa: E402
 from make_golden import check_kat  # noqa: E402
 from oracle_lib import Oracle, assert_states_equal  # noqa: E402
 
-from multiraft_amd import Engine, synth_fold_batch, synth_seed, synth_tick_state  # noqa: E402
+from multiraft_amd import Engine, entry_positions, synth_fold_batch, synth_seed, synth_tick_state  # noqa: E402
 from multiraft_amd._abi import AE_ARGS, AE_RESULT, RV_ARGS, RV_RESULT  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -129,8 +129,8 @@ def test_item_path_gpu():
         a2 = args[ok].copy()
         off = 0
         for j, a in enumerate(args[ok]):
-            s = a["entries_offset"]
-            ent.append(st["log_term"][s:s + a["n_entries"]])
+            # entries_offset is a logical ring position: unrolled through log_head
+            ent.append(st["log_term"][entry_positions(st["log_head"], L, [a["entries_offset"]], [a["n_entries"]])])
             a2["entries_offset"][j] = off
             off += a["n_entries"]
         ent = np.concatenate(ent + [np.zeros(1, np.int32)]).astype(np.int32)
@@ -396,3 +396,30 @@ def test_applier_compact_gpu(cap):
             assert n2 == n - k and np.array_equal(sl2, want[k:])
         assert e.collect_apply_compact()[3] == 0
         assert_states_equal(e.store_state(), o.state(), G, P, L, "applier compact")
+
+
+def test_applier_compact_snapshot_outputs_gpu():
+    """The compacted applier without snapshot outputs behaves as the dense
+    one without them: only commitIndex > lastApplied slots are listed and a
+    pending SnapshotValid (hasSnapshot, raft.go:168-177) stays for the call
+    that takes it; that call lists it first, with the dummy's Index and Term."""
+    G, P, L = 300, 5, 64
+    st, lp, _ = synth_tick_state(G, P, L, seed=82)
+    rng = np.random.default_rng(3)
+    hs = rng.random(G * P) < 0.2
+    st["has_snapshot"] = hs.astype(np.int32)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        ofr, oto = o.collect_apply()                        # dense, no snapshot outputs
+        want = np.nonzero(oto >= ofr)[0]
+        sl, f, t, n = e.collect_apply_compact()
+        assert n == len(want) and np.array_equal(sl, want)
+        assert np.array_equal(f, ofr[want]) and np.array_equal(t, oto[want])
+        assert np.array_equal(e.store_state()["has_snapshot"], st["has_snapshot"])   # untouched
+        ofr, oto, osi, ost = o.collect_apply(snapshots=True)
+        want = np.nonzero((oto >= ofr) | (osi >= 0))[0]
+        sl, si, stm, f, t, n = e.collect_apply_compact(snapshots=True)
+        assert n == len(want) == int(hs.sum()) and np.array_equal(sl, want)
+        assert np.array_equal(si, osi[want]) and np.array_equal(stm, ost[want])
+        assert not e.store_state()["has_snapshot"].any()
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "applier compact, snapshots")

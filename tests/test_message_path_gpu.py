@@ -40,7 +40,7 @@ def _message_round(e, o, st, slots, peers, G, P, L, mode, equal):
         rep, herr = e.handle_append_entries(args, None)
         orep, oherr = o.handle_append_entries(args, None)
     else:
-        a2, buf = external_entries(args, ok, st["log_term"], misalign=(mode == "misaligned"))
+        a2, buf = external_entries(args, ok, st, L, misalign=(mode == "misaligned"))
         a2 = a2[ok]
         rep, herr = e.handle_append_entries(a2, buf)
         orep, oherr = o.handle_append_entries(a2, buf)
@@ -156,3 +156,35 @@ def test_handle_sets_gpu(order):
         assert_states_equal(e.store_state(), o.state(), G, P, L, f"sets ({order})")
         if order == "with_errors":
             assert (herr != 0).any() and (herr == 0).any()
+
+
+def _shift_indices(st, off):
+    """The same logs with every Raft Index moved up by `off` (terms, rings and
+    every relation between indices unchanged)."""
+    st = {k: v.copy() for k, v in st.items()}
+    for k in ("dummy_index", "last_index", "commit_index", "last_applied", "match_index", "next_index"):
+        st[k] = (st[k].astype(np.int64) + off).astype(np.int32)
+    return st
+
+
+@pytest.mark.parametrize("mode", ["aligned", "misaligned", "staged"])
+def test_handle_high_indices_gpu(mode):
+    """prev_log_index above 2^30 (Go's int allows any Index; the engine any
+    below 2^31): entries from a host buffer and from the staged copy are
+    addressed relative to the pass's first Index, so nothing wraps."""
+    G, P, L = 96, 5, 256
+    off = (1 << 30) + 12345
+    st, lp, _ = synth_tick_state(G, P, L, seed=404)
+    if mode == "staged":
+        rng = np.random.default_rng(41)
+        st, slots, peers = stale_second_leader_state(st, lp, G, P, L, rng, range(0, G, 2))
+    else:
+        slots, peers = all_follower_items(lp, G, P)
+    st = _shift_indices(st, off)
+    assert int(st["dummy_index"].min()) >= off and int(st["last_index"].max()) < 2**31 - 1
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        rep, herr = _message_round(e, o, st, slots, peers, G, P, L,
+                                   "reference" if mode == "staged" else mode, assert_states_equal)
+    assert (rep["success"][herr == 0] == 1).any()

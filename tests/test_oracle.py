@@ -435,7 +435,7 @@ def test_handle_by_reference_stages_entries():
     args, gerr = a.gather_append_args(slots, peers)
     assert (gerr == 0).all()
     rep, herr = a.handle_append_entries(args, None)
-    a2, buf = external_entries(args, gerr == 0, st["log_term"], misalign=False)
+    a2, buf = external_entries(args, gerr == 0, st, L, misalign=False)
     rep2, herr2 = b.handle_append_entries(a2, buf)
     assert np.array_equal(herr, herr2) and np.array_equal(rep, rep2)
     assert_states_equal(a.state(), b.state(), G, P, L, "staged vs copied entries")

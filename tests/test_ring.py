@@ -68,8 +68,7 @@ def test_oracle_by_reference_entries_across_the_wrap():
     b.gather_append_args(slots, peers)
     ok = gerr == 0
     rep, herr = a.handle_append_entries(args, None)
-    logical = {"log_term": logical_logs(rt, G, P, L).reshape(-1)}
-    a2, buf = external_entries(args, ok, logical["log_term"])
+    a2, buf = external_entries(args, ok, rt, L)   # the ring unrolled through log_head
     rep2, herr2 = b.handle_append_entries(a2[ok], buf)
     assert np.array_equal(rep[ok], rep2) and np.array_equal(herr[ok], herr2)
     assert_states_equal(a.state(), b.state(), G, P, L, "by reference across the wrap")
@@ -133,8 +132,7 @@ def test_message_path_rotated_gpu(mode):
             rep, herr = e.handle_append_entries(args, None)
             orep, oherr = o.handle_append_entries(args, None)
         else:
-            a2, buf = external_entries(args, ok, logical_logs(rt, G, P, L).reshape(-1),
-                                       misalign=(mode == "misaligned"))
+            a2, buf = external_entries(args, ok, rt, L, misalign=(mode == "misaligned"))
             args, slots, peers = args[ok], slots[ok], peers[ok]
             rep, herr = e.handle_append_entries(a2[ok], buf)
             orep, oherr = o.handle_append_entries(a2[ok], buf)

@@ -11,7 +11,7 @@ log size under MAXLOGSIZE, no index regression after a full crash)."""
 import pytest
 
 from oracle_lib import Oracle
-from sim2b import SCENARIOS
+from sim2b import SCENARIOS, run_scenario
 
 
 def _oracle(G, P, L, st):
@@ -28,13 +28,13 @@ def _gpu(G, P, L, st):
 @pytest.mark.parametrize("name", list(SCENARIOS))
 @pytest.mark.parametrize("seed", [1, 2])
 def test_scenario_oracle(name, seed):
-    SCENARIOS[name](_oracle, seed=seed)
+    run_scenario(_oracle, name, seed)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(SCENARIOS))
 def test_scenario_gpu(name):
-    SCENARIOS[name](_gpu)
+    run_scenario(_gpu, name, 1)
 
 
 def test_persistence_is_load_bearing(monkeypatch):
@@ -43,6 +43,6 @@ def test_persistence_is_load_bearing(monkeypatch):
     check (config.go:144-163): the 2C scenarios above really restart from
     the persisted state."""
     import sim2b
-    monkeypatch.setattr(sim2b.Cluster, "_flush", lambda self: None)
+    monkeypatch.setattr(sim2b.MultiSim, "_flush", lambda self: None)
     with pytest.raises(AssertionError):
-        sim2b.persist1_2c(_oracle, seed=1)
+        run_scenario(_oracle, "Persist12C", 1)

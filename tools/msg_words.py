@@ -84,3 +84,81 @@ def handle_words(st, args, rep, herr, G, P, L, chunk=2048):
     last_after = np.where(newlast, prev + n, fl)
     words += int((merge & (args["leader_commit"] > fc) & (np.minimum(args["leader_commit"], last_after) >= 0)).sum())
     return {"words": words, "sets": n_sets, "merges": int(merge.sum()), "copied": int(np.where(copies, phi - m + 1, 0).sum())}
+
+
+def _quorum(m, me, P):
+    """h-th largest (h = P/2) of matchIndex[j != me] (raft_append_entry.go:91-98)."""
+    v = sorted((m[j] for j in range(P) if j != me), reverse=True)
+    return v[P // 2 - 1] if P // 2 >= 1 else max(v)
+
+
+def fold_words(st, res, seg, P, L):
+    """Algorithmic HBM words of one processAppendEntriesReply +
+    advanceCommitIndexForLeader batch (k_fold; raft_append_entry.go:66-105)
+    from the state before the call and the reply records, whatever kernel
+    runs it. Per reply: its record (8 words) read, its flag and error word
+    written. Per segment (one leader replica): the segment bounds (int64),
+    the replica's term, role, commit, last, dummy and ring head; nextIndex of
+    every replying peer (the gate, :73-74); matchIndex of every peer but the
+    leader's when a1 runs (:91-97); a1's log words: for each evaluation (:78)
+    the terms from min(M*, last) down to the first one equal to currentTerm,
+    or to the highest Index an earlier evaluation of the segment examined
+    (each word read once per segment); written: nextIndex (and matchIndex on
+    success) of every reply that passes the gate, commitIndex when it moves,
+    term / role / votedFor and the persist flag on a step-down.
+    Returns {"words", "a1_log_words", "segments", "evaluations"}."""
+    log = st["log_term"].reshape(-1)
+    head, dummy, last = st["log_head"], st["dummy_index"], st["last_index"]
+    term, role, commit = st["current_term"], st["state"], st["commit_index"]
+    match = st["match_index"].reshape(-1, P)
+    nxt = st["next_index"].reshape(-1, P)
+    n_seg = len(seg) - 1
+    words = 10 * len(res) + 2 * (n_seg + 1)
+    a1w = evals = 0
+    commits = commit.copy()                      # the commitIndex the fold leaves (self-check)
+    for sg in range(n_seg):
+        b, e = int(seg[sg]), int(seg[sg + 1])
+        if b >= e:
+            continue
+        s = int(res["slot"][b])
+        me = s % P
+        T, r, c = int(term[s]), int(role[s]), int(commit[s])
+        lst, d, h = int(last[s]), int(dummy[s]), int(head[s])
+        m, nx = [int(x) for x in match[s]], [int(x) for x in nxt[s]]
+        words += 6 + len(set(int(x) for x in res["peer"][b:e]))
+        t, H, a1 = T, c, False
+        wrote = 0
+        for i in range(b, e):
+            pr, rt = int(res["peer"][i]), int(res["reply_term"][i])
+            at, ap = int(res["args_term"][i]), int(res["args_prev_log_index"][i])
+            if rt > t:                                            # :67-72
+                t, r = rt, 3
+                wrote |= 1
+            elif rt == t and r == 1 and at == t and ap == nx[pr] - 1:   # :73-74
+                if int(res["reply_success"][i]):
+                    mv = int(res["args_n_entries"][i]) + ap
+                    m[pr], nx[pr] = mv, mv + 1
+                    words += 2
+                    a1 = True
+                    evals += 1
+                    top = min(_quorum(m, me, P), lst)
+                    if top > H:                                   # a1: (H, top], currentTerm = T here
+                        idx = np.arange(H + 1, top + 1)
+                        hit = np.nonzero(log[s * L + (h + idx - d) % L] == T)[0]
+                        k = int(idx[hit[-1]]) if len(hit) else H
+                        a1w += top - max(k, H + 1) + 1
+                        if k > H:
+                            c = k
+                        H = top
+                else:
+                    nx[pr] = int(res["reply_conflict_index"][i])
+                    words += 1
+        if a1:
+            words += P - 1
+        if c != int(commit[s]):
+            words += 1
+        if wrote:
+            words += 4
+        commits[s] = c
+    return {"words": words + a1w, "a1_log_words": a1w, "segments": n_seg, "evaluations": evals,
+            "commit": commits}
