@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -40,6 +41,11 @@ struct mraft_engine {
 namespace {
 
 thread_local std::string g_err;
+
+// mraft_handle_append_entries waits on the host for its plan's totals (a
+// pinned word the plan kernel writes); a stream that never reaches the plan
+// fails the call after this long instead of hanging the caller.
+constexpr int kPlanPollSeconds = 120;
 
 int fail(int code, const char *fmt, ...) {
   char buf[512];
@@ -451,10 +457,17 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
                           h->stream);
   // The plan's last workgroup writes the totals, then the sequence word.
   volatile unsigned long long *ph = h->plan_host;
+  const auto t_poll = std::chrono::steady_clock::now();
   for (unsigned spin = 1; ph[3] != h->plan_seq; ++spin) {
     if ((spin & 4095) == 0) {  // the stream drained (or failed) without the word: stop polling
       const hipError_t q = hipStreamQuery(h->stream);
-      if (q == hipErrorNotReady) continue;
+      if (q == hipErrorNotReady) {
+        // work queued ahead of the plan may take a while, but not forever (e.g.
+        // a stream waiting on a host-side dependency that never comes)
+        if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(kPlanPollSeconds))
+          return fail(MRAFT_E_HIP, "append plan not published after %d s (stream blocked?)", kPlanPollSeconds);
+        continue;
+      }
       HIP_TRY(q);
       if (ph[3] != h->plan_seq) return fail(MRAFT_E_HIP, "append plan did not publish its totals");
     }

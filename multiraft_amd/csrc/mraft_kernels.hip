@@ -272,8 +272,9 @@ __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *_
         total[4 + j] = v[j];
         host_total[j] = v[j];
       }
-      __builtin_amdgcn_s_waitcnt(0);  // the totals' stores complete before the sequence word's
-      host_total[3] = seq;            // the host polls this word
+      // the host polls the sequence word: a system-scope release orders the
+      // totals before it (one L2 write-back, in this last workgroup only)
+      __hip_atomic_store(&host_total[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       total[0] = 0;
       total[1] = 0;
       total[3] = 0;
