@@ -90,7 +90,7 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
 
     from multiraft_amd import DEVICE, Engine, _abi, synth_election_state, synth_seed, synth_tick_state
     sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from msg_words import handle_words
+    from msg_words import fold_words, handle_words
 
     out = {}
     lib = _abi.lib()
@@ -142,8 +142,17 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
         if i == 0:  # the first pass is warm-up; its inputs give the algorithmic bytes
             assert int(gerr.abs().sum()) == 0 and int(herr.abs().sum()) == 0 and int(ferr.abs().sum()) == 0
             host = {k: v.cpu().numpy() for k, v in master.items()}
-            hw = handle_words(host, args.cpu().numpy().view(_abi.AE_ARGS).reshape(-1),
-                              rep.cpu().numpy().view(_abi.AE_REPLY).reshape(-1), herr.cpu().numpy(), G, P, L)
+            args_h = args.cpu().numpy().view(_abi.AE_ARGS).reshape(-1)
+            hw = handle_words(host, args_h, rep.cpu().numpy().view(_abi.AE_REPLY).reshape(-1), herr.cpu().numpy(),
+                              G, P, L)
+            # the fold reads only leader replicas, which no message of this
+            # batch targets: their pre-handle state is the fold's input
+            res_h = res.cpu().numpy().view(_abi.AE_RESULT).reshape(-1)
+            assert not np.isin(res_h["slot"], args_h["slot"]).any()
+            fw = fold_words(host, res_h, seg.cpu().numpy(), P, L)
+            ld_sl = np.unique(res_h["slot"])
+            assert np.array_equal(fw["commit"][ld_sl], copy["commit_index"].cpu().numpy()[ld_sl]), \
+                "fold word count: replayed commits differ from the device's"
             del host
             continue
         t_call["gather"].append(e[0].elapsed_time(e[1]))
@@ -160,7 +169,15 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
         "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
-                     "sets": hw["sets"], "merges": hw["merges"]}}
+                     "sets": hw["sets"], "merges": hw["merges"]},
+        "fold_roofline": {"kernel": "mraft_process_append_replies (whole call: claim + k_fold)", "bound": "hbm",
+                          "algorithmic_bytes": 4 * fw["words"], "a1_log_bytes": 4 * fw["a1_log_words"],
+                          "achieved": 4 * fw["words"] / ms["fold"] / 1e6, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                          "frac": 4 * fw["words"] / (ms["fold"] / 1e3) / HBM_PEAK,
+                          "segments": fw["segments"], "a1_evaluations": fw["evaluations"],
+                          "note": "tools/msg_words.py fold_words: a1's log words (the Figure-8 gate's scans "
+                                  "down to the commit index) are most of the bytes; each scan is a chain of "
+                                  "dependent round trips"}}
     eng.close()
 
     # -- config #5 election storm

@@ -504,13 +504,10 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
   TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &fl));
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
   TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
-  HIP_TRY(hipMemsetAsync(fl, 0, sizeof(int32_t) * n, h->stream));
-  HIP_TRY(hipMemsetAsync(e, 0, sizeof(int32_t) * n, h->stream));
-  mraft::launch_claim(it, ns, sizeof(mraft_ae_result), offsetof(mraft_ae_result, slot),
-                      (const int64_t *)sb, gp_of(h), h->P, h->claim, h->epoch, (int32_t *)se,
-                      h->stream);
-  mraft::launch_fold(dev_of(h), (const mraft_ae_result *)it, n, (const int64_t *)sb, ns,
-                     (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
+  // two launches: the segment claims with the outputs zeroed, then the fold
+  // (which rejects a segment whose slot another one claimed)
+  mraft::launch_fold(dev_of(h), (const mraft_ae_result *)it, n, (const int64_t *)sb, ns, gp_of(h), h->claim,
+                     h->epoch, (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
   return sg.finish();
 }
 

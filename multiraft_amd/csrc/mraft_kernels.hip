@@ -51,6 +51,29 @@ __global__ void k_claim(const char *__restrict__ items, int64_t n, int stride, i
   atomicMax(&claim[slot], ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i));
 }
 
+// The reply fold's claim (mraft_process_append_replies): k_claim over the
+// segments, and the zeroing of the per-item outputs (items no segment covers
+// keep flag 0, error 0) in the same launch; the duplicate check happens in
+// k_fold itself (claim[slot] loads with the replica's state).
+__global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stride, int slot_off,
+                             const int64_t *__restrict__ seg_begin, int64_t gp,
+                             unsigned long long *__restrict__ claim, uint32_t epoch,
+                             int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
+                             int32_t *__restrict__ z1) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < nz) { z0[i] = 0; z1[i] = 0; }
+  if (i >= n) return;
+  int64_t rec = i;
+  if (seg_begin) {
+    if (seg_begin[i] >= seg_begin[i + 1]) { err[i] = 0; return; }
+    rec = seg_begin[i];
+  }
+  const int32_t slot = *(const int32_t *)(items + rec * stride + slot_off);
+  if (slot < 0 || slot >= gp) { err[i] = MRAFT_ITEM_BAD_SLOT; return; }
+  err[i] = 0;
+  atomicMax(&claim[slot], ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i));
+}
+
 __global__ void k_claim_check(const char *__restrict__ items, int64_t n, int stride, int slot_off,
                               const int64_t *__restrict__ seg_begin,
                               const unsigned long long *__restrict__ claim, uint32_t epoch,
@@ -595,34 +618,49 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #define MRAFT_FOLD_EXP 0  // timing experiments only (wrong results): 1 = no a1 log reads, 2 = probes only
 #endif
 #ifndef MRAFT_FOLD_SCANU
-#define MRAFT_FOLD_SCANU 4  // a1 scan: dword loads per lane in flight per iteration (64·U terms)
+#define MRAFT_FOLD_SCANU 4    // a1 scan, first iteration: dword loads per lane in flight (64·U terms)
+#endif
+#ifndef MRAFT_FOLD_SCANU2
+#define MRAFT_FOLD_SCANU2 12  // a1 scan, later iterations: a range still open after 64·U terms is
+                              // usually long (its top term is older than currentTerm and the log's
+                              // terms only grow: no hit below), so 768 terms per round trip (16
+                              // spills at 8 waves per SIMD)
 #endif
 
-// Highest idx in [lo, hi] with row[idx - base] == a, or lo - 1: the a1 scan
-// of the reply fold, 64·U terms per round trip (wave-uniform arguments).
+// One iteration of the a1 scan: the highest idx in [max(lo, top - 64·U + 1),
+// top] with row[idx] == a, or lo - 1 (wave-uniform arguments).
 template <int U>
+__device__ __forceinline__ int fold_scan_iter(const int32_t *__restrict__ row, int base, int head, int L,
+                                              int lo, int top, int a) {
+  const int lane = lane_id();
+  int v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int idx = top - lane - kWave * u;
+    const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the U loads issue back to back
+    v[u] = idx >= lo ? w : a + 1;
+  }
+  // Every ballot of the iteration (no early exit: an exit per vector lets
+  // the compiler sink each load behind the previous compare).
+  int r = lo - 1;
+#pragma unroll
+  for (int u = U - 1; u >= 0; --u) {
+    const unsigned long long m = __ballot(v[u] == a);
+    r = m ? top - kWave * u - first_lane(m) : r;
+  }
+  return r;
+}
+
+// Highest idx in [lo, hi] with row[idx - base] == a, or lo - 1: the a1 scan
+// of the reply fold, 64·U terms in the first round trip, 64·U2 after.
+template <int U, int U2>
 __device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row, int base, int head, int L,
                                                  int lo, int hi, int a) {
-  const int lane = lane_id();
-  for (int top = hi; top >= lo; top -= kWave * U) {
-    int v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = top - lane - kWave * u;
-      const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the U loads issue back to back
-      v[u] = idx >= lo ? w : a + 1;
-    }
-    // Every ballot of the iteration (no early exit: an exit per vector lets
-    // the compiler sink each load behind the previous compare).
-    int r = lo - 1;
-#pragma unroll
-    for (int u = U - 1; u >= 0; --u) {
-      const unsigned long long m = __ballot(v[u] == a);
-      r = m ? top - kWave * u - first_lane(m) : r;
-    }
-    if (r >= lo) return r;
-  }
-  return lo - 1;
+  if (hi < lo) return lo - 1;
+  int r = fold_scan_iter<U>(row, base, head, L, lo, hi, a);
+  for (int top = hi - kWave * U; r < lo && top >= lo; top -= kWave * U2)
+    r = fold_scan_iter<U2>(row, base, head, L, lo, top, a);
+  return r;
 }
 
 // Wave per segment (one 64-thread workgroup each). Lane k loads reply k of a
@@ -642,6 +680,7 @@ template <int P>
 __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result *__restrict__ items,
                                              const int64_t *__restrict__ seg_begin, int64_t sg,
                                              const int32_t *__restrict__ seg_err,
+                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
@@ -668,6 +707,12 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   else if (lane == 20) src = s.dummy;
   else if (lane == 21) src = s.head;
   const int vs = (src && !bad) ? src[si] : 0;
+  // items addressed to one replica slot in several segments: the lowest
+  // segment wins (k_claim_zero's atomicMax on the inverted index), the others
+  // are rejected before any state change — loaded beside the state
+  const unsigned long long cw = !bad ? claim[slot] : 0ull;
+  if (!bad && __builtin_amdgcn_readfirstlane((int)(uint32_t)cw) != (int)(0xFFFFFFFFull - (uint64_t)sg) ) bad = MRAFT_ITEM_DUP_SLOT;
+  if (!bad && (uint32_t)(cw >> 32) != epoch) bad = MRAFT_ITEM_DUP_SLOT;
   int term = __builtin_amdgcn_readlane(vs, 16), role = __builtin_amdgcn_readlane(vs, 17),
       commit = __builtin_amdgcn_readlane(vs, 18);
   const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20),
@@ -742,7 +787,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       const int src = first_lane(pend);
       pend &= pend - 1;
       const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
-      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
+      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
       if (lane == src && r >= lo) x = r;
     }
     FOLD_STAMP(4, x);
@@ -773,16 +818,17 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
 template <int P>
 __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft_ae_result *__restrict__ items,
                                              const int64_t *__restrict__ seg_begin, int64_t n_seg,
-                                             const int32_t *__restrict__ seg_err, int32_t *__restrict__ flags,
-                                             int32_t *__restrict__ item_err) {
+                                             const int32_t *__restrict__ seg_err,
+                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
   if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, flags, item_err);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, sg, seg_err, flags, item_err);
+    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err);
 }
 
 // ---------------------------------------------------------------- Start
@@ -1322,16 +1368,21 @@ extern "C" int mraft_debug_fold_trace(void *dst, long long nbytes) {
 #endif
 
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
-                 int64_t n_seg, int32_t *seg_err, int32_t *flags, int32_t *item_err,
-                 hipStream_t st) {
-  (void)n;
+                 int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
+                 int32_t *flags, int32_t *item_err, hipStream_t st) {
+  // one launch for the claims and the zeroed outputs, one for the fold
+  const int64_t nt = max(n_seg, n);
+  if (nt <= 0) return;
+  hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
+                     (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
+                     epoch, seg_err, n, flags, item_err);
   if (n_seg <= 0) return;
   const dim3 gr((unsigned)min(n_seg, (int64_t)MRAFT_FOLD_GRID)), bl(64);
   switch (s.P) {
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
-    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, seg_begin, n_seg, seg_err, flags,  \
-                       item_err);                                                             \
+    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, seg_begin, n_seg, seg_err, claim, epoch, \
+                       flags, item_err);                                                      \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)

@@ -1,0 +1,30 @@
+"""The compile-time alternatives kept in the kernel sources (DESIGN.md §5:
+each was measured against the default and lost, and stays selectable for
+A/B runs, tools/build_variants.sh) still compile for gfx950: the unpipelined
+compare / copy loops, plain (temporal) loads and stores, two dwordx4 per lane
+per compare chunk, the state pointers held across the pass, linear group
+order, four groups per workgroup, the handler without its LDS stash, and the
+fold's one-width a1 scan. CPU only (device-only compile, no GPU)."""
+import os
+import subprocess
+
+import pytest
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "multiraft_amd", "csrc")
+HIPCC = "/opt/rocm/bin/hipcc"
+
+VARIANTS = {
+    "mraft_tick.hip": ["-DMRAFT_PASS_PIPE=0", "-DMRAFT_TICK_NT=0", "-DMRAFT_TICK_V=2", "-DMRAFT_TICK_RELOAD=0",
+                       "-DMRAFT_TICK_XCD=0", "-DMRAFT_TICK_WPB=4", "-DMRAFT_TICK_MINW=6"],
+    "mraft_kernels.hip": ["-DMRAFT_AE_PIPE=0", "-DMRAFT_AE_STASH=0", "-DMRAFT_TICK_NT=1", "-DMRAFT_FOLD_XCD=1",
+                          "-DMRAFT_FOLD_SCANU2=4"],
+}
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="no hipcc")
+@pytest.mark.parametrize("src", list(VARIANTS))
+def test_alternatives_compile(src):
+    r = subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-c",
+                        *VARIANTS[src], os.path.join(CSRC, src), "-o", os.devnull],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]

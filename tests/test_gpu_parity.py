@@ -97,6 +97,37 @@ def test_fold_far_bad_slot_gpu():
         assert_states_equal(e.store_state(), o.state(), G, P, L, "fold bad slot")
 
 
+def test_fold_dup_empty_uncovered_gpu():
+    """Segments that repeat a leader slot (the lowest wins, the others are
+    MRAFT_ITEM_DUP_SLOT with no state change), empty segments, and items no
+    segment covers (flag 0, error 0): the claim and the outputs' zeroing run
+    in one launch, the duplicate check inside the fold."""
+    G, P, L = 1024, 5, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
+    items, seg = synth_fold_batch(st, G, P, L, lp, seed=synth_seed(3))
+    nseg = len(seg) - 1
+    parts, bounds = [items[:3]], [3]                     # 3 uncovered items first
+    for k in range(nseg):
+        parts.append(items[int(seg[k]):int(seg[k + 1])])
+        bounds.append(bounds[-1] + len(parts[-1]))
+        if k % 7 == 3:                                   # the same leader again, later in the batch
+            parts.append(items[int(seg[k]):int(seg[k + 1])][::-1])
+            bounds.append(bounds[-1] + len(parts[-1]))
+        if k % 11 == 5:                                  # an empty segment
+            bounds.append(bounds[-1])
+    parts.append(items[:4])                              # 4 uncovered items last
+    it2 = np.concatenate(parts)
+    sb = np.array(bounds, np.int64)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        f, err = e.process_append_replies(it2, sb)
+        of, oerr = o.process_append_replies(it2, sb)
+        assert (err == 5).any() and (err == 0).any()     # MRAFT_ITEM_DUP_SLOT
+        assert (err[:3] == 0).all() and (f[:3] == 0).all() and (err[-4:] == 0).all() and (f[-4:] == 0).all()
+        assert np.array_equal(err, oerr) and np.array_equal(f, of)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "fold dup")
+
+
 @pytest.mark.parametrize("P,seed", [(5, 24), (3, 25), (8, 26), (2, 27)])
 def test_fold_long_segments_gpu(P, seed):
     """Segments longer than one 64-reply batch, repeated peers, many a1

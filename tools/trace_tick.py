@@ -15,7 +15,7 @@ def main():
     import torch
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
     from multiraft_amd import _abi
-    G, P, L = 65536, 5, 4096
+    G, P, L = int(os.environ.get("TRACE_G", 65536)), 5, 4096
     st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
     dev = torch.device("cuda", 0)
     master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
@@ -35,6 +35,8 @@ def main():
     t = tr.reshape(G, 4).astype(np.int64)
     t -= t[:, 0].min()
     us = t / 100.0  # 100 MHz -> us
+    if os.environ.get("TRACE_SAVE"):
+        np.save(os.environ["TRACE_SAVE"], us)
     hdr, pas, tail, life = us[:, 1] - us[:, 0], us[:, 2] - us[:, 1], us[:, 3] - us[:, 2], us[:, 3] - us[:, 0]
     span = us[:, 3].max()
     print(f"span {span:.1f} us (first start {us[:,0].min():.1f}, last start {us[:,0].max():.1f}, "
