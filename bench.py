@@ -75,7 +75,7 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
+def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
     """The survey's other configurations, measured in the same run so they are
     on the driver's record (rank 0, one GPU, after the headline's timed
     region; never part of `value`):
@@ -84,8 +84,10 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
         roofline from its algorithmic bytes (tools/msg_words.py);
       * config #5, the election storm (65,536 x 7, 64 rounds per launch);
       * config #2 (1,024 x 3 x 256: cache-resident, launch-bound).
-    Each timed with HIP events on the engine's stream; `copy` is a state copy
-    the headline already used, restored from `master` before every step."""
+    Each timed with HIP events on the engine's stream; `copies` are the state
+    copies the headline already used, step i of the message path on copy i
+    restored from `master` (so its steps see both memory populations, like
+    the headline's)."""
     import torch
 
     from multiraft_amd import DEVICE, Engine, _abi, synth_election_state, synth_seed, synth_tick_state
@@ -120,6 +122,7 @@ def secondary(master, copy, lp, G, P, L, stream, dev, steps=8):
     t_call = {"gather": [], "handle": [], "fold": []}
     hw = None
     for i in range(steps + 1):
+        copy = copies[i % len(copies)]
         for k, v in master.items():
             copy[k].copy_(v)
         eng.bind(copy)
@@ -882,7 +885,7 @@ def main():
             out["roofline"]["placement_probe"] = pp
     if (world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096
             and fan is None):
-        out["secondary"] = secondary(master, clones[0], lp, G, P, L, stream, dev)  # reuses a spent copy
+        out["secondary"] = secondary(master, clones, lp, G, P, L, stream, dev)  # reuses the spent copies
         # config #4's N = 1 anchor: free config #3's copies, then all 262,144 groups on this GPU
         eng.close()
         del clones, master

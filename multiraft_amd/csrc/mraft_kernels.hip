@@ -620,6 +620,9 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #ifndef MRAFT_FOLD_SCANU
 #define MRAFT_FOLD_SCANU 4    // a1 scan, first iteration: dword loads per lane in flight (64·U terms)
 #endif
+#ifndef MRAFT_FOLD_MERGED_PROBE
+#define MRAFT_FOLD_MERGED_PROBE 1  // a batch with one a1 range scans from its top without a separate probe
+#endif
 #ifndef MRAFT_FOLD_SCANU2
 #define MRAFT_FOLD_SCANU2 12  // a1 scan, later iterations: a range still open after 64·U terms is
                               // usually long (its top term is older than currentTerm and the log's
@@ -781,14 +784,25 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     int x = -1;
     if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
     if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
-    if (plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
-    unsigned long long pend = __ballot(plo < phi && x < 0);
-    while (pend) {
-      const int src = first_lane(pend);
-      pend &= pend - 1;
-      const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
-      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
+    const unsigned long long rm = __ballot(plo <= phi);  // replies whose evaluation has a range
+    if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
+      // One range (the usual batch): no separate probe of its top word — the
+      // scan's first window starts there (one round trip fewer when the top
+      // term is not currentTerm, a 1-KiB window instead of one word when it is).
+      const int src = first_lane(rm);
+      const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64);
+      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);
       if (lane == src && r >= lo) x = r;
+    } else {
+      if (plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
+      unsigned long long pend = __ballot(plo < phi && x < 0);
+      while (pend) {
+        const int src = first_lane(pend);
+        pend &= pend - 1;
+        const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
+        const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
+        if (lane == src && r >= lo) x = r;
+      }
     }
     FOLD_STAMP(4, x);
     if (x >= 0) myfl |= MRAFT_F_COMMITTED;                               // :99-100

@@ -9,7 +9,7 @@ cd "$(dirname "$0")/../multiraft_amd/csrc"
 OUT=$(cd ../../tools && pwd)/variants
 HERE=$(pwd)
 mkdir -p "$OUT"
-rm -f "$OUT"/*.so
+[ -n "$KEEP" ] || rm -f "$OUT"/*.so
 build_one() {
   local spec="$1"
   cd "$HERE"

@@ -32,11 +32,13 @@ def main():
         torch.cuda.synchronize()
     tr = np.zeros(G * 4, dtype=np.uint64)
     assert fn(tr.ctypes.data, tr.nbytes) == 0
-    t = tr.reshape(G, 4).astype(np.int64)
+    tr = tr.reshape(G, 4)
+    xcc = (tr[:, 0] >> np.uint64(60)).astype(np.int64)   # the entry stamp carries the XCD in its top bits
+    t = (tr & np.uint64((1 << 60) - 1)).astype(np.int64)
     t -= t[:, 0].min()
     us = t / 100.0  # 100 MHz -> us
     if os.environ.get("TRACE_SAVE"):
-        np.save(os.environ["TRACE_SAVE"], us)
+        np.save(os.environ["TRACE_SAVE"], np.concatenate([us, xcc[:, None]], axis=1))
     hdr, pas, tail, life = us[:, 1] - us[:, 0], us[:, 2] - us[:, 1], us[:, 3] - us[:, 2], us[:, 3] - us[:, 0]
     span = us[:, 3].max()
     print(f"span {span:.1f} us (first start {us[:,0].min():.1f}, last start {us[:,0].max():.1f}, "

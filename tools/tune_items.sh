@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/tune_items
 for rep in $(seq 1 ${REPS:-2}); do
-for lib in tools/variants/libmraft_hip_*.so; do
+for lib in tools/variants/libmraft_hip_${VARIANTS:-*}.so; do
   tag=$(basename "$lib" .so); tag=${tag#libmraft_hip_}
   MRAFT_LIB="$PWD/$lib" STEPS=10 timeout -k 10 200 python tools/bench_items.py > gpurun_out/tune_items/$tag.$rep.json 2> gpurun_out/tune_items/$tag.$rep.err || { echo "$tag FAILED"; tail -3 gpurun_out/tune_items/$tag.$rep.err; exit 1; }
   python -c "import json; d=json.load(open('gpurun_out/tune_items/$tag.$rep.json')); print('$tag', d['ms_per_call'])"
