@@ -620,14 +620,17 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #ifndef MRAFT_FOLD_SCANU
 #define MRAFT_FOLD_SCANU 4    // a1 scan, first iteration: dword loads per lane in flight (64·U terms)
 #endif
+// Measured alternatives of the a1 scan (config #3 message path, both
+// populations of state copies, profiles/r3_experiments/fold_variants.txt):
+// a one-range batch scanning from its top without a separate probe, and 512 /
+// 768 / 1,024 / 1,280 terms per round trip after the first window (at 8, 8, 7
+// and 6 waves per SIMD) all fold in the same 0.125-0.144 ms or slower; the
+// wider windows lose (more load instructions, no fewer waits that matter).
 #ifndef MRAFT_FOLD_MERGED_PROBE
-#define MRAFT_FOLD_MERGED_PROBE 1  // a batch with one a1 range scans from its top without a separate probe
+#define MRAFT_FOLD_MERGED_PROBE 0  // 1: a batch with one a1 range scans from its top without a separate probe
 #endif
 #ifndef MRAFT_FOLD_SCANU2
-#define MRAFT_FOLD_SCANU2 12  // a1 scan, later iterations: a range still open after 64·U terms is
-                              // usually long (its top term is older than currentTerm and the log's
-                              // terms only grow: no hit below), so 768 terms per round trip (16
-                              // spills at 8 waves per SIMD)
+#define MRAFT_FOLD_SCANU2 4   // a1 scan, later iterations: dword loads per lane in flight (64·U2 terms)
 #endif
 
 // One iteration of the a1 scan: the highest idx in [max(lo, top - 64·U + 1),

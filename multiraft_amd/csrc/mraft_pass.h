@@ -354,6 +354,72 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
 // the loop will run for it: no extra traffic. (Two chunks ahead,
 // MRAFT_COPY_PIPE=2, measured no faster: the copy is memory-system-bound at 8
 // waves per SIMD, profiles/r2_experiments.)
+#ifndef MRAFT_COPY_DEPTH
+#define MRAFT_COPY_DEPTH 1  // copy-only loop: chunks loaded ahead of the one being stored
+#endif
+
+// The copy-only loop with D chunks loaded ahead (D >= 2), meant to shorten
+// the last groups of a launch (a lone wave's streaming rate is latency-bound).
+// Measured (same state copies, profiles/r3_experiments/ab_copydepth_g65536.txt):
+// D = 2, 3, 4 are all 3-4 % SLOWER than one chunk ahead (0.350 vs 0.339 ms):
+// more bytes in flight per wave only queue in the memory system. Kept as an
+// A/B alternative.
+template <int D, bool COUNT, class Src, class F>
+__device__ __forceinline__ void copy_loop_deep(const Src &src, const F &fo, int c, int nend, int plo, int phi,
+                                               int slo, int shi, int T, int &found) {
+  constexpr int NI = F::kNI;
+  constexpr int CW = 256;
+  const int lane = lane_id();
+  const int cmask = fo.copy;
+  const bool scan = slo <= shi;
+  // chunk cc is needed: a follower still copies there, or the commit scan runs there
+  auto need = [&](int cc) { return cc <= phi && ((cmask && cc < nend) || (scan && cc <= shi)); };
+  auto load = [&](int cc) {
+    int4 v = make_int4(0, 0, 0, 0);
+    if (need(cc) && cc + 4 * lane + 3 >= plo && cc + 4 * lane <= phi) v = ld4(src.at(cc + 4 * lane));
+    return v;
+  };
+  if (!need(c)) return;
+  int4 buf[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) buf[d] = load(c + d * CW);
+  for (;;) {
+    const int i0 = c + 4 * lane;
+    const int4 cur = buf[0];
+#pragma unroll
+    for (int d = 0; d + 1 < D; ++d) buf[d] = buf[d + 1];
+    buf[D - 1] = load(c + D * CW);  // issued before this chunk's stores
+    if (scan && c <= shi && c + CW - 1 >= slo) {
+      const int e[4] = {cur.x, cur.y, cur.z, cur.w};
+      int lu = -1;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u >= slo && i0 + u <= shi && e[u] == T) lu = u;
+      const unsigned long long m = __ballot(lu >= 0);
+      if (m) {
+        const int l = 63 - __clzll((long long)m);
+        found = c + 4 * l + __shfl(lu, l, 64);
+      }
+    }
+    if (!COUNT && cmask && c < nend) {
+#pragma unroll
+      for (int q = 0; q < NI; ++q) {
+        if (!((cmask >> q) & 1)) continue;
+        if (i0 + 3 < nend) {
+          st4(fo.at(q, i0), cur.x, cur.y, cur.z, cur.w);
+        } else {
+          const int e[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (i0 + u < nend) st1(fo.at(q, i0 + u), e[u]);
+        }
+      }
+    }
+    c += CW;
+    if (!need(c)) return;
+  }
+}
+
 template <bool VEC, bool COUNT, class Src, class F>
 __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, int nend, int plo, int phi,
                                           int slo, int shi, int T, int &found) {
@@ -361,6 +427,10 @@ __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, in
   constexpr int CW = 256;
   const int lane = lane_id();
   int cmask = fo.copy;
+  if constexpr (VEC && MRAFT_COPY_DEPTH > 1) {
+    copy_loop_deep<MRAFT_COPY_DEPTH, COUNT>(src, fo, c, nend, plo, phi, slo, shi, T, found);
+    return;
+  }
   if constexpr (VEC) {
     if (c > phi || (!cmask && !(slo <= shi && c <= shi))) return;
     int4 cur = make_int4(0, 0, 0, 0);

@@ -22,11 +22,14 @@ def main():
     import torch
     from multiraft_amd import DEVICE, synth_seed, synth_tick_state
     from multiraft_amd._abi import MraftSoa, STATE_FIELDS, soa_of
-    G = int(os.environ.get("GROUPS", 65536))
+    G = int(os.environ.get("TICK_GROUPS", 65536))  # (bash reserves GROUPS)
     P, L = 5, 4096
     N = int(os.environ.get("COPIES", 8))
     R = int(os.environ.get("REPS", 2))
-    libs = sorted(glob.glob(os.path.join(ROOT, "tools", "variants", "libmraft_hip_*.so")))
+    # VARIANTS: comma-separated tags or globs (the first one is the reference)
+    libs = []
+    for pat in os.environ.get("VARIANTS", "*").split(","):
+        libs += sorted(glob.glob(os.path.join(ROOT, "tools", "variants", f"libmraft_hip_{pat}.so")))
     tags = [os.path.basename(p)[len("libmraft_hip_"):-3] for p in libs]
     st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
     dev = torch.device("cuda", 0)
@@ -67,7 +70,9 @@ def main():
                     sig = [int(gf.sum())] + [int((c[k].to(torch.int64) * (1 + torch.arange(c[k].numel(), device=dev) % 7)).sum())
                                              for k in STATE_FIELDS if k != "log_term"]
                     live = c["log_term"].view(G * P, L)
-                    sig.append(int(live[:, :64].to(torch.int64).sum()))
+                    w = 1 + torch.arange(G * P, device=dev, dtype=torch.int64) % 13
+                    sig.append(int((live.sum(dim=1, dtype=torch.int64) * w).sum()))
+                    sig.append(int((live[:, 1::7].sum(dim=1, dtype=torch.int64) * w).sum()))
                     if ref is None:
                         ref = sig
                     elif sig != ref:
