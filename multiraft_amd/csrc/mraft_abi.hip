@@ -449,7 +449,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   mraft::launch_claim_ae((const mraft_ae_args *)a, n, src_n, h->L, gp_of(h), h->claim, h->srcmark, h->epoch,
                          (int32_t *)e, h->stream);
   mraft::launch_ae_set_plan((const mraft_ae_args *)a, n, src_n, h->L, ni, h->claim, h->srcmark, h->epoch,
-                            (const int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev,
+                            (int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev,
                             h->plan_host_dev, ++h->plan_seq, h->stream);
   // main launch: grid sized by the upper bound n, the set count read on the device
   mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, (const int64_t *)soff,

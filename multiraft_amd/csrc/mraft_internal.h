@@ -29,7 +29,7 @@ void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
                      unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, hipStream_t st);
 void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
                         const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
-                        const int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
+                        int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
                         unsigned long long *total, unsigned long long *host_total, unsigned long long seq,
                         hipStream_t st);
 void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,

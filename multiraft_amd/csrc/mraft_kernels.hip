@@ -171,15 +171,21 @@ struct AeKey {
   int end;      // Index of the last entry
 };
 
-enum : int { AK_ERR = -2, AK_BAD = -1, AK_RING = 0, AK_STAGED = 1, AK_WRITER = 2 };
+enum : int { AK_DUP = -3, AK_ERR = -2, AK_BAD = -1, AK_RING = 0, AK_STAGED = 1, AK_WRITER = 2 };
 
-__device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t n_log, int L,
+__device__ __forceinline__ bool ae_ref_ok(const mraft_ae_args &a, int64_t n_log, int L) {
+  return !(a.n_entries < 0 || a.entries_offset < 0 || a.entries_offset + a.n_entries > n_log ||
+           a.entries_offset % L + a.n_entries > L);
+}
+
+// Item i's kind. `dup`: check item i's claim (the plan's own duplicate-slot
+// verdict: the lowest item addressed to a slot wins, k_claim_ae's atomicMax).
+__device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t i, bool dup, int64_t n_log, int L,
                                        const unsigned long long *__restrict__ claim,
                                        const uint32_t *__restrict__ srcmark, uint32_t epoch, AeKey &key) {
   if (e) return AK_ERR;
-  if (a.n_entries < 0 || a.entries_offset < 0 || a.entries_offset + a.n_entries > n_log ||
-      a.entries_offset % L + a.n_entries > L)
-    return AK_BAD;
+  if (dup && claim[a.slot] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i))) return AK_DUP;
+  if (!ae_ref_ok(a, n_log, L)) return AK_BAD;
   key.row = a.entries_offset / L;
   key.base = (int)(a.entries_offset % L) - (a.prev_log_index + 1);
   key.end = a.prev_log_index + a.n_entries;
@@ -188,20 +194,24 @@ __device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t n_
   return AK_RING;
 }
 
-// k_claim_check for AppendEntries by reference, marking the source rows
-// this batch also writes (every claim is in place: k_claim ran before).
-__global__ void k_claim_check_mark(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L,
-                                   const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                   int32_t *__restrict__ err, uint32_t *__restrict__ srcmark) {
+// The claims of AppendEntries by reference (k_claim's slot check and
+// atomicMax), and in the same pass the source rows: srcmark[row] = epoch for
+// every row some item reads entries from. The plan then finds the items
+// whose receiving row is read by another (srcmark of their slot) and the
+// duplicate slots (claim word) itself: one launch fewer than a separate
+// check. (An item that turns out to be a duplicate still marked its source;
+// that can only stage or defer some other item needlessly, never change a
+// result: staged entries are the pre-call entries.)
+__global__ void k_claim_ae(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L, int64_t gp,
+                           unsigned long long *__restrict__ claim, uint32_t *__restrict__ srcmark, uint32_t epoch,
+                           int32_t *__restrict__ err) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= n || err[i]) return;
+  if (i >= n) return;
   const mraft_ae_args a = args[i];
-  if (claim[a.slot] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i))) {
-    err[i] = MRAFT_ITEM_DUP_SLOT;
-    return;
-  }
-  AeKey k;
-  if (ae_kind(a, 0, n_log, L, claim, nullptr, epoch, k) == AK_STAGED) srcmark[k.row] = epoch;
+  if (a.slot < 0 || a.slot >= gp) { err[i] = MRAFT_ITEM_BAD_SLOT; return; }
+  err[i] = 0;
+  atomicMax(&claim[a.slot], ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i));
+  if (a.n_entries > 0 && ae_ref_ok(a, n_log, L)) srcmark[a.entries_offset / L] = epoch;
 }
 
 // Appends `va` (when `wa`) to la and `vb` (when `wb`) to lb, with one
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *_
                                                      int64_t n_log, int L, int ni,
                                                      const unsigned long long *__restrict__ claim,
                                                      const uint32_t *__restrict__ srcmark, uint32_t epoch,
-                                                     const int32_t *__restrict__ err, int64_t *__restrict__ soff,
+                                                     int32_t *__restrict__ err, int64_t *__restrict__ soff,
                                                      int64_t *__restrict__ sets, int64_t *__restrict__ defer,
                                                      unsigned long long *__restrict__ total,
                                                      volatile unsigned long long *__restrict__ host_total,
@@ -252,11 +262,14 @@ __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *_
   const int t = threadIdx.x;
   const int64_t i = blockIdx.x * (int64_t)kAeOwn - kAeHalo + t;
   AeKey k{-1, 0, 0};
-  const int kind = (i >= 0 && i < n) ? ae_kind(args[i], err[i], n_log, L, claim, srcmark, epoch, k) : -3;
+  // err[i] holds k_claim_ae's slot verdict; the duplicate verdict is taken
+  // here from the claim word (and written by the item's owner below)
+  const int kind = (i >= 0 && i < n) ? ae_kind(args[i], err[i], i, true, n_log, L, claim, srcmark, epoch, k) : -9;
   kd[t] = kind; kr[t] = k.row; kb[t] = k.base; ke[t] = k.end;
   __syncthreads();
   const bool own = t >= kAeHalo && t < kAeHalo + kAeOwn && i < n;
   if (own) {
+    if (kind == AK_DUP) err[i] = MRAFT_ITEM_DUP_SLOT;
     int64_t o = -1;
     if (kind == AK_STAGED) o = (int64_t)atomicAdd(&total[0], (unsigned long long)args[i].n_entries);
     else if (kind >= AK_RING) o = -2;
@@ -1325,16 +1338,13 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
 void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp,
                      unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_claim, dim3(blocks_for(n)), dim3(kBlock), 0, st, (const char *)args, n,
-                     (int)sizeof(mraft_ae_args), (int)offsetof(mraft_ae_args, slot), (const int64_t *)nullptr, gp, 0,
-                     claim, epoch, err);
-  hipLaunchKernelGGL(k_claim_check_mark, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, claim, epoch,
-                     err, srcmark);
+  hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, gp, claim, srcmark,
+                     epoch, err);
 }
 
 void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
                         const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
-                        const int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
+                        int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
                         unsigned long long *total, unsigned long long *host_total, unsigned long long seq,
                         hipStream_t st) {
   if (n <= 0) return;

@@ -30,8 +30,11 @@ build_one() {
   g++ -O3 -std=c++17 -fPIC -c mraft_persist.cpp -o build_$tag/mraft_persist.o &
   g++ -O3 -std=c++17 -fPIC -c mraft_router.cpp -o build_$tag/mraft_router.o &
   wait
+  for f in mraft_abi mraft_kernels mraft_tick mraft_elect mraft_persist mraft_router; do
+    [ -f build_$tag/$f.o ] || { echo "variant $tag: $f did not compile" >&2; rm -rf build_$tag; return 1; }
+  done
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUT"/libmraft_hip_$tag.so build_$tag/*.o \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined || return 1
   rm -rf build_$tag
   printf "%s " "$tag"; /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mcode-object-version=5 \
       $defs -Rpass-analysis=kernel-resource-usage -c mraft_tick.hip -o /dev/null 2>&1 | \
