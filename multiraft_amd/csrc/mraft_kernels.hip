@@ -623,8 +623,14 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #ifndef MRAFT_FOLD_XCD
 #define MRAFT_FOLD_XCD 0  // 1: XCD-contiguous segment ranges
 #endif
+#ifndef MRAFT_FOLD_GROUP
+#define MRAFT_FOLD_GROUP 4  // reply segments per wave (16 lanes each) when every one has <= 16 replies; 1: one per wave
+#endif
 #ifndef MRAFT_FOLD_MINW
-#define MRAFT_FOLD_MINW 8  // __launch_bounds__ minimum waves per SIMD of the reply fold (8: SGPRs spill to VGPR lanes, 13 % faster than 7 waves)
+// __launch_bounds__ minimum waves per SIMD of the reply fold: one segment per
+// wave, 8 (SGPRs spill to VGPR lanes; 13 % faster than 7); four per wave, 6
+// (80 VGPRs, no scratch; at 8 the per-lane fold state spills 72 B/lane)
+#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP == 4 ? 6 : 8)
 #endif
 
 #ifndef MRAFT_FOLD_EXP
@@ -845,9 +851,156 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   FOLD_STAMP(5, commit);
 }
 
+// Group helpers: the wave as four 16-lane groups, group j on lanes 16j..16j+15.
+__device__ __forceinline__ int g16_base() { return (int)(lane_id() & ~15u); }
+__device__ __forceinline__ unsigned g16_mask(bool pred) {  // this lane's group's ballot, bit k = lane 16j+k
+  return (unsigned)((__ballot(pred) >> g16_base()) & 0xFFFFull);
+}
+__device__ __forceinline__ int g16_bcast(int v, int k) { return __shfl(v, g16_base() + k, 64); }
+
+// fold_segment for four segments at once, one per 16-lane group: the same
+// statements on per-group (not wave-uniform) values, so four segments' chains
+// of dependent loads (bounds -> replies -> replica state -> probes -> scans)
+// overlap in one wave. Only segments of at most 16 replies: a wave whose four
+// segments include a longer one folds them one by one on all 64 lanes.
+template <int P>
+__device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result *__restrict__ items,
+                                            int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t sg0,
+                                            int64_t n_seg, const int32_t *__restrict__ seg_err,
+                                            const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                            int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
+  const int lane = lane_id(), gl = lane & 15;
+  const int64_t sg = sg0 + (lane >> 4);
+  const bool live = sg < n_seg;
+  int64_t b = 0, e = 0;
+  int bad = 0;
+  if (live) {
+    b = seg_begin ? seg_begin[sg] : sg;
+    e = seg_begin ? seg_begin[sg + 1] : sg + 1;
+    bad = seg_err[sg];  // the claim verdict: a bad segment's slot may be out of range
+  }
+  const int cnt = (int)(e > b ? min(e - b, (int64_t)17) : 0);  // 0: nothing to fold (empty or inverted)
+  if (__ballot(cnt > 16)) {  // a segment longer than a group: all four on the 64-lane path
+    for (int j = 0; j < 4; ++j)
+      if (sg0 + j < n_seg) fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err);
+    return;
+  }
+  (void)n_items;
+  mraft_ae_result it{};
+  if (gl < cnt) it = items[b + gl];
+  const int slot = g16_bcast(it.slot, 0);
+  const int me = cnt ? slot % P : 0;
+  const int64_t mrow = (int64_t)slot * P;
+  // The replica's state, two loads per lane: lanes 0..P-1 matchIndex, 8..8+P-1
+  // nextIndex; lanes 16.. of the second load the scalars.
+  int va = 0, vb = 0;
+  if (cnt && !bad) {
+    if (gl < P) va = s.match[mrow + gl];
+    else if (gl >= 8 && gl < 8 + P) va = s.next[mrow + gl - 8];
+    const int32_t *src = gl == 0 ? s.term : gl == 1 ? s.role : gl == 2 ? s.commit : gl == 3 ? s.last
+                         : gl == 4 ? s.dummy : gl == 5 ? s.head : nullptr;
+    if (src) vb = src[slot];
+  }
+  // a slot claimed by an earlier segment of the batch: rejected (k_fold's check)
+  const unsigned long long cw = (cnt && !bad) ? claim[slot] : 0ull;
+  if (cnt && !bad && ((uint32_t)cw != (uint32_t)(0xFFFFFFFFull - (uint64_t)sg) || (uint32_t)(cw >> 32) != epoch))
+    bad = MRAFT_ITEM_DUP_SLOT;
+  int term = g16_bcast(vb, 0), role = g16_bcast(vb, 1), commit = g16_bcast(vb, 2);
+  const int last = g16_bcast(vb, 3), dummy = g16_bcast(vb, 4), head = g16_bcast(vb, 5);
+  if (g16_mask(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)))
+    bad = MRAFT_ITEM_BAD_SLOT;
+  if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
+  if (bad) {
+    if (gl < cnt) { item_err[b + gl] = bad; flags[b + gl] = 0; }
+  }
+  const bool go = cnt && !bad;
+  int m[8], nx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    m[j] = j < P ? g16_bcast(va, j) : 0;
+    nx[j] = j < P ? g16_bcast(va, 8 + j) : 0;
+  }
+  const int c0 = commit, t0 = term, r0 = role;
+  const int32_t *lrow = s.log + (int64_t)slot * s.L;
+  bool touched_mn = false;
+  int H = commit;
+  int nmax = 0;
+  for (int k = 0; k < 16; ++k)
+    if (__ballot(go && k < cnt)) nmax = k + 1;
+  int myfl = 0, plo = 1, phi = 0;  // this lane's reply: flags and a1 range
+  for (int k = 0; k < nmax; ++k) {
+    const int pr = g16_bcast(it.peer, k), rt = g16_bcast(it.reply_term, k);
+    const int at = g16_bcast(it.args_term, k), ap = g16_bcast(it.args_prev_log_index, k);
+    const int rs = g16_bcast(it.reply_success, k), rn = g16_bcast(it.args_n_entries, k);
+    const int rci = g16_bcast(it.reply_conflict_index, k);
+    if (go && k < cnt) {
+      int fl = 0, nxp = 0;
+#pragma unroll
+      for (int j = 0; j < P; ++j) if (j == pr) nxp = nx[j];
+      if (rt > term) {                                                   // :67-72
+        term = rt; role = kFollower;
+        fl |= MRAFT_F_STEPPED_DOWN;
+      } else if (rt == term && role == kLeader && at == term && ap == nxp - 1) {  // :73-74
+        fl |= MRAFT_F_APPLIED;
+        touched_mn = true;
+        if (rs) {
+          const int mv = rn + ap;                                        // :76
+          nxp = mv + 1;                                                  // :77
+#pragma unroll
+          for (int j = 0; j < P; ++j) if (j == pr) m[j] = mv;
+          const int top = min(quorum_rt<P>(m, me), last);                // a1, :78
+          if (top > H) {
+            if (gl == k) { plo = H + 1; phi = top; }
+            H = top;
+          }
+        } else {
+          nxp = rci;                                                     // :82
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) if (j == pr) nx[j] = nxp;
+        if (nxp < last + 1) fl |= MRAFT_F_NEED_MORE;                     // :84-86
+      }
+      if (gl == k) myfl = fl;
+    }
+  }
+  // a1's ranges of each group: every top word probed at once, the others scanned
+  int x = -1;
+  if (go && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
+  // the ranges whose top word differs, of all four groups, one after another
+  // with the whole wave (a 16-lane scan moves a quarter of the terms per round
+  // trip and measured 33 % slower over the call)
+  for (unsigned long long pw = __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
+    const int src = first_lane(pw);
+    const int lo = __builtin_amdgcn_readlane(plo, src), hi = __builtin_amdgcn_readlane(phi, src) - 1;
+    const int sslot = __builtin_amdgcn_readlane(slot, src), sd = __builtin_amdgcn_readlane(dummy, src),
+              sh = __builtin_amdgcn_readlane(head, src), st0 = __builtin_amdgcn_readlane(t0, src);
+    const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(s.log + (int64_t)sslot * s.L, sd, sh, s.L,
+                                                                         lo, hi, st0);  // lo - 1 if none
+    if (lane == src && r >= lo) x = r;
+  }
+  if (go && x >= 0) myfl |= MRAFT_F_COMMITTED;                           // :99-100
+  const unsigned fm = g16_mask(go && x >= 0);
+  if (fm) commit = __shfl(x, g16_base() + 31 - __clz((int)fm), 64);      // the latest range that found one
+  if (go && gl < cnt) {
+    flags[b + gl] = myfl;
+    item_err[b + gl] = 0;
+  }
+  if (go && gl == 0 && (term != t0 || role != r0)) {
+    s.term[slot] = term; s.role[slot] = role; s.voted[slot] = -1;
+    mark_persist(s, slot, MRAFT_PERSIST_STATE);                          // :72
+  }
+  if (go && gl == 0 && commit != c0) s.commit[slot] = commit;
+  if (go && touched_mn) {
+    int om = 0, on = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) if (gl == j) { om = m[j]; on = nx[j]; }
+    if (gl < P) { s.match[mrow + gl] = om; s.next[mrow + gl] = on; }
+  }
+}
+
 template <int P>
 __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft_ae_result *__restrict__ items,
-                                             const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                                             int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t n_seg,
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
@@ -855,6 +1008,11 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
     if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err);
+    return;
+  }
+  if (MRAFT_FOLD_GROUP == 4) {
+    for (int64_t sg0 = 4 * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += 4 * (int64_t)gridDim.x)
+      fold_group4<P>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
@@ -1404,11 +1562,12 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
                      epoch, seg_err, n, flags, item_err);
   if (n_seg <= 0) return;
-  const dim3 gr((unsigned)min(n_seg, (int64_t)MRAFT_FOLD_GRID)), bl(64);
+  const int64_t waves = MRAFT_FOLD_GROUP == 4 ? (n_seg + 3) / 4 : n_seg;
+  const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
   switch (s.P) {
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
-    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, seg_begin, n_seg, seg_err, claim, epoch, \
+    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
                        flags, item_err);                                                      \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)

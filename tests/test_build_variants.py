@@ -17,7 +17,7 @@ VARIANTS = {
     "mraft_tick.hip": ["-DMRAFT_PASS_PIPE=0", "-DMRAFT_TICK_NT=0", "-DMRAFT_TICK_V=2", "-DMRAFT_TICK_RELOAD=0",
                        "-DMRAFT_TICK_XCD=0", "-DMRAFT_TICK_WPB=4", "-DMRAFT_TICK_MINW=6", "-DMRAFT_COPY_DEPTH=3"],
     "mraft_kernels.hip": ["-DMRAFT_AE_PIPE=0", "-DMRAFT_AE_STASH=0", "-DMRAFT_TICK_NT=1", "-DMRAFT_FOLD_XCD=1",
-                          "-DMRAFT_FOLD_SCANU2=12", "-DMRAFT_FOLD_MERGED_PROBE=1"],
+                          "-DMRAFT_FOLD_SCANU2=12", "-DMRAFT_FOLD_MERGED_PROBE=1", "-DMRAFT_FOLD_GROUP=1"],
 }
 
 

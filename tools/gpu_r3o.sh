@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 3, call O: the reply fold with four segments per wave — parity (fold,
+# message path, ring, scenario replays on one group and on many) and A/B
+# against one segment per wave on the config #3 message path.
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r3o
+mkdir -p "$OUT"
+export MRAFT_SIM_PROGRESS=1000
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_message_path_gpu.py tests/test_ring.py tests/test_sim2b.py tests/test_sim_many.py -m gpu -x -q -s \
+  --timeout 800 --timeout-method thread > "$OUT/tests.txt" 2>&1 || { echo "FAILED tests"; grep -E "FAILED|Error|assert" "$OUT/tests.txt" | head -20; tail -30 "$OUT/tests.txt"; exit 1; }
+tail -2 "$OUT/tests.txt"
+REPS=3 VARIANTS="k*" bash tools/tune_items.sh || exit 1
