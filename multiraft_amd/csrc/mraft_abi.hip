@@ -504,10 +504,13 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
   TRY(sg.map(out_flags, sizeof(int32_t) * n, false, true, &fl));
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
   TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
-  // two launches: the segment claims with the outputs zeroed, then the fold
-  // (which rejects a segment whose slot another one claimed)
+  void *sc;
+  TRY(scratch(h, 7, mraft::fold_scan_bytes(n), &sc));
+  // three launches: the segment claims with the outputs zeroed, the fold
+  // (which rejects a segment whose slot another one claimed), the a1 scans
+  // its probes left open
   mraft::launch_fold(dev_of(h), (const mraft_ae_result *)it, n, (const int64_t *)sb, ns, gp_of(h), h->claim,
-                     h->epoch, (int32_t *)se, (int32_t *)fl, (int32_t *)e, h->stream);
+                     h->epoch, (int32_t *)se, (int32_t *)fl, (int32_t *)e, sc, h->stream);
   return sg.finish();
 }
 

@@ -59,9 +59,13 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
                              const int64_t *__restrict__ seg_begin, int64_t gp,
                              unsigned long long *__restrict__ claim, uint32_t epoch,
                              int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
-                             int32_t *__restrict__ z1) {
+                             int32_t *__restrict__ z1, int2 *__restrict__ z2) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < nz) { z0[i] = 0; z1[i] = 0; }
+  if (i < nz) {
+    z0[i] = 0;
+    z1[i] = 0;
+    if (z2) z2[i] = make_int2(0, -1);  // no a1 range pending for k_fold_scan
+  }
   if (i >= n) return;
   int64_t rec = i;
   if (seg_begin) {
@@ -352,18 +356,60 @@ enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE
 #define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
 #endif
 
+#ifndef MRAFT_AE_RELOAD
+#define MRAFT_AE_RELOAD 1  // after the pass, kernel arguments re-read from the kernarg segment (not held across it)
+#endif
+
+// Every argument of k_handle_set, as its one kernel argument: the handler
+// re-reads them from the kernel-argument segment after the streaming pass
+// (reload_hs) instead of holding ~16 pointers live across it (at 8 waves per
+// SIMD they spilled through VGPR lanes to scratch: 28 B per lane, ~100 MB of
+// scratch write-back per config-#3 call).
+struct HsArgs {
+  Dev s;
+  const mraft_ae_args *args;
+  int64_t n;
+  const int32_t *ent0;
+  int64_t n_ent0;
+  const int32_t *stage;
+  int64_t n_stage;
+  const int64_t *soff, *sets;
+  int64_t n_sets;
+  const unsigned long long *set_count;
+  mraft_ae_reply *rep;
+  int32_t *err;
+};
+
+__device__ __forceinline__ HsArgs reload_hs() {
+  const __attribute__((address_space(4))) HsArgs *kp =
+      (const __attribute__((address_space(4))) HsArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  HsArgs k;
+  k.s.term = kp->s.term; k.s.voted = kp->s.voted; k.s.role = kp->s.role; k.s.commit = kp->s.commit;
+  k.s.applied = kp->s.applied; k.s.dummy = kp->s.dummy; k.s.last = kp->s.last; k.s.votes = kp->s.votes;
+  k.s.log = kp->s.log; k.s.match = kp->s.match; k.s.next = kp->s.next; k.s.pdirty = kp->s.pdirty;
+  k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
+  k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
+  k.n_stage = kp->n_stage; k.soff = kp->soff; k.sets = kp->sets; k.n_sets = kp->n_sets;
+  k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err;
+  return k;
+}
+
 template <int NI>
-__device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__restrict__ args,
-                                           const int32_t *__restrict__ ent0, int64_t n_ent0,
-                                           const int32_t *__restrict__ stage, int64_t n_stage,
-                                           const int64_t *__restrict__ soff, int64_t first, int size,
-                                           mraft_ae_reply *__restrict__ rep, int32_t *__restrict__ err) {
+__device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int size) {
+  const Dev &s = k0.s;
+  const mraft_ae_args *__restrict__ args = k0.args;
+  const int32_t *__restrict__ ent0 = k0.ent0;
+  const int64_t n_ent0 = k0.n_ent0;
+  const int32_t *__restrict__ stage = k0.stage;
+  const int64_t n_stage = k0.n_stage;
+  const int64_t *__restrict__ soff = k0.soff;
   const int lane = lane_id();
   const bool mine = lane < size;
-  const int64_t i = first + (mine ? lane : 0);
+  int64_t i = first + (mine ? lane : 0);
   // Three round trips before the pass: the item (error word, args, plan),
   // the follower's scalars, log[prev].
-  const int e = mine ? err[i] : 1;
+  const int e = mine ? k0.err[i] : 1;
   mraft_ae_args a = args[i];
   const int64_t so = soff ? soff[i] : -1;
   asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
@@ -491,13 +537,15 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
 #if MRAFT_AE_STASH
     // This lane's reply inputs wait in LDS during the pass (the pass needs
     // the registers: at 8 waves per SIMD they would spill to scratch).
-    __shared__ int stash[8][64];
-    {
-      volatile int *st = &stash[0][0];
-      st[0 * 64 + lane] = cls; st[1 * 64 + lane] = f; st[2 * 64 + lane] = fterm; st[3 * 64 + lane] = flast;
-      st[4 * 64 + lane] = fc; st[5 * 64 + lane] = a.term; st[6 * 64 + lane] = a.leader_commit;
-      st[7 * 64 + lane] = r.conflict_index;
-    }
+    // (plain LDS stores and loads across a compiler memory barrier: a
+    // volatile generic pointer made them flat accesses with 64-bit addresses
+    // the compiler hoisted and spilled)
+    __shared__ int stash[11][64];
+    stash[0][lane] = cls; stash[1][lane] = f; stash[2][lane] = fterm; stash[3][lane] = flast;
+    stash[4][lane] = fc; stash[5][lane] = a.term; stash[6][lane] = a.leader_commit;
+    stash[7][lane] = r.conflict_index; stash[8][lane] = r.term;
+    stash[9][lane] = (int)(uint32_t)(uint64_t)i; stash[10][lane] = (int)((uint64_t)i >> 32);
+    asm volatile("" ::: "memory");
 #endif
     if (vec) {
       int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
@@ -513,12 +561,19 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
       copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
     }
 #if MRAFT_AE_STASH
-    {
-      volatile int *st = &stash[0][0];
-      cls = st[0 * 64 + lane]; f = st[1 * 64 + lane]; fterm = st[2 * 64 + lane]; flast = st[3 * 64 + lane];
-      fc = st[4 * 64 + lane]; a.term = st[5 * 64 + lane]; a.leader_commit = st[6 * 64 + lane];
-      r.conflict_index = st[7 * 64 + lane];
-    }
+    asm volatile("" ::: "memory");
+    cls = stash[0][lane]; f = stash[1][lane]; fterm = stash[2][lane]; flast = stash[3][lane];
+    fc = stash[4][lane]; a.term = stash[5][lane]; a.leader_commit = stash[6][lane];
+    r.conflict_index = stash[7][lane]; r.term = stash[8][lane];
+    i = (int64_t)(((uint64_t)(uint32_t)stash[10][lane] << 32) | (uint32_t)stash[9][lane]);
+#endif
+#if MRAFT_AE_RELOAD
+    const HsArgs kr = reload_hs();
+    int32_t *__restrict__ err = kr.err;
+    mraft_ae_reply *__restrict__ rep = kr.rep;
+#else
+    int32_t *__restrict__ err = k0.err;
+    mraft_ae_reply *__restrict__ rep = k0.rep;
 #endif
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
@@ -535,21 +590,31 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
       }
     }
   }
+#if MRAFT_AE_RELOAD
+  const HsArgs kt = reload_hs();
+  const Dev &s2 = kt.s;
+  int32_t *__restrict__ err2 = kt.err;
+  mraft_ae_reply *__restrict__ rep2 = kt.rep;
+#else
+  const Dev &s2 = k0.s;
+  int32_t *__restrict__ err2 = k0.err;
+  mraft_ae_reply *__restrict__ rep2 = k0.rep;
+#endif
   if (cls == AE_NONE) {
-    if (mine) rep[i] = r;
+    if (mine) rep2[i] = r;
   } else if (cls == AE_BAD) {
-    rep[i] = r;
-    err[i] = MRAFT_ITEM_BAD_SLOT;
+    rep2[i] = r;
+    err2[i] = MRAFT_ITEM_BAD_SLOT;
   } else if (cls == AE_STALE) {
-    rep[i] = r;
-    mark_persist(s, f, MRAFT_PERSIST_STATE);                           // deferred :111
+    rep2[i] = r;
+    mark_persist(s2, f, MRAFT_PERSIST_STATE);                          // deferred :111
   } else if (cls >= AE_BELOW) {
-    if (a.term > fterm) { s.term[f] = a.term; s.voted[f] = -1; }      // :116-118
-    s.role[f] = kFollower;                                             // :120
-    if (newlast >= 0) s.last[f] = newlast;
-    if (fcommit_new >= 0) s.commit[f] = fcommit_new;
-    mark_persist(s, f, MRAFT_PERSIST_STATE);                           // deferred :111
-    rep[i] = r;
+    if (a.term > fterm) { s2.term[f] = a.term; s2.voted[f] = -1; }    // :116-118
+    s2.role[f] = kFollower;                                            // :120
+    if (newlast >= 0) s2.last[f] = newlast;
+    if (fcommit_new >= 0) s2.commit[f] = fcommit_new;
+    mark_persist(s2, f, MRAFT_PERSIST_STATE);                          // deferred :111
+    rep2[i] = r;
   }
 }
 
@@ -558,15 +623,9 @@ __device__ __forceinline__ void handle_one(const Dev &s, const mraft_ae_args *__
 // ... (grid a multiple of 8: each XCD keeps its contiguous range of sets,
 // neighbouring sets share one L2).
 template <int NI>
-__global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(Dev s, const mraft_ae_args *__restrict__ args,
-                                                                  int64_t n, const int32_t *__restrict__ ent0,
-                                                                  int64_t n_ent0, const int32_t *__restrict__ stage,
-                                                                  int64_t n_stage, const int64_t *__restrict__ soff,
-                                                                  const int64_t *__restrict__ sets, int64_t n_sets,
-                                                                  const unsigned long long *__restrict__ set_count,
-                                                                  mraft_ae_reply *__restrict__ rep,
-                                                                  int32_t *__restrict__ err) {
-  const int64_t nb = sets ? (set_count ? (int64_t)*set_count : n_sets) : n;
+__global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(HsArgs ka) {
+  const int64_t *__restrict__ sets = ka.sets;
+  const int64_t nb = sets ? (ka.set_count ? (int64_t)*ka.set_count : ka.n_sets) : ka.n;
   for (int64_t v = blockIdx.x;; v += gridDim.x) {
     int64_t gb = v;
     if (MRAFT_AE_XCD) {
@@ -578,9 +637,9 @@ __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(Dev s, const m
     }
     if (sets) {
       const int64_t h = sets[gb];
-      handle_one<NI>(s, args, ent0, n_ent0, stage, n_stage, soff, h >> 3, (int)(h & 7) + 1, rep, err);
+      handle_one<NI>(ka, h >> 3, (int)(h & 7) + 1);
     } else {
-      handle_one<NI>(s, args, ent0, n_ent0, stage, n_stage, soff, gb, 1, rep, err);
+      handle_one<NI>(ka, gb, 1);
     }
   }
 }
@@ -851,6 +910,55 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   FOLD_STAMP(5, commit);
 }
 
+#ifndef MRAFT_FOLD_SPLIT
+#define MRAFT_FOLD_SPLIT 1  // the four-segment fold's a1 scans in a second launch (k_fold_scan)
+#endif
+#ifndef MRAFT_FSCAN_W
+#define MRAFT_FSCAN_W 4     // replies per k_fold_scan wave
+#endif
+#ifndef MRAFT_FSCAN_U
+#define MRAFT_FSCAN_U 8     // k_fold_scan: dword loads per lane in flight (64·U terms per round trip; 4: +7 %)
+#endif
+
+// a1's scans of the reply fold (raft_append_entry.go:89-105; the loop reads
+// terms from the top of the range down to the first one equal to currentTerm),
+// for the ranges k_fold's probes left open: wave per MRAFT_FSCAN_W replies, each
+// pending range scanned with the whole wave from its top down, stopping at the
+// first hit as Go does. Split from k_fold so the scans of every segment stream
+// at once instead of behind each segment's chain of dependent loads (bounds ->
+// replies -> replica state -> probe). A hit sets MRAFT_F_COMMITTED on its reply
+// and raises the replica's commitIndex (atomicMax: several waves may hold
+// ranges of one segment).
+__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int2 *__restrict__ pend,
+                                                     const int4 *__restrict__ prec, int64_t n,
+                                                     int32_t *__restrict__ flags) {
+  const int lane = lane_id();
+  const int64_t i = (int64_t)blockIdx.x * MRAFT_FSCAN_W + lane;
+  int lo = 0, hi = -1;
+  if (lane < MRAFT_FSCAN_W && i < n) {
+    const int2 v = pend[i];
+    lo = v.x;
+    hi = v.y;
+  }
+  const unsigned long long pm = __ballot(hi >= lo);
+  if (!pm) return;
+  int4 r = make_int4(0, 0, 0, 0);
+  if (hi >= lo) r = prec[i];
+  const int L = s.L;
+  for (unsigned long long m = pm; m; m &= m - 1) {
+    const int k = first_lane(m);
+    const int klo = __builtin_amdgcn_readlane(lo, k), khi = __builtin_amdgcn_readlane(hi, k);
+    const int kslot = __builtin_amdgcn_readlane(r.x, k), kt0 = __builtin_amdgcn_readlane(r.y, k);
+    const int kd = __builtin_amdgcn_readlane(r.z, k), kh = __builtin_amdgcn_readlane(r.w, k);
+    const int x = fold_scan_down_eq<MRAFT_FSCAN_U, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
+                                                                  kt0);  // klo - 1 if none
+    if (lane == k && x >= klo) {
+      flags[i] |= MRAFT_F_COMMITTED;                                     // :99-100
+      atomicMax(&s.commit[kslot], x);
+    }
+  }
+}
+
 // Group helpers: the wave as four 16-lane groups, group j on lanes 16j..16j+15.
 __device__ __forceinline__ int g16_base() { return (int)(lane_id() & ~15u); }
 __device__ __forceinline__ unsigned g16_mask(bool pred) {  // this lane's group's ballot, bit k = lane 16j+k
@@ -868,7 +976,8 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
                                             int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t sg0,
                                             int64_t n_seg, const int32_t *__restrict__ seg_err,
                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                            int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
+                                            int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                            int2 *__restrict__ pend, int4 *__restrict__ prec) {
   const int lane = lane_id(), gl = lane & 15;
   const int64_t sg = sg0 + (lane >> 4);
   const bool live = sg < n_seg;
@@ -966,10 +1075,21 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
   // a1's ranges of each group: every top word probed at once, the others scanned
   int x = -1;
   if (go && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
+  if (pend) {
+    // the ranges whose top word differs are scanned by k_fold_scan, after this
+    // launch: it ORs MRAFT_F_COMMITTED into the reply's flags and raises the
+    // replica's commitIndex to the highest index it finds (the ranges of a
+    // segment are disjoint and ascending, so "the latest range that found
+    // one" is the maximum over all of them, probes included)
+    if (go && plo < phi && x < 0) {
+      pend[b + gl] = make_int2(plo, phi - 1);
+      prec[b + gl] = make_int4(slot, t0, dummy, head);
+    }
+  }
   // the ranges whose top word differs, of all four groups, one after another
   // with the whole wave (a 16-lane scan moves a quarter of the terms per round
   // trip and measured 33 % slower over the call)
-  for (unsigned long long pw = __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
+  for (unsigned long long pw = pend ? 0ull : __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
     const int src = first_lane(pw);
     const int lo = __builtin_amdgcn_readlane(plo, src), hi = __builtin_amdgcn_readlane(phi, src) - 1;
     const int sslot = __builtin_amdgcn_readlane(slot, src), sd = __builtin_amdgcn_readlane(dummy, src),
@@ -1003,7 +1123,8 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
                                              int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t n_seg,
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
+                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                             int2 *__restrict__ pend, int4 *__restrict__ prec) {
   if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
@@ -1012,7 +1133,7 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
   }
   if (MRAFT_FOLD_GROUP == 4) {
     for (int64_t sg0 = 4 * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += 4 * (int64_t)gridDim.x)
-      fold_group4<P>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err);
+      fold_group4<P>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend, prec);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
@@ -1526,8 +1647,8 @@ static void launch_set(const Dev &s, const mraft_ae_args *args, int64_t n, const
   // MRAFT_AE_SPB sets of the bound (grid a multiple of 8, see k_handle_set)
   int64_t nb = sets ? n_sets : n;
   if (set_count) nb = ((nb + MRAFT_AE_SPB - 1) / MRAFT_AE_SPB + 7) / 8 * 8;
-  hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, s, args, n, ent, n_ent, stage, n_stage,
-                     soff, sets, n_sets, set_count, rep, err);
+  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err};
+  hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, ka);
 }
 
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
@@ -1554,13 +1675,18 @@ extern "C" int mraft_debug_fold_trace(void *dst, long long nbytes) {
 
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
-                 int32_t *flags, int32_t *item_err, hipStream_t st) {
-  // one launch for the claims and the zeroed outputs, one for the fold
+                 int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st) {
+  // one launch for the claims and the zeroed outputs, one for the fold, one
+  // for the a1 scans the fold's probes left open (MRAFT_FOLD_SPLIT; scan_buf:
+  // fold_scan_bytes(n) of scratch)
   const int64_t nt = max(n_seg, n);
   if (nt <= 0) return;
+  const bool split = MRAFT_FOLD_SPLIT && MRAFT_FOLD_GROUP == 4 && scan_buf && n > 0;
+  int2 *pend = split ? (int2 *)scan_buf : nullptr;
+  int4 *prec = split ? (int4 *)((char *)scan_buf + ((sizeof(int2) * (size_t)n + 15) & ~(size_t)15)) : nullptr;
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
-                     epoch, seg_err, n, flags, item_err);
+                     epoch, seg_err, n, flags, item_err, pend);
   if (n_seg <= 0) return;
   const int64_t waves = MRAFT_FOLD_GROUP == 4 ? (n_seg + 3) / 4 : n_seg;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
@@ -1568,13 +1694,20 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err);                                                      \
+                       flags, item_err, pend, prec);                                          \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
 #undef MRAFT_FOLD_CASE
-    default: break;
+    default: return;
   }
+  if (split)
+    hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W)), dim3(64), 0, st, s,
+                       pend, prec, n, flags);
+}
+
+size_t fold_scan_bytes(int64_t n) {
+  return n <= 0 ? 16 : ((sizeof(int2) * (size_t)n + 15) & ~(size_t)15) + sizeof(int4) * (size_t)n;
 }
 
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
