@@ -126,21 +126,22 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
         for k, v in master.items():
             copy[k].copy_(v)
         eng.bind(copy)
-        e = [ev() for _ in range(6)]
+        # one event between consecutive calls (each event is a marker packet
+        # on the queue: DESIGN.md §7)
+        e = [ev() for _ in range(5)]
         e[0].record(stream)
         ck(lib.mraft_gather_append_args(eng._h, slots_d.data_ptr(), peers_d.data_ptr(), n, args.data_ptr(),
                                         gerr.data_ptr(), DEVICE), "gather")
         e[1].record(stream)
-        e[2].record(stream)
         ck(lib.mraft_handle_append_entries(eng._h, args.data_ptr(), n, None, 0, rep.data_ptr(), herr.data_ptr(),
                                            DEVICE), "handle")
-        e[3].record(stream)
+        e[2].record(stream)
         res[:, 0], res[:, 1], res[:, 2], res[:, 3], res[:, 4] = slots_d, peers_d, args[:, 1], args[:, 3], args[:, 6]
         res[:, 5:8] = rep[:, 0:3]
-        e[4].record(stream)
+        e[3].record(stream)
         ck(lib.mraft_process_append_replies(eng._h, res.data_ptr(), n, seg.data_ptr(), len(seg) - 1,
                                             flags.data_ptr(), ferr.data_ptr(), DEVICE), "fold")
-        e[5].record(stream)
+        e[4].record(stream)
         torch.cuda.synchronize()
         if i == 0:  # the first pass is warm-up; its inputs give the algorithmic bytes
             assert int(gerr.abs().sum()) == 0 and int(herr.abs().sum()) == 0 and int(ferr.abs().sum()) == 0
@@ -159,8 +160,8 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
             del host
             continue
         t_call["gather"].append(e[0].elapsed_time(e[1]))
-        t_call["handle"].append(e[2].elapsed_time(e[3]))
-        t_call["fold"].append(e[4].elapsed_time(e[5]))
+        t_call["handle"].append(e[1].elapsed_time(e[2]))
+        t_call["fold"].append(e[3].elapsed_time(e[4]))
     ms = {k: float(np.mean(v)) for k, v in t_call.items()}
     step_ms = sum(ms.values())
     hb = 4 * hw["words"]
@@ -173,7 +174,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
                      "sets": hw["sets"], "merges": hw["merges"]},
-        "fold_roofline": {"kernel": "mraft_process_append_replies (whole call: claim + k_fold)", "bound": "hbm",
+        "fold_roofline": {"kernel": "mraft_process_append_replies (whole call: claim + k_fold + k_fold_scan)", "bound": "hbm",
                           "algorithmic_bytes": 4 * fw["words"], "a1_log_bytes": 4 * fw["a1_log_words"],
                           "achieved": 4 * fw["words"] / ms["fold"] / 1e6, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                           "frac": 4 * fw["words"] / (ms["fold"] / 1e3) / HBM_PEAK,

@@ -423,7 +423,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
     mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h), h->P,
                         h->claim, h->epoch, (int32_t *)e, h->stream);
     mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, nullptr, nullptr, 0,
-                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
+                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, h->stream);
     return sg.finish();
   }
   // Entries by reference into the engine's log: messages reading the same
@@ -431,8 +431,8 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   // read or write a row another item of this batch writes or reads are
   // deferred to a second launch, the readers' entries staged first (the
   // reference's copy at gather time, raft_append_entry.go:50-54). The plan's
-  // totals reach the host (pinned words the plan kernel writes) while the
-  // main launch runs.
+  // totals reach the host (pinned words the main launch's first workgroup
+  // writes) while the main launch runs.
   if (!h->plan_host) {
     HIP_TRY(hipHostMalloc((void **)&h->plan_host, 4 * sizeof(unsigned long long),
                           hipHostMallocMapped | hipHostMallocCoherent));
@@ -447,15 +447,15 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   TRY(scratch(h, 17, sizeof(int64_t) * (size_t)n, &sets));
   TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
   mraft::launch_claim_ae((const mraft_ae_args *)a, n, src_n, h->L, gp_of(h), h->claim, h->srcmark, h->epoch,
-                         (int32_t *)e, h->stream);
+                         (int32_t *)e, h->plan_dev, h->stream);
   mraft::launch_ae_set_plan((const mraft_ae_args *)a, n, src_n, h->L, ni, h->claim, h->srcmark, h->epoch,
-                            (int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev,
-                            h->plan_host_dev, ++h->plan_seq, h->stream);
-  // main launch: grid sized by the upper bound n, the set count read on the device
+                            (int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev, h->stream);
+  // main launch: grid sized by the upper bound n, the set count read on the
+  // device (the plan's packed counter plan_dev[1]); its first workgroup writes
+  // the totals to the host's pinned words, then the sequence word
   mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, (const int64_t *)soff,
-                          (const int64_t *)sets, n, h->plan_dev + 5, ni, (mraft_ae_reply *)r, (int32_t *)e,
-                          h->stream);
-  // The plan's last workgroup writes the totals, then the sequence word.
+                          (const int64_t *)sets, n, h->plan_dev + 1, ni, (mraft_ae_reply *)r, (int32_t *)e,
+                          h->plan_host_dev, ++h->plan_seq, h->stream);
   volatile unsigned long long *ph = h->plan_host;
   const auto t_poll = std::chrono::steady_clock::now();
   for (unsigned spin = 1; ph[3] != h->plan_seq; ++spin) {
@@ -481,7 +481,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
     }
     mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
                             (int64_t)staged, (const int64_t *)soff, (const int64_t *)defer, (int64_t)n_defer,
-                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, h->stream);
+                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, h->stream);
   }
   return sg.finish();
 }

@@ -59,12 +59,12 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
                              const int64_t *__restrict__ seg_begin, int64_t gp,
                              unsigned long long *__restrict__ claim, uint32_t epoch,
                              int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
-                             int32_t *__restrict__ z1, int2 *__restrict__ z2) {
+                             int32_t *__restrict__ z1, int4 *__restrict__ z2) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < nz) {
     z0[i] = 0;
     z1[i] = 0;
-    if (z2) z2[i] = make_int2(0, -1);  // no a1 range pending for k_fold_scan
+    if (z2) reinterpret_cast<int2 *>(z2)[4 * i] = make_int2(0, -1);  // no a1 range pending for k_fold_scan
   }
   if (i >= n) return;
   int64_t rec = i;
@@ -107,21 +107,23 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
   const int slot = slots[i], peer = peers[i];
   if (slot < 0 || slot >= gp || peer < 0 || peer >= P || peer == slot % P) {
     e = MRAFT_ITEM_BAD_SLOT;
-  } else if (s.role[slot] != kLeader) {                                // raft_append_entry.go:22-25
-    e = MRAFT_ITEM_BAD_STATE;
   } else {
-    const int dummy = s.dummy[slot], last = s.last[slot], head = s.head[slot];
-    const int prev = s.next[(int64_t)slot * P + peer] - 1;             // :26
-    if (prev < dummy) e = MRAFT_ITEM_NEED_SNAPSHOT;                    // :27
+    // every word that depends only on the slot in one round trip (the role
+    // check does not gate the loads: one dependent round trip fewer)
+    const int role = s.role[slot], dummy = s.dummy[slot], last = s.last[slot], head = s.head[slot];
+    const int nxt = s.next[(int64_t)slot * P + peer], term = s.term[slot], commit = s.commit[slot];
+    const int prev = nxt - 1;                                          // :26
+    if (role != kLeader) e = MRAFT_ITEM_BAD_STATE;                     // raft_append_entry.go:22-25
+    else if (prev < dummy) e = MRAFT_ITEM_NEED_SNAPSHOT;               // :27
     else if (prev > last) e = MRAFT_ITEM_PREV_BEYOND_LAST;             // :41-43
     else {
       a.slot = (slot / P) * P + peer;
       a.leader_id = slot % P;
-      a.term = s.term[slot];
+      a.term = term;
       a.prev_log_index = prev;
       a.prev_log_term = s.log[(int64_t)slot * L + ring(prev - dummy + head, L)];  // :49
       a.n_entries = last - prev;                                       // :50
-      a.leader_commit = s.commit[slot];                                // :51
+      a.leader_commit = commit;                                        // :51
       a.entries_offset = (int64_t)slot * L + (prev + 1 - dummy);       // :54 (by reference: logical)
     }
   }
@@ -208,8 +210,12 @@ __device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t i,
 // result: staged entries are the pre-call entries.)
 __global__ void k_claim_ae(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L, int64_t gp,
                            unsigned long long *__restrict__ claim, uint32_t *__restrict__ srcmark, uint32_t epoch,
-                           int32_t *__restrict__ err) {
+                           int32_t *__restrict__ err, unsigned long long *__restrict__ total) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i == 0) {  // arm the plan's accumulators (the previous call's handler has read them)
+    total[0] = 0;
+    total[1] = 0;
+  }
   if (i >= n) return;
   const mraft_ae_args a = args[i];
   if (a.slot < 0 || a.slot >= gp) { err[i] = MRAFT_ITEM_BAD_SLOT; return; }
@@ -256,9 +262,7 @@ __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *_
                                                      const uint32_t *__restrict__ srcmark, uint32_t epoch,
                                                      int32_t *__restrict__ err, int64_t *__restrict__ soff,
                                                      int64_t *__restrict__ sets, int64_t *__restrict__ defer,
-                                                     unsigned long long *__restrict__ total,
-                                                     volatile unsigned long long *__restrict__ host_total,
-                                                     unsigned long long seq) {
+                                                     unsigned long long *__restrict__ total) {
   constexpr int NW = kAePlanT / 64;
   __shared__ int lds[2 * NW + 2];
   __shared__ int kd[kAePlanT], kb[kAePlanT], ke[kAePlanT];
@@ -297,29 +301,11 @@ __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *_
     }
   }
   block_append2<NW>(head >= 0, head, sets, own && kind >= AK_STAGED, i * 8, defer, &total[1], lds);
-  // The last workgroup to finish publishes the totals (total[4..6]: read by
-  // the handler launches; and to the host's pinned words, so the host needs
-  // no copy after this kernel) and re-arms the accumulators for the next call.
-  // No fence: the totals are device-coherent atomics, this workgroup's were
-  // performed before its `done` increment (their results were awaited), and
-  // the handler reads the lists after this kernel ends. (A device-scope fence
-  // here writes back the XCD's L2 per workgroup: +23 us.)
-  if (threadIdx.x == 0) {
-    if (atomicAdd(&total[3], 1ull) == gridDim.x - 1) {
-      const unsigned long long staged = atomicAdd(&total[0], 0ull), both = atomicAdd(&total[1], 0ull);
-      const unsigned long long v[3] = {staged, both & 0xFFFFFFFFull, both >> 32};
-      for (int j = 0; j < 3; ++j) {
-        total[4 + j] = v[j];
-        host_total[j] = v[j];
-      }
-      // the host polls the sequence word: a system-scope release orders the
-      // totals before it (one L2 write-back, in this last workgroup only)
-      __hip_atomic_store(&host_total[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      total[0] = 0;
-      total[1] = 0;
-      total[3] = 0;
-    }
-  }
+  // The totals stay in the device accumulators (total[0]: staged words,
+  // total[1]: main sets | deferred items << 32); the main handler launch reads
+  // its set count there and its first workgroup publishes them to the host.
+  // (Round 2 had the plan's last workgroup publish them: one more contended
+  // atomic per workgroup and a serial tail, ~5 us.)
 }
 
 __global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const int32_t *__restrict__ head, int L,
@@ -375,9 +361,11 @@ struct HsArgs {
   int64_t n_stage;
   const int64_t *soff, *sets;
   int64_t n_sets;
-  const unsigned long long *set_count;
+  const unsigned long long *set_count;  // the plan's packed counter: main sets in the low word
   mraft_ae_reply *rep;
   int32_t *err;
+  volatile unsigned long long *host_total;  // main launch: workgroup 0 publishes the plan's totals here
+  unsigned long long seq;
 };
 
 __device__ __forceinline__ HsArgs reload_hs() {
@@ -391,7 +379,7 @@ __device__ __forceinline__ HsArgs reload_hs() {
   k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
   k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
   k.n_stage = kp->n_stage; k.soff = kp->soff; k.sets = kp->sets; k.n_sets = kp->n_sets;
-  k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err;
+  k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err; k.host_total = kp->host_total; k.seq = kp->seq;
   return k;
 }
 
@@ -625,7 +613,17 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
 template <int NI>
 __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(HsArgs ka) {
   const int64_t *__restrict__ sets = ka.sets;
-  const int64_t nb = sets ? (ka.set_count ? (int64_t)*ka.set_count : ka.n_sets) : ka.n;
+  const unsigned long long sc = ka.set_count ? *ka.set_count : 0ull;
+  const int64_t nb = sets ? (ka.set_count ? (int64_t)(sc & 0xFFFFFFFFull) : ka.n_sets) : ka.n;
+  if (ka.host_total && blockIdx.x == 0 && threadIdx.x == 0) {
+    // the plan's totals to the host's pinned words (staged, sets, deferred),
+    // then the sequence word with a system-scope release (the host polls it)
+    const unsigned long long staged = ka.set_count[-1];
+    ka.host_total[0] = staged;
+    ka.host_total[1] = sc & 0xFFFFFFFFull;
+    ka.host_total[2] = sc >> 32;
+    __hip_atomic_store(&ka.host_total[3], ka.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   for (int64_t v = blockIdx.x;; v += gridDim.x) {
     int64_t gb = v;
     if (MRAFT_AE_XCD) {
@@ -683,13 +681,13 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #define MRAFT_FOLD_XCD 0  // 1: XCD-contiguous segment ranges
 #endif
 #ifndef MRAFT_FOLD_GROUP
-#define MRAFT_FOLD_GROUP 4  // reply segments per wave (16 lanes each) when every one has <= 16 replies; 1: one per wave
+#define MRAFT_FOLD_GROUP 8  // reply segments per wave (64 / this lanes each: 8 or 4, 4 measured 10 % slower); 1: one per wave
 #endif
 #ifndef MRAFT_FOLD_MINW
 // __launch_bounds__ minimum waves per SIMD of the reply fold: one segment per
 // wave, 8 (SGPRs spill to VGPR lanes; 13 % faster than 7); four per wave, 6
 // (80 VGPRs, no scratch; at 8 the per-lane fold state spills 72 B/lane)
-#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP == 4 ? 6 : 8)
+#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP > 1 ? 6 : 8)
 #endif
 
 #ifndef MRAFT_FOLD_EXP
@@ -709,6 +707,21 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #endif
 #ifndef MRAFT_FOLD_SCANU2
 #define MRAFT_FOLD_SCANU2 4   // a1 scan, later iterations: dword loads per lane in flight (64·U2 terms)
+#endif
+#ifndef MRAFT_FOLD_SPLIT
+#define MRAFT_FOLD_SPLIT 1  // the four-segment fold's a1 scans in a second launch (k_fold_scan)
+#endif
+#ifndef MRAFT_FOLD_PROBE
+#define MRAFT_FOLD_PROBE 1  // split fold: k_fold probes each range's top word (0: k_fold_scan's first window does)
+#endif
+#ifndef MRAFT_FSCAN_U1
+#define MRAFT_FSCAN_U1 MRAFT_FSCAN_U  // k_fold_scan: dword loads per lane in the first window
+#endif
+#ifndef MRAFT_FSCAN_W
+#define MRAFT_FSCAN_W 4     // replies per k_fold_scan wave
+#endif
+#ifndef MRAFT_FSCAN_U
+#define MRAFT_FSCAN_U 8     // k_fold_scan: dword loads per lane in flight (64·U terms per round trip; 4: +7 %)
 #endif
 
 // One iteration of the a1 scan: the highest idx in [max(lo, top - 64·U + 1),
@@ -765,7 +778,8 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
                                              const int64_t *__restrict__ seg_begin, int64_t sg,
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
+                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                             int4 *__restrict__ pend) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   int bad = uni(seg_err[sg]);  // the claim verdict: a bad segment's slot may be out of range
@@ -866,7 +880,14 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
     if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
     const unsigned long long rm = __ballot(plo <= phi);  // replies whose evaluation has a range
-    if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
+    if (MRAFT_FOLD_SPLIT) {
+      // probes here, scans in k_fold_scan (as fold_group4)
+      if (MRAFT_FOLD_PROBE && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
+      if (plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
+        pend[2 * (b + base + lane)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
+        pend[2 * (b + base + lane) + 1] = make_int4(dummy, head, 0, 0);
+      }
+    } else if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
       // One range (the usual batch): no separate probe of its top word — the
       // scan's first window starts there (one round trip fewer when the top
       // term is not currentTerm, a 1-KiB window instead of one word when it is).
@@ -910,15 +931,6 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   FOLD_STAMP(5, commit);
 }
 
-#ifndef MRAFT_FOLD_SPLIT
-#define MRAFT_FOLD_SPLIT 1  // the four-segment fold's a1 scans in a second launch (k_fold_scan)
-#endif
-#ifndef MRAFT_FSCAN_W
-#define MRAFT_FSCAN_W 4     // replies per k_fold_scan wave
-#endif
-#ifndef MRAFT_FSCAN_U
-#define MRAFT_FSCAN_U 8     // k_fold_scan: dword loads per lane in flight (64·U terms per round trip; 4: +7 %)
-#endif
 
 // a1's scans of the reply fold (raft_append_entry.go:89-105; the loop reads
 // terms from the top of the range down to the first one equal to currentTerm),
@@ -929,29 +941,26 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
 // replies -> replica state -> probe). A hit sets MRAFT_F_COMMITTED on its reply
 // and raises the replica's commitIndex (atomicMax: several waves may hold
 // ranges of one segment).
-__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int2 *__restrict__ pend,
-                                                     const int4 *__restrict__ prec, int64_t n,
+__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend, int64_t n,
                                                      int32_t *__restrict__ flags) {
   const int lane = lane_id();
   const int64_t i = (int64_t)blockIdx.x * MRAFT_FSCAN_W + lane;
-  int lo = 0, hi = -1;
+  // the reply's record in one round trip: {lo, hi, slot, currentTerm},
+  // {dummy, head} (hi < lo: nothing pending)
+  int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0);
   if (lane < MRAFT_FSCAN_W && i < n) {
-    const int2 v = pend[i];
-    lo = v.x;
-    hi = v.y;
+    ra = pend[2 * i];
+    rb = pend[2 * i + 1];
   }
-  const unsigned long long pm = __ballot(hi >= lo);
-  if (!pm) return;
-  int4 r = make_int4(0, 0, 0, 0);
-  if (hi >= lo) r = prec[i];
+  const int lo = ra.x, hi = ra.y;
   const int L = s.L;
-  for (unsigned long long m = pm; m; m &= m - 1) {
+  for (unsigned long long m = __ballot(hi >= lo); m; m &= m - 1) {
     const int k = first_lane(m);
     const int klo = __builtin_amdgcn_readlane(lo, k), khi = __builtin_amdgcn_readlane(hi, k);
-    const int kslot = __builtin_amdgcn_readlane(r.x, k), kt0 = __builtin_amdgcn_readlane(r.y, k);
-    const int kd = __builtin_amdgcn_readlane(r.z, k), kh = __builtin_amdgcn_readlane(r.w, k);
-    const int x = fold_scan_down_eq<MRAFT_FSCAN_U, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
-                                                                  kt0);  // klo - 1 if none
+    const int kslot = __builtin_amdgcn_readlane(ra.z, k), kt0 = __builtin_amdgcn_readlane(ra.w, k);
+    const int kd = __builtin_amdgcn_readlane(rb.x, k), kh = __builtin_amdgcn_readlane(rb.y, k);
+    const int x = fold_scan_down_eq<MRAFT_FSCAN_U1, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
+                                                                   kt0);  // klo - 1 if none
     if (lane == k && x >= klo) {
       flags[i] |= MRAFT_F_COMMITTED;                                     // :99-100
       atomicMax(&s.commit[kslot], x);
@@ -959,27 +968,32 @@ __global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int2 *__restri
   }
 }
 
-// Group helpers: the wave as four 16-lane groups, group j on lanes 16j..16j+15.
-__device__ __forceinline__ int g16_base() { return (int)(lane_id() & ~15u); }
-__device__ __forceinline__ unsigned g16_mask(bool pred) {  // this lane's group's ballot, bit k = lane 16j+k
-  return (unsigned)((__ballot(pred) >> g16_base()) & 0xFFFFull);
+// Lane groups of GW lanes (the wave as 64 / GW groups).
+template <int GW>
+__device__ __forceinline__ int gw_base() { return (int)(lane_id() & ~(unsigned)(GW - 1)); }
+template <int GW>
+__device__ __forceinline__ unsigned gw_mask(bool pred) {  // this lane's group's ballot, bit k = its lane k
+  return (unsigned)((__ballot(pred) >> gw_base<GW>()) & ((1ull << GW) - 1));
 }
-__device__ __forceinline__ int g16_bcast(int v, int k) { return __shfl(v, g16_base() + k, 64); }
+template <int GW>
+__device__ __forceinline__ int gw_bcast(int v, int k) { return __shfl(v, gw_base<GW>() + k, 64); }
 
-// fold_segment for four segments at once, one per 16-lane group: the same
-// statements on per-group (not wave-uniform) values, so four segments' chains
-// of dependent loads (bounds -> replies -> replica state -> probes -> scans)
-// overlap in one wave. Only segments of at most 16 replies: a wave whose four
-// segments include a longer one folds them one by one on all 64 lanes.
-template <int P>
-__device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result *__restrict__ items,
+// fold_segment for 64 / GW segments at once, one per GW-lane group: the same
+// statements on per-group (not wave-uniform) values, so the segments' chains
+// of dependent loads (bounds -> replies -> replica state -> probes) overlap in
+// one wave. Only segments of at most GW replies: a wave whose segments include
+// a longer one folds them one by one on all 64 lanes.
+template <int P, int GW>
+__device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result *__restrict__ items,
                                             int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t sg0,
                                             int64_t n_seg, const int32_t *__restrict__ seg_err,
                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                            int2 *__restrict__ pend, int4 *__restrict__ prec) {
-  const int lane = lane_id(), gl = lane & 15;
-  const int64_t sg = sg0 + (lane >> 4);
+                                            int4 *__restrict__ pend) {
+  constexpr int NG = 64 / GW;
+  static_assert(GW >= P && GW >= 6, "a group holds the replica's match / next rows and six scalars");
+  const int lane = lane_id(), gl = lane & (GW - 1);
+  const int64_t sg = sg0 + lane / GW;
   const bool live = sg < n_seg;
   int64_t b = 0, e = 0;
   int bad = 0;
@@ -988,24 +1002,27 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
     e = seg_begin ? seg_begin[sg + 1] : sg + 1;
     bad = seg_err[sg];  // the claim verdict: a bad segment's slot may be out of range
   }
-  const int cnt = (int)(e > b ? min(e - b, (int64_t)17) : 0);  // 0: nothing to fold (empty or inverted)
-  if (__ballot(cnt > 16)) {  // a segment longer than a group: all four on the 64-lane path
-    for (int j = 0; j < 4; ++j)
-      if (sg0 + j < n_seg) fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err);
+  const int cnt = (int)(e > b ? min(e - b, (int64_t)(GW + 1)) : 0);  // 0: nothing to fold (empty or inverted)
+  if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
+    for (int j = 0; j < NG; ++j)
+      if (sg0 + j < n_seg)
+        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend);
     return;
   }
   (void)n_items;
   mraft_ae_result it{};
   if (gl < cnt) it = items[b + gl];
-  const int slot = g16_bcast(it.slot, 0);
+  const int slot = gw_bcast<GW>(it.slot, 0);
   const int me = cnt ? slot % P : 0;
   const int64_t mrow = (int64_t)slot * P;
-  // The replica's state, two loads per lane: lanes 0..P-1 matchIndex, 8..8+P-1
-  // nextIndex; lanes 16.. of the second load the scalars.
-  int va = 0, vb = 0;
+  // The replica's state, three independent loads per lane: lanes 0..P-1 of
+  // the group matchIndex and nextIndex, lanes 0..5 the scalars.
+  int va = 0, vn = 0, vb = 0;
   if (cnt && !bad) {
-    if (gl < P) va = s.match[mrow + gl];
-    else if (gl >= 8 && gl < 8 + P) va = s.next[mrow + gl - 8];
+    if (gl < P) {
+      va = s.match[mrow + gl];
+      vn = s.next[mrow + gl];
+    }
     const int32_t *src = gl == 0 ? s.term : gl == 1 ? s.role : gl == 2 ? s.commit : gl == 3 ? s.last
                          : gl == 4 ? s.dummy : gl == 5 ? s.head : nullptr;
     if (src) vb = src[slot];
@@ -1014,9 +1031,9 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
   const unsigned long long cw = (cnt && !bad) ? claim[slot] : 0ull;
   if (cnt && !bad && ((uint32_t)cw != (uint32_t)(0xFFFFFFFFull - (uint64_t)sg) || (uint32_t)(cw >> 32) != epoch))
     bad = MRAFT_ITEM_DUP_SLOT;
-  int term = g16_bcast(vb, 0), role = g16_bcast(vb, 1), commit = g16_bcast(vb, 2);
-  const int last = g16_bcast(vb, 3), dummy = g16_bcast(vb, 4), head = g16_bcast(vb, 5);
-  if (g16_mask(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)))
+  int term = gw_bcast<GW>(vb, 0), role = gw_bcast<GW>(vb, 1), commit = gw_bcast<GW>(vb, 2);
+  const int last = gw_bcast<GW>(vb, 3), dummy = gw_bcast<GW>(vb, 4), head = gw_bcast<GW>(vb, 5);
+  if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)))
     bad = MRAFT_ITEM_BAD_SLOT;
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {
@@ -1026,22 +1043,22 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
   int m[8], nx[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    m[j] = j < P ? g16_bcast(va, j) : 0;
-    nx[j] = j < P ? g16_bcast(va, 8 + j) : 0;
+    m[j] = j < P ? gw_bcast<GW>(va, j) : 0;
+    nx[j] = j < P ? gw_bcast<GW>(vn, j) : 0;
   }
   const int c0 = commit, t0 = term, r0 = role;
   const int32_t *lrow = s.log + (int64_t)slot * s.L;
   bool touched_mn = false;
   int H = commit;
   int nmax = 0;
-  for (int k = 0; k < 16; ++k)
+  for (int k = 0; k < GW; ++k)
     if (__ballot(go && k < cnt)) nmax = k + 1;
   int myfl = 0, plo = 1, phi = 0;  // this lane's reply: flags and a1 range
   for (int k = 0; k < nmax; ++k) {
-    const int pr = g16_bcast(it.peer, k), rt = g16_bcast(it.reply_term, k);
-    const int at = g16_bcast(it.args_term, k), ap = g16_bcast(it.args_prev_log_index, k);
-    const int rs = g16_bcast(it.reply_success, k), rn = g16_bcast(it.args_n_entries, k);
-    const int rci = g16_bcast(it.reply_conflict_index, k);
+    const int pr = gw_bcast<GW>(it.peer, k), rt = gw_bcast<GW>(it.reply_term, k);
+    const int at = gw_bcast<GW>(it.args_term, k), ap = gw_bcast<GW>(it.args_prev_log_index, k);
+    const int rs = gw_bcast<GW>(it.reply_success, k), rn = gw_bcast<GW>(it.args_n_entries, k);
+    const int rci = gw_bcast<GW>(it.reply_conflict_index, k);
     if (go && k < cnt) {
       int fl = 0, nxp = 0;
 #pragma unroll
@@ -1074,22 +1091,23 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
   }
   // a1's ranges of each group: every top word probed at once, the others scanned
   int x = -1;
-  if (go && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
-  if (pend) {
+  if ((MRAFT_FOLD_PROBE || !MRAFT_FOLD_SPLIT) && go && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0)
+    x = phi;  // :98
+  if (MRAFT_FOLD_SPLIT) {
     // the ranges whose top word differs are scanned by k_fold_scan, after this
     // launch: it ORs MRAFT_F_COMMITTED into the reply's flags and raises the
     // replica's commitIndex to the highest index it finds (the ranges of a
     // segment are disjoint and ascending, so "the latest range that found
     // one" is the maximum over all of them, probes included)
-    if (go && plo < phi && x < 0) {
-      pend[b + gl] = make_int2(plo, phi - 1);
-      prec[b + gl] = make_int4(slot, t0, dummy, head);
+    if (go && plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
+      pend[2 * (b + gl)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
+      pend[2 * (b + gl) + 1] = make_int4(dummy, head, 0, 0);
     }
   }
   // the ranges whose top word differs, of all four groups, one after another
   // with the whole wave (a 16-lane scan moves a quarter of the terms per round
   // trip and measured 33 % slower over the call)
-  for (unsigned long long pw = pend ? 0ull : __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
+  for (unsigned long long pw = MRAFT_FOLD_SPLIT ? 0ull : __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
     const int src = first_lane(pw);
     const int lo = __builtin_amdgcn_readlane(plo, src), hi = __builtin_amdgcn_readlane(phi, src) - 1;
     const int sslot = __builtin_amdgcn_readlane(slot, src), sd = __builtin_amdgcn_readlane(dummy, src),
@@ -1099,8 +1117,8 @@ __device__ __forceinline__ void fold_group4(const Dev &s, const mraft_ae_result 
     if (lane == src && r >= lo) x = r;
   }
   if (go && x >= 0) myfl |= MRAFT_F_COMMITTED;                           // :99-100
-  const unsigned fm = g16_mask(go && x >= 0);
-  if (fm) commit = __shfl(x, g16_base() + 31 - __clz((int)fm), 64);      // the latest range that found one
+  const unsigned fm = gw_mask<GW>(go && x >= 0);
+  if (fm) commit = __shfl(x, gw_base<GW>() + 31 - __clz((int)fm), 64);   // the latest range that found one
   if (go && gl < cnt) {
     flags[b + gl] = myfl;
     item_err[b + gl] = 0;
@@ -1124,20 +1142,21 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int2 *__restrict__ pend, int4 *__restrict__ prec) {
+                                             int4 *__restrict__ pend) {
   if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend);
     return;
   }
-  if (MRAFT_FOLD_GROUP == 4) {
-    for (int64_t sg0 = 4 * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += 4 * (int64_t)gridDim.x)
-      fold_group4<P>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend, prec);
+  if (MRAFT_FOLD_GROUP > 1) {
+    constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
+    for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
+      fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err);
+    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend);
 }
 
 // ---------------------------------------------------------------- Start
@@ -1615,21 +1634,20 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
 }
 
 void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp,
-                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, hipStream_t st) {
+                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err,
+                     unsigned long long *total, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, gp, claim, srcmark,
-                     epoch, err);
+                     epoch, err, total);
 }
 
 void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
                         const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
                         int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
-                        unsigned long long *total, unsigned long long *host_total, unsigned long long seq,
-                        hipStream_t st) {
+                        unsigned long long *total, hipStream_t st) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_ae_set_plan, dim3(blocks_for(n, kAeOwn)), dim3(kAePlanT), 0, st, args, n, n_log, L,
-                     ni < 1 ? 1 : ni > kAeHalo ? kAeHalo : ni, claim, srcmark, epoch, err, soff, sets, defer, total,
-                     host_total, seq);
+                     ni < 1 ? 1 : ni > kAeHalo ? kAeHalo : ni, claim, srcmark, epoch, err, soff, sets, defer, total);
 }
 
 void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
@@ -1642,25 +1660,27 @@ template <int NI>
 static void launch_set(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                        const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
                        int64_t n_sets, const unsigned long long *set_count, mraft_ae_reply *rep, int32_t *err,
-                       hipStream_t st) {
+                       unsigned long long *host_total, unsigned long long seq, hipStream_t st) {
   // with the count on the device, n_sets is an upper bound: a workgroup per
   // MRAFT_AE_SPB sets of the bound (grid a multiple of 8, see k_handle_set)
   int64_t nb = sets ? n_sets : n;
   if (set_count) nb = ((nb + MRAFT_AE_SPB - 1) / MRAFT_AE_SPB + 7) / 8 * 8;
-  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err};
+  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, seq};
   hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, ka);
 }
 
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                       const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
                       int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
-                      int32_t *err, hipStream_t st) {
+                      int32_t *err, unsigned long long *host_total, unsigned long long seq, hipStream_t st) {
   if (n <= 0 || (sets && n_sets <= 0)) return;
 #define MRAFT_SET_CASE(k) \
-  case k: launch_set<k>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, st); break;
+  case k: launch_set<k>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, \
+                        seq, st); break;
   switch (sets ? ni : 1) {
     MRAFT_SET_CASE(1) MRAFT_SET_CASE(2) MRAFT_SET_CASE(3) MRAFT_SET_CASE(4) MRAFT_SET_CASE(5) MRAFT_SET_CASE(6)
-    default: launch_set<7>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, st);
+    default: launch_set<7>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total,
+                           seq, st);
   }
 #undef MRAFT_SET_CASE
 }
@@ -1681,20 +1701,20 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   // fold_scan_bytes(n) of scratch)
   const int64_t nt = max(n_seg, n);
   if (nt <= 0) return;
-  const bool split = MRAFT_FOLD_SPLIT && MRAFT_FOLD_GROUP == 4 && scan_buf && n > 0;
-  int2 *pend = split ? (int2 *)scan_buf : nullptr;
-  int4 *prec = split ? (int4 *)((char *)scan_buf + ((sizeof(int2) * (size_t)n + 15) & ~(size_t)15)) : nullptr;
+  const bool split = MRAFT_FOLD_SPLIT;  // the ABI always passes scan_buf
+  if (split && !scan_buf) return;
+  int4 *pend = split ? (int4 *)scan_buf : nullptr;
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
                      epoch, seg_err, n, flags, item_err, pend);
   if (n_seg <= 0) return;
-  const int64_t waves = MRAFT_FOLD_GROUP == 4 ? (n_seg + 3) / 4 : n_seg;
+  const int64_t waves = (n_seg + MRAFT_FOLD_GROUP - 1) / MRAFT_FOLD_GROUP;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
   switch (s.P) {
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err, pend, prec);                                          \
+                       flags, item_err, pend);                                                \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
@@ -1703,11 +1723,11 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   }
   if (split)
     hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W)), dim3(64), 0, st, s,
-                       pend, prec, n, flags);
+                       pend, n, flags);
 }
 
 size_t fold_scan_bytes(int64_t n) {
-  return n <= 0 ? 16 : ((sizeof(int2) * (size_t)n + 15) & ~(size_t)15) + sizeof(int4) * (size_t)n;
+  return n <= 0 ? 32 : 2 * sizeof(int4) * (size_t)n;
 }
 
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
