@@ -342,6 +342,22 @@ enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE
 #define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
 #endif
 
+#ifndef MRAFT_AE_PDIRTY_ATOMIC
+#define MRAFT_AE_PDIRTY_ATOMIC 1  // the handler's persist marks as non-returning atomic ORs (0: load, OR, store)
+#endif
+// The handler's mark at the end of a set's wave as a non-returning atomic OR:
+// the wave does not wait for a load of the bits (a dependent round trip at
+// its very end). Same-box A/B: handle call -8 us on average over three passes
+// (profiles/r3_v8/message_path_ab.txt, r3w); the same change in the fused
+// tick measured +0.7 % there and is not used.
+__device__ __forceinline__ void mark_persist_ae(const Dev &s, int64_t slot, int bits) {
+  if (MRAFT_AE_PDIRTY_ATOMIC) {
+    if (s.pdirty && bits) (void)__hip_atomic_fetch_or(&s.pdirty[slot], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    mark_persist(s, slot, bits);
+  }
+}
+
 #ifndef MRAFT_AE_RELOAD
 #define MRAFT_AE_RELOAD 1  // after the pass, kernel arguments re-read from the kernarg segment (not held across it)
 #endif
@@ -595,13 +611,13 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     err2[i] = MRAFT_ITEM_BAD_SLOT;
   } else if (cls == AE_STALE) {
     rep2[i] = r;
-    mark_persist(s2, f, MRAFT_PERSIST_STATE);                          // deferred :111
+    mark_persist_ae(s2, f, MRAFT_PERSIST_STATE);                       // deferred :111
   } else if (cls >= AE_BELOW) {
     if (a.term > fterm) { s2.term[f] = a.term; s2.voted[f] = -1; }    // :116-118
     s2.role[f] = kFollower;                                            // :120
     if (newlast >= 0) s2.last[f] = newlast;
     if (fcommit_new >= 0) s2.commit[f] = fcommit_new;
-    mark_persist(s2, f, MRAFT_PERSIST_STATE);                          // deferred :111
+    mark_persist_ae(s2, f, MRAFT_PERSIST_STATE);                       // deferred :111
     rep2[i] = r;
   }
 }

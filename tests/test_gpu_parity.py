@@ -144,6 +144,25 @@ def test_fold_long_segments_gpu(P, seed):
         assert_states_equal(e.store_state(), o.state(), G, P, L, "fold long")
 
 
+@pytest.mark.parametrize("P,seed", [(5, 34), (3, 35), (8, 36)])
+def test_fold_short_segments_gpu(P, seed):
+    """Segments of at most eight replies (the eight-segments-per-wave fold),
+    several a1 evaluations each, so one segment's pending ranges land in
+    different k_fold_scan waves and the replica's commitIndex is the maximum
+    of their hits and the probes' (atomicMax); Figure-8 logs included."""
+    from oracle_lib import random_reply_segments
+    G, L = 1024, 512
+    st, lp, _ = synth_tick_state(G, P, L, seed=seed)
+    items, seg = random_reply_segments(st, G, P, lp, seed=seed, max_len=8)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        f, err = e.process_append_replies(items, seg)
+        of, oerr = o.process_append_replies(items, seg)
+        assert np.array_equal(err, oerr) and np.array_equal(f, of)
+        assert (f & 2).any()  # MRAFT_F_COMMITTED: some evaluations commit
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "fold short")
+
+
 def test_item_path_gpu():
     G, P, L = 256, 5, 256
     st, lp, _ = synth_tick_state(G, P, L, seed=61)
