@@ -59,12 +59,12 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
                              const int64_t *__restrict__ seg_begin, int64_t gp,
                              unsigned long long *__restrict__ claim, uint32_t epoch,
                              int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
-                             int32_t *__restrict__ z1, int4 *__restrict__ z2) {
+                             int32_t *__restrict__ z1, int32_t *__restrict__ z2) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < nz) {
     z0[i] = 0;
     z1[i] = 0;
-    if (z2) reinterpret_cast<int2 *>(z2)[4 * i] = make_int2(0, -1);  // no a1 range pending for k_fold_scan
+    if (z2) z2[i] = 0;  // no a1 range pending for k_fold_scan
   }
   if (i >= n) return;
   int64_t rec = i;
@@ -795,7 +795,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend) {
+                                             int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   int bad = uni(seg_err[sg]);  // the claim verdict: a bad segment's slot may be out of range
@@ -902,6 +902,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       if (plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
         pend[2 * (b + base + lane)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
         pend[2 * (b + base + lane) + 1] = make_int4(dummy, head, 0, 0);
+        pmark[b + base + lane] = 1;
       }
     } else if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
       // One range (the usual batch): no separate probe of its top word — the
@@ -957,18 +958,22 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
 // replies -> replica state -> probe). A hit sets MRAFT_F_COMMITTED on its reply
 // and raises the replica's commitIndex (atomicMax: several waves may hold
 // ranges of one segment).
-__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend, int64_t n,
+__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend,
+                                                     const int32_t *__restrict__ pmark, int64_t n,
                                                      int32_t *__restrict__ flags) {
   const int lane = lane_id();
   const int64_t i = (int64_t)blockIdx.x * MRAFT_FSCAN_W + lane;
-  // the reply's record in one round trip: {lo, hi, slot, currentTerm},
-  // {dummy, head} (hi < lo: nothing pending)
+  // the reply's marker and record in one round trip: {lo, hi, slot,
+  // currentTerm}, {dummy, head} (marker 0: nothing pending, the record is
+  // stale)
   int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0);
+  int mk = 0;
   if (lane < MRAFT_FSCAN_W && i < n) {
+    mk = pmark[i];
     ra = pend[2 * i];
     rb = pend[2 * i + 1];
   }
-  const int lo = ra.x, hi = ra.y;
+  const int lo = ra.x, hi = mk ? ra.y : ra.x - 1;
   const int L = s.L;
   for (unsigned long long m = __ballot(hi >= lo); m; m &= m - 1) {
     const int k = first_lane(m);
@@ -1005,7 +1010,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
                                             int64_t n_seg, const int32_t *__restrict__ seg_err,
                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                            int4 *__restrict__ pend) {
+                                            int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
   constexpr int NG = 64 / GW;
   static_assert(GW >= P && GW >= 6, "a group holds the replica's match / next rows and six scalars");
   const int lane = lane_id(), gl = lane & (GW - 1);
@@ -1022,7 +1027,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
     for (int j = 0; j < NG; ++j)
       if (sg0 + j < n_seg)
-        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend);
+        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend, pmark);
     return;
   }
   (void)n_items;
@@ -1118,6 +1123,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     if (go && plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
       pend[2 * (b + gl)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
       pend[2 * (b + gl) + 1] = make_int4(dummy, head, 0, 0);
+      pmark[b + gl] = 1;
     }
   }
   // the ranges whose top word differs, of all four groups, one after another
@@ -1158,21 +1164,22 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend) {
+                                             int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
   if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pmark);
     return;
   }
-  if (MRAFT_FOLD_GROUP > 1) {
+  if constexpr (MRAFT_FOLD_GROUP > 1) {
     constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
     for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
-      fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend);
+      fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
+                         pmark);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend);
+    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pmark);
 }
 
 // ---------------------------------------------------------------- Start
@@ -1719,10 +1726,11 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   if (nt <= 0) return;
   const bool split = MRAFT_FOLD_SPLIT;  // the ABI always passes scan_buf
   if (split && !scan_buf) return;
-  int4 *pend = split ? (int4 *)scan_buf : nullptr;
+  int4 *pend = split ? (int4 *)scan_buf : nullptr;               // 2 int4 per reply
+  int32_t *pmark = split ? (int32_t *)(pend + 2 * n) : nullptr;  // 1 int per reply
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
-                     epoch, seg_err, n, flags, item_err, pend);
+                     epoch, seg_err, n, flags, item_err, pmark);
   if (n_seg <= 0) return;
   const int64_t waves = (n_seg + MRAFT_FOLD_GROUP - 1) / MRAFT_FOLD_GROUP;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
@@ -1730,7 +1738,7 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err, pend);                                                \
+                       flags, item_err, pend, pmark);                                         \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
@@ -1739,11 +1747,11 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   }
   if (split)
     hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W)), dim3(64), 0, st, s,
-                       pend, n, flags);
+                       pend, pmark, n, flags);
 }
 
 size_t fold_scan_bytes(int64_t n) {
-  return n <= 0 ? 32 : 2 * sizeof(int4) * (size_t)n;
+  return n <= 0 ? 48 : (2 * sizeof(int4) + sizeof(int32_t)) * (size_t)n;
 }
 
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,

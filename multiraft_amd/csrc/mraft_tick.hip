@@ -213,12 +213,6 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #ifndef MRAFT_PASS_PIPE
 #define MRAFT_PASS_PIPE 1   // compare chunks software-pipelined (next chunk's loads before this chunk's stores)
 #endif
-#ifndef MRAFT_TICK_TAIL_N
-#define MRAFT_TICK_TAIL_N 0  // the launch's last N workgroups (dispatched last) stream their copy-only loop
-#endif                       // MRAFT_TICK_TAIL_D chunks ahead (0: off)
-#ifndef MRAFT_TICK_TAIL_D
-#define MRAFT_TICK_TAIL_D 4
-#endif
 #ifndef MRAFT_TICK_WPB
 #define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
 #endif
@@ -490,10 +484,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         for (; c <= phi && fo.cmp; c += 256 * V)
           pass_chunk<V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
       }
-      if (MRAFT_TICK_TAIL_N > 0 && (int)blockIdx.x >= (int)gridDim.x - MRAFT_TICK_TAIL_N)
-        copy_loop_deep<MRAFT_TICK_TAIL_D, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
-      else
-        copy_loop<true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
+      copy_loop<true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     } else {
       int c = plo;
       for (; c <= phi && fo.cmp; c += 256 * V)
