@@ -377,7 +377,8 @@ struct HsArgs {
   int64_t n_stage;
   const int64_t *soff, *sets;
   int64_t n_sets;
-  const unsigned long long *set_count;  // the plan's packed counter: main sets in the low word
+  const unsigned long long *set_count;  // the plan's packed counter (main sets in the low word, deferred items
+                                        // in the high word); set_count[-1] is its staged-word count
   mraft_ae_reply *rep;
   int32_t *err;
   volatile unsigned long long *host_total;  // main launch: workgroup 0 publishes the plan's totals here
