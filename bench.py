@@ -180,8 +180,8 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
                           "frac": 4 * fw["words"] / (ms["fold"] / 1e3) / HBM_PEAK,
                           "segments": fw["segments"], "a1_evaluations": fw["evaluations"],
                           "note": "tools/msg_words.py fold_words: a1's log words (the Figure-8 gate's scans "
-                                  "down to the commit index) are most of the bytes; each scan is a chain of "
-                                  "dependent round trips"}}
+                                  "down to the commit index) are most of the bytes; k_fold folds the replies and "
+                                  "probes each range's top word, k_fold_scan scans the ranges the probes left open"}}
     eng.close()
 
     # -- config #5 election storm
