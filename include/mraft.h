@@ -315,7 +315,8 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * followers, as the gather lays them out) are served together, reading the
  * entries once; items that read a row this call also writes, and the items
  * writing such rows, run after the others, the former from a staged copy.
- * The call then blocks the host until the batch plan is known (the GPU keeps
+ * The call then blocks the host until the batch plan is known: the main
+ * launch's first workgroup publishes it when that launch starts (the GPU keeps
  * working meanwhile). */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
