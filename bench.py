@@ -486,6 +486,24 @@ def describe_workload(strong, world, G_total, P, L, config, dist_on, rccl, backe
     return w
 
 
+def full_mask_stream(device: int) -> int:
+    """A HIP stream on a dedicated hardware queue: hipExtStreamCreateWithCUMask
+    with every CU of the device enabled (host plumbing for --shards)."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    nw = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * nw)(*[(0xFFFFFFFF if (w + 1) * 32 <= ncu else (1 << (ncu - 32 * w)) - 1)
+                                    for w in range(nw)])
+    s = ctypes.c_void_p()
+    rc = hip.hipSetDevice(device)
+    rc = rc or hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), nw, mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    return s.value
+
+
 def spawn_ranks(n: int) -> int:
     """`--gpus N` without a launcher: start N rank processes (one per GPU) and
     wait for them. The parent never touches the GPU (it only forwards the
@@ -565,6 +583,12 @@ def main():
     ap.add_argument("--extra-marks", type=int, default=0,
                     help="experiment: record this many extra (untimed) events on the tick stream "
                          "after every tick")
+    ap.add_argument("--shards", type=int, default=2,
+                    help="independent group shards per GPU, one engine and one stream each, ticked "
+                         "in turn every step: shard s's tick i+1 follows its tick i on its own stream "
+                         "and overlaps the other shards' ticks, so one launch's last generation of "
+                         "groups shares the device with the next launch's first (DESIGN.md §6; "
+                         "1 = one launch per step)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch plumbing only (no GPU call): start the ranks, build every rank's "
                          "shard of the seeded workload, run the control plane and print the line "
@@ -682,6 +706,39 @@ def main():
     torch.cuda.set_stream(stream)
     lp_d = torch.from_numpy(lp).to(dev)
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
+    # Group shards (--shards): shard s = groups [s*gs, (s+1)*gs) of every state
+    # copy (contiguous slices of each SoA array: no copies), its own engine and
+    # stream (shard 0's is the main stream). One shard: the main engine itself.
+    S = args.shards if (args.shards > 1 and not restore and G % args.shards == 0) else 1
+    gs = G // S
+    per_group = {k: v.numel() // G for k, v in master.items()}
+    shards = []
+    for si in range(S):
+        if S == 1:
+            e_s, st_s = eng, stream
+        else:
+            # Each shard's stream on a hardware queue of its own: a stream
+            # created with a CU mask gets a dedicated queue (pooled streams may
+            # share one, and two shards' launches on one queue serialise).
+            # Without the fan-in the mask holds every CU; with it, the same CUs
+            # as the main tick stream (mraft_fanin_reserve_cus).
+            e_s = Engine(gs, P, L, device=local_dev, alloc=False)
+            if rccl and args.fanin_cus:
+                e_s.fanin_reserve_cus(args.fanin_cus)
+                st_s = torch.cuda.ExternalStream(e_s.stream(), device=dev)
+            else:
+                st_s = torch.cuda.ExternalStream(full_mask_stream(local_dev), device=dev)
+                e_s.set_stream(st_s.cuda_stream)
+        shards.append((e_s, st_s, slice(si * gs, (si + 1) * gs)))
+    if S > 1:
+        stream = shards[0][1]  # the timing and the fan-in's first wait follow shard 0's stream
+        torch.cuda.set_stream(stream)
+
+    def shard_views(c):
+        return [{k: v[sl.start * per_group[k]:sl.stop * per_group[k]] for k, v in c.items()}
+                for (_, _, sl) in shards]
+
+    views = [shard_views(c) for c in clones] if S > 1 else None
     on_host = dist_on and not rccl
     # Per-step GetState export blocks (commitIndex | term<<1|leader, one buffer
     # so the router's fan-in is ONE collective per tick) and their gathers:
@@ -711,18 +768,22 @@ def main():
     # step a few microseconds of idle device (the round-2 fan-in runs recorded
     # four per tick: ~20 us per step beyond the kernel).
     chain = not restore and args.fanin_marks == "chain"
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
+    marks_s = [[torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
+               for _ in range(S)]
+    marks = marks_s[0]
+    t_begin = torch.cuda.Event(enable_timing=True)
+    t_end = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
     extra = [torch.cuda.Event() for _ in range(args.extra_marks)]
 
     # The all-gather, timed on its own stream (reported beside the step).
     ag_marks = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)] if fan is not None else []
     ag_ms = []
 
-    def mark_start(i):
-        return marks[i] if chain else marks[2 * i]
+    def mark_start(i, si=0):
+        return marks_s[si][i] if chain else marks_s[si][2 * i]
 
-    def mark_end(i):
-        return marks[i + 1] if chain else marks[2 * i + 1]
+    def mark_end(i, si=0):
+        return marks_s[si][i + 1] if chain else marks_s[si][2 * i + 1]
 
     def step(i, timed):
         if restore:  # not enough HBM for a copy per step: restore inside the step
@@ -731,14 +792,25 @@ def main():
                 c[k].copy_(master[k], non_blocking=True)
         else:
             c = clones[i] if timed else clones[K]
-        eng.bind(c)
-        if timed and (i == 0 or not chain):
-            mark_start(i).record(stream)
-        # the tick with the GetState export fused in (one launch per step)
         j = i if timed else K + i  # timed steps use blocks 0..K-1, warmup K..K+W-1
-        eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
-        if timed:
-            mark_end(i).record(stream)
+        if S == 1:
+            eng.bind(c)
+            if timed and (i == 0 or not chain):
+                mark_start(i).record(stream)
+            # the tick with the GetState export fused in (one launch per step)
+            eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
+            if timed:
+                mark_end(i).record(stream)
+        else:
+            vs = views[i] if timed else views[K]
+            for si, (e_s, st_s, sl) in enumerate(shards):
+                e_s.bind(vs[si])
+                if timed and (i == 0 or not chain):
+                    mark_start(i, si).record(st_s)
+                e_s.replicate_tick_export(lp_d[sl], gf_d[sl], status[j, :G][sl], status[j, G:][sl],
+                                          where=DEVICE)
+                if timed:
+                    mark_end(i, si).record(st_s)
         for x in extra:  # experiment: marker packets between ticks
             x.record(stream)
         if dist_on:  # the shard router's fan-in
@@ -754,12 +826,15 @@ def main():
                 ordered = False
                 if overlap and timed and chain:
                     # the fan-in stream waits on the tick's own end marker
-                    comm_stream.wait_event(mark_end(i))
+                    # (every shard's)
+                    for si in range(S):
+                        comm_stream.wait_event(mark_end(i, si))
                     ordered = True
                 elif timed and overlap:
                     # the gather starts once the tick is done: its start mark
                     # waits for the tick on the fan-in stream as well
-                    comm_stream.wait_stream(stream)
+                    for (_, st_s, _) in shards:
+                        comm_stream.wait_stream(st_s)
                 if timed:
                     ag_marks[2 * i].record(comm_stream)
                 fan.gather(status[j], gathered[j], overlap=overlap, ordered=ordered)
@@ -773,13 +848,43 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    t_begin.record(stream)
+    for (_, st_s, _) in shards[1:]:
+        st_s.wait_event(t_begin)
     for i in range(K):
         step(i, True)
+    for si, (_, st_s, _) in enumerate(shards):
+        t_end[si].record(st_s)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist_on:
         dist.barrier()
-    ker_ms = [mark_start(i).elapsed_time(mark_end(i)) for i in range(K)]
+    # device time of the timed region: from the first launch's start marker to
+    # the last shard's end
+    span_ms = max(t_begin.elapsed_time(e) for e in t_end)
+    launch_ms = [[mark_start(i, si).elapsed_time(mark_end(i, si)) for i in range(K)] for si in range(S)]
+    if S > 1:
+        # the shards' last step (a pristine copy) equals one launch over every
+        # group on the same input: flags and export words
+        ck = clones[K]
+        for k in ck:
+            ck[k].copy_(master[k])
+        torch.cuda.synchronize()  # the copies ran on torch's stream, the tick runs on the engine's
+        eng.bind(ck)
+        gf1 = torch.zeros_like(gf_d)
+        st1 = torch.zeros_like(status[0])
+        eng.replicate_tick_export(lp_d, gf1, st1[:G], st1[G:], where=DEVICE)
+        torch.cuda.synchronize()
+        assert torch.equal(gf1, gf_d) and torch.equal(st1, status[K - 1]), "sharded tick differs from one launch"
+    # per step: one launch (S = 1), or the shards' launches overlapping: the
+    # step's share of the device span, apportioned by its launches' durations
+    if S == 1:
+        ker_ms = launch_ms[0]
+    else:
+        w = np.sum(np.array(launch_ms), axis=0)
+        ker_ms = list(w / w.sum() * span_ms)
+        log(rank, f"{S} shards: device span {span_ms / K:.4f} ms per step; shard launch ms mean "
+                  + " ".join(f"{float(np.mean(x)):.4f}" for x in launch_ms))
     log(rank, "tick kernel ms per step: " + " ".join(f"{x:.3f}" for x in ker_ms))
     flags = gf_d.cpu().numpy()
     if fan is not None:
@@ -839,7 +944,12 @@ def main():
                    "fanin_reserved_cus": args.fanin_cus if fan is not None else 0,
                    "tick_stream_marks_per_step": (1 if chain else 2) + args.extra_marks
                    + (1 if fan is not None and not chain else 0),
-                   "step_minus_kernel_ms": dt / K * 1e3 - float(np.mean(ker_ms))},
+                   "step_minus_kernel_ms": dt / K * 1e3 - float(np.mean(ker_ms)),
+                   "shards_per_gpu": S,
+                   "shard_pipelining": (None if S == 1 else
+                                        f"{S} engines on {S} streams over contiguous group ranges of "
+                                        f"{gs}; each shard's tick i+1 follows its tick i on its own "
+                                        "stream, the shards' launches overlap (DESIGN.md §6)")},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
@@ -852,6 +962,15 @@ def main():
                      "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms)),
                      "kernel_ms_median": float(np.median(ker_ms)),
                      "kernel_ms_steps": [round(float(x), 4) for x in ker_ms],
+                     "device_ms_per_step": span_ms / K,
+                     "launches_per_step": S,
+                     "launch_ms_mean": [round(float(np.mean(x)), 4) for x in launch_ms],
+                     "timing": ("one launch per step: HIP events around each launch" if S == 1 else
+                                f"{S} overlapping launches per step (one per shard and stream): "
+                                "kernel_ms_mean = device time of the timed region / steps (events "
+                                "from the first launch's start to the last shard's end); "
+                                "kernel_ms_steps apportions it by each step's launch durations; "
+                                "launch_ms_mean = each shard's launch duration, overlap included"),
                      "note": ("each step ticks its own fresh state copy; copies whose log image sits in "
                               "physical memory that takes streaming writes ~10 % slower run ~13 % slower "
                               "(DESIGN.md §5 placement lottery): kernel_ms_steps shows both populations"),
@@ -890,6 +1009,7 @@ def main():
         # config #4's N = 1 anchor: free config #3's copies, then all 262,144 groups on this GPU
         eng.close()
         del clones, master
+        views = ck = None  # the shards' slices of the copies
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         c4 = config4_one_gpu(dev, stream)
@@ -908,6 +1028,10 @@ def main():
     if fan is not None:
         eng.fanin_synchronize()
         fan.close()
+    if S > 1:
+        torch.cuda.synchronize()
+        for (e_s, _, _) in shards:
+            e_s.close()
     eng.close()
     if dist_on:
         dist.destroy_process_group()
