@@ -504,6 +504,15 @@ def full_mask_stream(device: int) -> int:
     return s.value
 
 
+def destroy_stream(handle: int) -> None:
+    """Destroys a full_mask_stream (before the process exits: a stream left
+    to the runtime's teardown crashed it under rocprofv3)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamSynchronize(ctypes.c_void_p(handle))
+    hip.hipStreamDestroy(ctypes.c_void_p(handle))
+
+
 def spawn_ranks(n: int) -> int:
     """`--gpus N` without a launcher: start N rank processes (one per GPU) and
     wait for them. The parent never touches the GPU (it only forwards the
@@ -713,6 +722,7 @@ def main():
     gs = G // S
     per_group = {k: v.numel() // G for k, v in master.items()}
     shards = []
+    own_streams = []  # full_mask_stream handles, destroyed at the end
     for si in range(S):
         if S == 1:
             e_s, st_s = eng, stream
@@ -727,7 +737,8 @@ def main():
                 e_s.fanin_reserve_cus(args.fanin_cus)
                 st_s = torch.cuda.ExternalStream(e_s.stream(), device=dev)
             else:
-                st_s = torch.cuda.ExternalStream(full_mask_stream(local_dev), device=dev)
+                own_streams.append(full_mask_stream(local_dev))
+                st_s = torch.cuda.ExternalStream(own_streams[-1], device=dev)
                 e_s.set_stream(st_s.cuda_stream)
         shards.append((e_s, st_s, slice(si * gs, (si + 1) * gs)))
     if S > 1:
@@ -1032,6 +1043,9 @@ def main():
         torch.cuda.synchronize()
         for (e_s, _, _) in shards:
             e_s.close()
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+        for h in own_streams:
+            destroy_stream(h)
     eng.close()
     if dist_on:
         dist.destroy_process_group()

@@ -473,3 +473,55 @@ def test_applier_compact_snapshot_outputs_gpu():
         assert np.array_equal(si, osi[want]) and np.array_equal(stm, ost[want])
         assert not e.store_state()["has_snapshot"].any()
         assert_states_equal(e.store_state(), o.state(), G, P, L, "applier compact, snapshots")
+
+
+def test_tick_shards_on_dedicated_queues_gpu():
+    """bench.py --shards: engines over contiguous group ranges of one state
+    image (SoA slices, no copies), each on a stream of its own hardware queue,
+    their launches overlapping over several fresh copies, give the same flags,
+    export words and state as one launch over every group (and the oracle)."""
+    import torch
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import destroy_stream, full_mask_stream
+    from multiraft_amd import DEVICE
+
+    G, P, L, S, C = 4096, 5, 256, 2, 3
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
+    dev = torch.device("cuda", 0)
+    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    per = {k: v.numel() // G for k, v in master.items()}
+    lp_d = torch.from_numpy(lp).to(dev)
+    gs = G // S
+    copies = [{k: v.clone() for k, v in master.items()} for _ in range(C)]
+    flags = [torch.zeros(G, dtype=torch.int32, device=dev) for _ in range(C)]
+    exp = [torch.zeros(2 * G, dtype=torch.int32, device=dev) for _ in range(C)]
+    engines, streams = [], []
+    for s in range(S):
+        e = Engine(gs, P, L, alloc=False)
+        streams.append(full_mask_stream(0))
+        e.set_stream(streams[-1])
+        engines.append(e)
+    for c in range(C):
+        for s, e in enumerate(engines):
+            sl = slice(s * gs, (s + 1) * gs)
+            e.bind({k: v[s * gs * per[k]:(s + 1) * gs * per[k]] for k, v in copies[c].items()})
+            e.replicate_tick_export(lp_d[sl], flags[c][sl], exp[c][:G][sl], exp[c][G:][sl], where=DEVICE)
+    torch.cuda.synchronize()
+    for e in engines:
+        e.close()
+    for h in streams:
+        destroy_stream(h)
+    with _engine(G, P, L, st) as one:
+        f1, c1, t1 = one.replicate_tick_export(lp)
+        want = one.store_state()
+    o = Oracle(G, P, L, st)
+    of = o.replicate_tick(lp)
+    assert np.array_equal(f1, of)
+    for c in range(C):
+        assert np.array_equal(flags[c].cpu().numpy(), f1)
+        assert np.array_equal(exp[c][:G].cpu().numpy(), c1) and np.array_equal(exp[c][G:].cpu().numpy(), t1)
+        got = {k: v.cpu().numpy() for k, v in copies[c].items()}
+        for k in want:
+            if k in got:
+                assert np.array_equal(got[k], want[k]), k
