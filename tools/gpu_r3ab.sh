@@ -4,7 +4,7 @@
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r3_v13
+OUT=gpurun_out/${TAG:-r3_v13}
 mkdir -p "$OUT"
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$OUT/gpu_tests.txt" 2>&1 || { echo "FAILED tests"; grep -E "FAILED|Error|assert" "$OUT/gpu_tests.txt" | head -20; tail -20 "$OUT/gpu_tests.txt"; exit 1; }
 tail -2 "$OUT/gpu_tests.txt"
