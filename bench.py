@@ -242,12 +242,21 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
 CONFIG4_ANCHOR = os.path.join(ROOT, "profiles", "config4_n1_anchor.json")
 
 
-def config4_one_gpu(dev, stream, steps=10):
+def pmc_json_path(G: int, S: int) -> str:
+    """The committed PMC traffic summary of the tick at G groups per GPU in S
+    shards (tools/pmc_summary.py): pmc_traffic[_g<G>][_s<S>].json."""
+    name = "pmc_traffic" + ("" if G == 65536 else f"_g{G}") + ("" if S == 1 else f"_s{S}") + ".json"
+    return os.path.join(ROOT, "profiles", name)
+
+
+def config4_one_gpu(dev, stream, steps=10, shards=(1, 2)):
     """BASELINE config #4 on ONE GPU: all 262,144 groups (config #3's
-    generator and mix, the workload the N > 1 lines split N ways) in one tick
-    launch per step, each step on its own fresh HBM-resident copy (as many as
-    fit; ~21.5 GB each). The N = 1 point of the strong-scaling series, timed
-    exactly like the headline (one marker per tick on the engine stream)."""
+    generator and mix, the workload the N > 1 lines split N ways) ticked once
+    per step, each step on its own fresh HBM-resident copy (as many as fit;
+    ~21.5 GB each), timed like the headline (one marker per tick on each tick
+    queue), once per shard count in `shards` (the copies restored in between):
+    the N = 1 points of the strong-scaling series, one per S the N > 1 lines
+    may use."""
     import torch
 
     from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
@@ -269,63 +278,95 @@ def config4_one_gpu(dev, stream, steps=10):
     eng.bind(master)
     rd, wr, active = eng.replicate_tick_count(lp_d, where=DEVICE)
     algo = 4 * (rd + wr)
-    eng.bind(clones[-1])  # warm-up on a copy that is re-timed last
-    eng.replicate_tick(lp_d, gf, where=DEVICE)
-    torch.cuda.synchronize()
-    if pool > 1:  # the warm-up copy is spent: refresh it for the timed steps
-        for k in master:
-            clones[-1][k].copy_(master[k])
-    torch.cuda.synchronize()
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(pool + 1)]
-    t0 = time.perf_counter()
-    marks[0].record(stream)
-    for i in range(pool):
-        eng.bind(clones[i])
+    out = {"workload": "config #4 on one GPU: 262,144 groups x 5 peers x 4,096-entry logs (config #3's "
+                       "generator and mix; the N > 1 lines split it N ways), one tick per step on a fresh "
+                       "copy, with 1 and with 2 tick shards (mraft_set_tick_shards)",
+           "groups": G4, "steps": pool, "state_copy_gib": clone_bytes / 2**30, "generate_s": gen_s,
+           "by_shards": {}}
+    pj_traffic = {}
+    for S in shards:
+        pj = pmc_json_path(G4, S)
+        if os.path.exists(pj):
+            pm = json.load(open(pj))
+            if pm.get("kernel_src_sha") == kernel_src_sha() and pm.get("shards", 1) == S:
+                pj_traffic[S] = (pm.get("hbm_bytes_per_launch"), f"profiles/{os.path.basename(pj)} ({pm.get('tag')})")
+    for n, S in enumerate(shards):
+        eng.set_tick_shards(S)
+        qs = [stream] if S == 1 else [torch.cuda.ExternalStream(eng.shard_stream(s), device=dev) for s in range(S)]
+        eng.bind(clones[-1])  # warm-up on a copy that is re-timed last
         eng.replicate_tick(lp_d, gf, where=DEVICE)
-        marks[i + 1].record(stream)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    ker = [marks[i].elapsed_time(marks[i + 1]) for i in range(pool)]
+        eng.synchronize()
+        if pool > 1 or n > 0:  # refresh the spent copies for the timed steps
+            for c in (clones if n > 0 else clones[-1:]):
+                for k in master:
+                    c[k].copy_(master[k])
+        torch.cuda.synchronize()
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(pool + 1)] for _ in qs]
+        t_begin = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        t_begin.record(stream)
+        for i in range(pool):
+            eng.bind(clones[i])
+            if i == 0:
+                for q, m in zip(qs, marks):
+                    m[0].record(q)
+            eng.replicate_tick(lp_d, gf, where=DEVICE)
+            for q, m in zip(qs, marks):
+                m[i + 1].record(q)
+        eng.synchronize()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        span = max(t_begin.elapsed_time(m[-1]) for m in marks)
+        launch = [[m[i].elapsed_time(m[i + 1]) for i in range(pool)] for m in marks]
+        km = span / pool if S > 1 else float(np.mean(launch[0]))
+        r = {"ms_per_step": dt / pool * 1e3, "decisions_per_s": G4 * pool / dt,
+             "roofline": {"kernel": f"k_tick_group<5,false> x {S}", "bound": "hbm", "algorithmic_bytes": algo,
+                          "achieved": algo / (km / 1e3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                          "frac": algo / (km / 1e3) / HBM_PEAK, "kernel_ms_mean": km,
+                          "launch_ms_mean": [round(float(np.mean(x)), 4) for x in launch],
+                          "active_groups": active,
+                          "timing": ("HIP events around each launch" if S == 1 else
+                                     "device span of the timed region / steps (first start marker to the last "
+                                     "shard's end marker)")}}
+        if S == 1:
+            r["roofline"]["kernel_ms_steps"] = [round(x, 4) for x in launch[0]]
+            r["roofline"]["kernel_ms_min"] = float(np.min(launch[0]))
+        if S in pj_traffic:
+            r["roofline"]["traffic"], r["roofline"]["traffic_source"] = pj_traffic[S]
+        out["by_shards"][str(S)] = r
     eng.close()
     del clones, master
     torch.cuda.empty_cache()
-    km = float(np.mean(ker))
-    out = {"workload": "config #4 on one GPU: 262,144 groups x 5 peers x 4,096-entry logs (config #3's "
-                       "generator and mix; the N > 1 lines split it N ways), one tick launch per step, "
-                       "fresh copy per step",
-           "groups": G4, "steps": pool, "state_copy_gib": clone_bytes / 2**30, "generate_s": gen_s,
-           "ms_per_step": dt / pool * 1e3, "decisions_per_s": G4 * pool / dt,
-           "roofline": {"kernel": "k_tick_group<5,false>", "bound": "hbm", "algorithmic_bytes": algo,
-                        "achieved": algo / (km / 1e3) / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                        "frac": algo / (km / 1e3) / HBM_PEAK, "kernel_ms_mean": km,
-                        "kernel_ms_min": float(np.min(ker)), "kernel_ms_steps": [round(x, 4) for x in ker],
-                        "active_groups": active}}
-    pj = os.path.join(ROOT, "profiles", f"pmc_traffic_g{G4}.json")
-    if os.path.exists(pj):
-        pm = json.load(open(pj))
-        if pm.get("kernel_src_sha") == kernel_src_sha():
-            out["roofline"]["traffic"] = pm.get("hbm_bytes_per_launch")
-            out["roofline"]["traffic_source"] = f"profiles/{os.path.basename(pj)} ({pm.get('tag')})"
     return out
 
 
-def strong_scaling_ref(strong, world, G_total) -> dict:
+def strong_scaling_ref(strong, world, G_total, shards=1) -> dict:
     """For N > 1 strong-scaling lines of config #4: the N = 1 point of the
-    same series (all 262,144 groups on one GPU), as last measured by a
-    one-GPU bench run (secondary.config4_one_gpu -> tools/write_anchor.py)."""
+    same series (all 262,144 groups on one GPU) with the same number of tick
+    shards per GPU, as last measured by a one-GPU bench run
+    (secondary.config4_one_gpu -> tools/write_anchor.py)."""
     if not (strong and world > 1 and G_total == 262144):
         return {}
     if not os.path.exists(CONFIG4_ANCHOR):
         return {"strong_scaling_reference_ms": None,
                 "strong_scaling_reference": {"what": "no one-GPU config #4 anchor committed"}}
     a = json.load(open(CONFIG4_ANCHOR))
-    return {"strong_scaling_reference_ms": a.get("ms_per_step"),
+    by = a.get("by_shards") or {}
+    e = by.get(str(shards))
+    if e is None:
+        return {"strong_scaling_reference_ms": None,
+                "strong_scaling_reference": {"what": f"no one-GPU config #4 anchor with {shards} tick shard(s) "
+                                                     f"committed (have: {sorted(by)})",
+                                             "source": f"profiles/{os.path.basename(CONFIG4_ANCHOR)} ({a.get('tag')})"}}
+    return {"strong_scaling_reference_ms": e.get("ms_per_step"),
             "strong_scaling_reference": {
-                "what": "N = 1 point of this series: config #4's 262,144 groups on one GPU "
-                        "(secondary.config4_one_gpu of a one-GPU bench.py run, same generator and timing)",
+                "what": "N = 1 point of this series: config #4's 262,144 groups on one GPU with the same "
+                        f"tick shards per GPU ({shards}) (secondary.config4_one_gpu of a one-GPU bench.py run, "
+                        "same generator and timing)",
+                "shards_per_gpu": shards,
                 "source": f"profiles/{os.path.basename(CONFIG4_ANCHOR)} ({a.get('tag')})",
-                "ms_per_step": a.get("ms_per_step"), "kernel_ms_mean": a.get("kernel_ms_mean"),
-                "decisions_per_s": a.get("decisions_per_s")}}
+                "ms_per_step": e.get("ms_per_step"), "kernel_ms_mean": e.get("kernel_ms_mean"),
+                "decisions_per_s": e.get("decisions_per_s")}}
 
 
 def placement_probe(copies, G, P, L, dev):
@@ -486,31 +527,26 @@ def describe_workload(strong, world, G_total, P, L, config, dist_on, rccl, backe
     return w
 
 
-def full_mask_stream(device: int) -> int:
-    """A HIP stream on a dedicated hardware queue: hipExtStreamCreateWithCUMask
-    with every CU of the device enabled (host plumbing for --shards)."""
-    import ctypes
-    import torch
-    hip = ctypes.CDLL("libamdhip64.so")
-    ncu = torch.cuda.get_device_properties(device).multi_processor_count
-    nw = (ncu + 31) // 32
-    mask = (ctypes.c_uint32 * nw)(*[(0xFFFFFFFF if (w + 1) * 32 <= ncu else (1 << (ncu - 32 * w)) - 1)
-                                    for w in range(nw)])
-    s = ctypes.c_void_p()
-    rc = hip.hipSetDevice(device)
-    rc = rc or hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), nw, mask)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
-    return s.value
-
-
-def destroy_stream(handle: int) -> None:
-    """Destroys a full_mask_stream (before the process exits: a stream left
-    to the runtime's teardown crashed it under rocprofv3)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipStreamSynchronize(ctypes.c_void_p(handle))
-    hip.hipStreamDestroy(ctypes.c_void_p(handle))
+def stream_plan(shards: int, rccl: bool, fanin_cus: int, fanin: str) -> dict:
+    """The streams and hardware queues one rank uses (include/mraft.h), and
+    what orders the fan-in: the engine owns every queue it creates and
+    destroys them in mraft_destroy. Asserted by tests/test_bench_launch.py for
+    the N > 1 default (2 shards + the RCCL fan-in)."""
+    masked = rccl and fanin_cus > 0
+    plan = {
+        "engine_stream": "pooled HIP stream (torch's and the engine's; carries no tick when shards > 1)",
+        "tick_queues": shards if shards > 1 else 0,
+        "tick_queue_mask": ("every CU but the fan-in's %d" % fanin_cus if masked else "every CU")
+        if shards > 1 else None,
+        "tick_on": "engine stream" + (" (masked off the fan-in's CUs)" if masked else "") if shards == 1
+        else f"{shards} shard queues",
+        "fanin_queue": (1 if masked else 0) if rccl else None,
+        "fanin_on": None if not rccl else ("engine stream" if fanin == "inline" else
+                                           "fan-in queue (%d CUs)" % fanin_cus if masked else "fan-in stream (pooled)"),
+        "fanin_waits_for": None if not rccl else "the end marker of every shard's tick",
+    }
+    plan["dedicated_queues"] = plan["tick_queues"] + (plan["fanin_queue"] or 0) + (1 if masked and shards == 1 else 0)
+    return plan
 
 
 def spawn_ranks(n: int) -> int:
@@ -664,11 +700,15 @@ def main():
 
     rccl = dist_on and args.dist_backend == "nccl"
     if args.dry_run:
+        S_dry = args.shards if (args.shards > 1 and G >= args.shards) else 1
+        plans = [stream_plan(S_dry, rccl, args.fanin_cus, args.fanin)]
         if dist_on:
             dist.barrier()
             n = torch.tensor([float(G)], dtype=torch.float64)
             dist.all_reduce(n)
             assert int(n.item()) == G_total, "the shards do not cover the workload"
+            plans = [None] * world
+            dist.all_gather_object(plans, stream_plan(S_dry, rccl, args.fanin_cus, args.fanin))
         if rank == 0:
             print(json.dumps({
                 "metric": METRIC, "value": None, "unit": "decisions/s", "n_gpus": world,
@@ -678,8 +718,9 @@ def main():
                                                          dist_on, rccl, args.dist_backend),
                            "groups_per_gpu": G, "global_groups": G_total, "peers": P,
                            "log_capacity": L, "shard_of_rank0": [0, G],
-                           "leaders_in_shard_rank0": int((lp >= 0).sum())},
-                **strong_scaling_ref(strong, world, G_total)}),
+                           "leaders_in_shard_rank0": int((lp >= 0).sum()),
+                           "shards_per_gpu": S_dry, "stream_plan_by_rank": plans},
+                **strong_scaling_ref(strong, world, G_total, S_dry)}),
                 file=result_out, flush=True)
         if dist_on:
             dist.barrier()
@@ -702,54 +743,29 @@ def main():
     log(rank, f"{pool} state copies of {clone_bytes / 2**30:.2f} GiB each"
               f"{' (restore inside timed steps)' if restore else ''}")
 
+    # Group shards (--shards): the engine splits every tick into S contiguous
+    # group ranges, each launched on a hardware queue the engine owns
+    # (mraft_set_tick_shards); shard s's tick i+1 follows only its own tick i.
+    S = args.shards if (args.shards > 1 and not restore and G >= args.shards) else 1
     eng = Engine(G, P, L, device=local_dev, alloc=False)
+    eng.set_tick_shards(S)
     if rccl and args.fanin_cus:
-        # the tick runs on a stream masked off the reserved CUs (include/mraft.h)
+        # the tick's queues are masked off the fan-in's reserved CUs (include/mraft.h)
         eng.fanin_reserve_cus(args.fanin_cus)
+    if S == 1 and rccl and args.fanin_cus:
         stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
     else:
         # A dedicated (non-null) stream shared by torch and the engine, so the
-        # events below bracket exactly the engine's kernels.
+        # events below bracket exactly the engine's kernels (S = 1) or fork
+        # the shard queues after torch's work (S > 1).
         stream = torch.cuda.Stream(dev)
         eng.set_stream(stream.cuda_stream)
     torch.cuda.set_stream(stream)
+    tick_streams = ([stream] if S == 1 else
+                    [torch.cuda.ExternalStream(eng.shard_stream(si), device=dev) for si in range(S)])
     lp_d = torch.from_numpy(lp).to(dev)
     gf_d = torch.zeros(G, dtype=torch.int32, device=dev)
-    # Group shards (--shards): shard s = groups [s*gs, (s+1)*gs) of every state
-    # copy (contiguous slices of each SoA array: no copies), its own engine and
-    # stream (shard 0's is the main stream). One shard: the main engine itself.
-    S = args.shards if (args.shards > 1 and not restore and G % args.shards == 0) else 1
-    gs = G // S
-    per_group = {k: v.numel() // G for k, v in master.items()}
-    shards = []
-    own_streams = []  # full_mask_stream handles, destroyed at the end
-    for si in range(S):
-        if S == 1:
-            e_s, st_s = eng, stream
-        else:
-            # Each shard's stream on a hardware queue of its own: a stream
-            # created with a CU mask gets a dedicated queue (pooled streams may
-            # share one, and two shards' launches on one queue serialise).
-            # Without the fan-in the mask holds every CU; with it, the same CUs
-            # as the main tick stream (mraft_fanin_reserve_cus).
-            e_s = Engine(gs, P, L, device=local_dev, alloc=False)
-            if rccl and args.fanin_cus:
-                e_s.fanin_reserve_cus(args.fanin_cus)
-                st_s = torch.cuda.ExternalStream(e_s.stream(), device=dev)
-            else:
-                own_streams.append(full_mask_stream(local_dev))
-                st_s = torch.cuda.ExternalStream(own_streams[-1], device=dev)
-                e_s.set_stream(st_s.cuda_stream)
-        shards.append((e_s, st_s, slice(si * gs, (si + 1) * gs)))
-    if S > 1:
-        stream = shards[0][1]  # the timing and the fan-in's first wait follow shard 0's stream
-        torch.cuda.set_stream(stream)
-
-    def shard_views(c):
-        return [{k: v[sl.start * per_group[k]:sl.stop * per_group[k]] for k, v in c.items()}
-                for (_, _, sl) in shards]
-
-    views = [shard_views(c) for c in clones] if S > 1 else None
+    plan = stream_plan(S, rccl, args.fanin_cus, args.fanin)
     on_host = dist_on and not rccl
     # Per-step GetState export blocks (commitIndex | term<<1|leader, one buffer
     # so the router's fan-in is ONE collective per tick) and their gathers:
@@ -771,17 +787,16 @@ def main():
     rd, wr, active = eng.replicate_tick_count(lp_d, where=DEVICE)
     algo_bytes = 4 * (rd + wr)
 
-    # Per-launch kernel timing on the engine's stream. With nothing else on the
-    # stream between ticks (no restores) one marker between consecutive ticks
+    # Per-launch kernel timing on the tick's queue(s). With nothing else on a
+    # queue between ticks (no restores) one marker between consecutive ticks
     # serves as the end of one and the start of the next, and the fan-in
     # stream waits on that same marker (MRAFT_FANIN_ORDERED): one marker
-    # packet per tick on the tick's queue. Every extra marker there costs the
+    # packet per tick on each tick queue. Every extra marker there costs the
     # step a few microseconds of idle device (the round-2 fan-in runs recorded
     # four per tick: ~20 us per step beyond the kernel).
     chain = not restore and args.fanin_marks == "chain"
     marks_s = [[torch.cuda.Event(enable_timing=True) for _ in range(K + 1 if chain else 2 * K)]
                for _ in range(S)]
-    marks = marks_s[0]
     t_begin = torch.cuda.Event(enable_timing=True)
     t_end = [torch.cuda.Event(enable_timing=True) for _ in range(S)]
     extra = [torch.cuda.Event() for _ in range(args.extra_marks)]
@@ -804,26 +819,18 @@ def main():
         else:
             c = clones[i] if timed else clones[K]
         j = i if timed else K + i  # timed steps use blocks 0..K-1, warmup K..K+W-1
-        if S == 1:
-            eng.bind(c)
-            if timed and (i == 0 or not chain):
-                mark_start(i).record(stream)
-            # the tick with the GetState export fused in (one launch per step)
-            eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
-            if timed:
-                mark_end(i).record(stream)
-        else:
-            vs = views[i] if timed else views[K]
-            for si, (e_s, st_s, sl) in enumerate(shards):
-                e_s.bind(vs[si])
-                if timed and (i == 0 or not chain):
-                    mark_start(i, si).record(st_s)
-                e_s.replicate_tick_export(lp_d[sl], gf_d[sl], status[j, :G][sl], status[j, G:][sl],
-                                          where=DEVICE)
-                if timed:
-                    mark_end(i, si).record(st_s)
+        eng.bind(c)
+        if timed and (i == 0 or not chain):
+            for si in range(S):
+                mark_start(i, si).record(tick_streams[si])
+        # the tick with the GetState export fused in (one call per step; S
+        # launches on the engine's shard queues when S > 1)
+        eng.replicate_tick_export(lp_d, gf_d, status[j, :G], status[j, G:], where=DEVICE)
+        if timed:
+            for si in range(S):
+                mark_end(i, si).record(tick_streams[si])
         for x in extra:  # experiment: marker packets between ticks
-            x.record(stream)
+            x.record(tick_streams[0])
         if dist_on:  # the shard router's fan-in
             if on_host:
                 t1 = time.perf_counter()
@@ -834,19 +841,16 @@ def main():
                 # RCCL all-gather of this tick's words (C ABI). Overlapped: on
                 # the fan-in stream after the tick, beside the next tick (which
                 # writes another block), so the next batch never waits for it.
+                # Untimed steps let the engine order it (it waits for every
+                # shard's last launch, include/mraft.h).
                 ordered = False
-                if overlap and timed and chain:
-                    # the fan-in stream waits on the tick's own end marker
-                    # (every shard's)
+                if timed:
+                    # the gather (and its start mark) waits on every shard's
+                    # end marker: the fan-in stream (overlap) or the engine
+                    # stream (inline; the engine would join the shards there)
                     for si in range(S):
                         comm_stream.wait_event(mark_end(i, si))
-                    ordered = True
-                elif timed and overlap:
-                    # the gather starts once the tick is done: its start mark
-                    # waits for the tick on the fan-in stream as well
-                    for (_, st_s, _) in shards:
-                        comm_stream.wait_stream(st_s)
-                if timed:
+                    ordered = overlap
                     ag_marks[2 * i].record(comm_stream)
                 fan.gather(status[j], gathered[j], overlap=overlap, ordered=ordered)
                 if timed:
@@ -854,18 +858,18 @@ def main():
 
     for i in range(W):
         step(i, False)
+    eng.synchronize()
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    t_begin.record(stream)
-    for (_, st_s, _) in shards[1:]:
-        st_s.wait_event(t_begin)
+    t_begin.record(stream)  # the first tick's shard queues fork from this stream after it
     for i in range(K):
         step(i, True)
-    for si, (_, st_s, _) in enumerate(shards):
-        t_end[si].record(st_s)
+    for si in range(S):
+        t_end[si].record(tick_streams[si])
+    eng.synchronize()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if dist_on:
@@ -880,12 +884,14 @@ def main():
         ck = clones[K]
         for k in ck:
             ck[k].copy_(master[k])
-        torch.cuda.synchronize()  # the copies ran on torch's stream, the tick runs on the engine's
-        eng.bind(ck)
+        one = Engine(G, P, L, device=local_dev, alloc=False)  # one launch, on torch's stream
+        one.set_stream(stream.cuda_stream)
+        one.bind(ck)
         gf1 = torch.zeros_like(gf_d)
         st1 = torch.zeros_like(status[0])
-        eng.replicate_tick_export(lp_d, gf1, st1[:G], st1[G:], where=DEVICE)
-        torch.cuda.synchronize()
+        one.replicate_tick_export(lp_d, gf1, st1[:G], st1[G:], where=DEVICE)
+        one.synchronize()
+        one.close()
         assert torch.equal(gf1, gf_d) and torch.equal(st1, status[K - 1]), "sharded tick differs from one launch"
     # per step: one launch (S = 1), or the shards' launches overlapping: the
     # step's share of the device span, apportioned by its launches' durations
@@ -916,14 +922,13 @@ def main():
     achieved = algo_bytes / ker_s
     traffic, traffic_src = None, None
     if not args.pmc_json:
-        args.pmc_json = os.path.join(ROOT, "profiles", "pmc_traffic.json" if G == 65536
-                                     else f"pmc_traffic_g{G}.json")
+        args.pmc_json = pmc_json_path(G, S)
     if os.path.exists(args.pmc_json):
         # PMC traffic of this exact kernel source and config, from the
         # committed rocprofv3 summary (tools/profile_round.sh + pmc_summary.py).
         try:
             pm = json.load(open(args.pmc_json))
-            if ((pm.get("groups"), pm.get("peers"), pm.get("log")) == (G, P, L)
+            if ((pm.get("groups"), pm.get("peers"), pm.get("log"), pm.get("shards", 1)) == (G, P, L, S)
                     and pm.get("kernel_src_sha") == kernel_src_sha()):
                 traffic = pm.get("hbm_bytes_per_launch")
                 traffic_src = f"profiles/{os.path.basename(args.pmc_json)} ({pm.get('tag')})"
@@ -958,9 +963,11 @@ def main():
                    "step_minus_kernel_ms": dt / K * 1e3 - float(np.mean(ker_ms)),
                    "shards_per_gpu": S,
                    "shard_pipelining": (None if S == 1 else
-                                        f"{S} engines on {S} streams over contiguous group ranges of "
-                                        f"{gs}; each shard's tick i+1 follows its tick i on its own "
-                                        "stream, the shards' launches overlap (DESIGN.md §6)")},
+                                        f"mraft_set_tick_shards({S}): one engine, {S} contiguous group "
+                                        f"ranges of ~{G // S} on {S} hardware queues the engine owns; each "
+                                        "shard's tick i+1 follows its own tick i, the shards' launches "
+                                        "overlap (DESIGN.md §6)"),
+                   "stream_plan": plan},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
@@ -970,9 +977,12 @@ def main():
                      "algorithmic_read_bytes": 4 * rd, "algorithmic_write_bytes": 4 * wr,
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "algorithmic_bytes_per_decision": algo_bytes / max(active, 1),
-                     "kernel_ms_mean": ker_s * 1e3, "kernel_ms_min": float(np.min(ker_ms)),
-                     "kernel_ms_median": float(np.median(ker_ms)),
-                     "kernel_ms_steps": [round(float(x), 4) for x in ker_ms],
+                     "kernel_ms_mean": ker_s * 1e3,
+                     "kernel_ms_min": float(np.min(ker_ms)) if S == 1 else None,
+                     "kernel_ms_median": float(np.median(ker_ms)) if S == 1 else None,
+                     ("kernel_ms_steps" if S == 1 else "kernel_ms_steps_apportioned"):
+                         [round(float(x), 4) for x in ker_ms],
+                     "launch_ms_steps": None if S == 1 else [[round(float(x), 4) for x in sh] for sh in launch_ms],
                      "device_ms_per_step": span_ms / K,
                      "launches_per_step": S,
                      "launch_ms_mean": [round(float(np.mean(x)), 4) for x in launch_ms],
@@ -980,8 +990,9 @@ def main():
                                 f"{S} overlapping launches per step (one per shard and stream): "
                                 "kernel_ms_mean = device time of the timed region / steps (events "
                                 "from the first launch's start to the last shard's end); "
-                                "kernel_ms_steps apportions it by each step's launch durations; "
-                                "launch_ms_mean = each shard's launch duration, overlap included"),
+                                "kernel_ms_steps_apportioned splits it by each step's launch durations "
+                                "(derived, not measured per step); launch_ms_steps / launch_ms_mean = "
+                                "each shard's measured launch durations, overlap included"),
                      "note": ("each step ticks its own fresh state copy; copies whose log image sits in "
                               "physical memory that takes streaming writes ~10 % slower run ~13 % slower "
                               "(DESIGN.md §5 placement lottery): kernel_ms_steps shows both populations"),
@@ -990,7 +1001,7 @@ def main():
     }
     if world > 1:
         out["roofline"]["kernel_ms_mean_max_over_ranks"] = ker_max_ms
-    out.update(strong_scaling_ref(strong, world, G_total))
+    out.update(strong_scaling_ref(strong, world, G_total, S))
     if world == 1 and not restore:
         pp = placement_probe(clones[:K], G, P, L, dev)
         if pp is not None:
@@ -1011,8 +1022,11 @@ def main():
                     kms = float(km[sel].mean())
                     pops[name] = {"steps": int(sel.sum()), "kernel_ms_mean": round(kms, 4),
                                   "frac": algo_bytes / (kms / 1e3) / HBM_PEAK}
+                if S > 1:  # per-step device time is apportioned (derived) with overlapping shards
+                    for v in pops.values():
+                        v["apportioned"] = True
                 pp["populations"] = pops
-                pp["corr_with_kernel_ms"] = float(np.corrcoef(pm, km)[0, 1])
+                pp["corr_with_kernel_ms" if S == 1 else "corr_with_apportioned_ms"] = float(np.corrcoef(pm, km)[0, 1])
             out["roofline"]["placement_probe"] = pp
     if (world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096
             and fan is None):
@@ -1020,13 +1034,15 @@ def main():
         # config #4's N = 1 anchor: free config #3's copies, then all 262,144 groups on this GPU
         eng.close()
         del clones, master
-        views = ck = None  # the shards' slices of the copies
+        ck = None
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        c4 = config4_one_gpu(dev, stream)
+        c4 = config4_one_gpu(dev, stream, shards=(1, 2))
         out["secondary"]["config4_one_gpu"] = c4
-        log(rank, f"config #4 on one GPU: {c4['ms_per_step']:.4f} ms/step, tick {c4['roofline']['kernel_ms_mean']:.4f} ms "
-                  f"({c4['roofline']['frac']:.3f} of 8 TB/s) over {c4['steps']} fresh copies")
+        for sk, c in c4["by_shards"].items():
+            log(rank, f"config #4 on one GPU, {sk} shard(s): {c['ms_per_step']:.4f} ms/step, device "
+                      f"{c['roofline']['kernel_ms_mean']:.4f} ms ({c['roofline']['frac']:.3f} of 8 TB/s) over "
+                      f"{c4['steps']} fresh copies")
     if rank == 0 and not args.no_cpu_baseline:
         # rank 0 only (the other ranks wait at the barrier below); a shorter
         # sample with more than one rank
@@ -1039,14 +1055,7 @@ def main():
     if fan is not None:
         eng.fanin_synchronize()
         fan.close()
-    if S > 1:
-        torch.cuda.synchronize()
-        for (e_s, _, _) in shards:
-            e_s.close()
-        torch.cuda.set_stream(torch.cuda.default_stream(dev))
-        for h in own_streams:
-            destroy_stream(h)
-    eng.close()
+    eng.close()  # waits for and destroys the engine's shard and fan-in queues
     if dist_on:
         dist.destroy_process_group()
 

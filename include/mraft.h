@@ -27,7 +27,8 @@
  *    call is asynchronous on the engine's stream; with MRAFT_HOST it is
  *    synchronous (results are in the caller's buffers on return).
  *  - Concurrency: calls on one handle must be serialized by the caller (one
- *    handle per GPU, one stream per handle). Within a call, items addressed to
+ *    handle per GPU, one stream per handle — plus, optionally, the engine's
+ *    own tick-shard queues, mraft_set_tick_shards). Within a call, items addressed to
  *    the same replica slot are NOT allowed (the reference serializes them under
  *    rf.mu, raft.go:17): all but the lowest-indexed such item are rejected with
  *    MRAFT_ITEM_DUP_SLOT in item_err and the rest are processed. Host-side
@@ -53,7 +54,7 @@
 extern "C" {
 #endif
 
-#define MRAFT_ABI_VERSION 3
+#define MRAFT_ABI_VERSION 4
 
 /* Node states, raft_rpc.go:8-12 (values preserved). */
 enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
@@ -62,7 +63,15 @@ enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
 enum { MRAFT_HOST = 0, MRAFT_DEVICE = 1 };
 
 /* mraft_create flags */
-enum { MRAFT_CREATE_NO_ALLOC = 1 };
+enum {
+  MRAFT_CREATE_NO_ALLOC = 1,
+  /* The engine's own stream is created on a hardware queue of its own
+   * (hipExtStreamCreateWithCUMask with every CU) instead of taken from the HIP
+   * runtime's pool, where it may share a queue with another stream and its
+   * launches would then run after that stream's. Owned and destroyed by
+   * mraft_destroy. */
+  MRAFT_CREATE_DEDICATED_QUEUE = 2
+};
 
 /* Return status codes. */
 enum {
@@ -270,11 +279,13 @@ typedef struct mraft_engine mraft_engine;
  * = dummyIndex. peers in [1, 8]; log_capacity >= 1. */
 int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity,
                  int32_t device, uint32_t flags, mraft_engine **out);
-/* Replaces Kill (utility.go:9-19): frees device state owned by the engine. */
+/* Replaces Kill (utility.go:9-19): waits for the engine's queues, frees device
+ * state and every stream / queue the engine created. */
 int mraft_destroy(mraft_engine *h);
 /* Use a caller-provided hipStream_t (NULL = the engine's own stream). */
 int mraft_set_stream(mraft_engine *h, void *hip_stream);
 void *mraft_get_stream(mraft_engine *h);
+/* Host wait for all work of the handle (engine stream and tick shards). */
 int mraft_synchronize(mraft_engine *h);
 int mraft_dims(const mraft_engine *h, int32_t *groups, int32_t *peers,
                int32_t *log_capacity);
@@ -317,7 +328,11 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * writing such rows, run after the others, the former from a staged copy.
  * The call then blocks the host until the batch plan is known: the main
  * launch's first workgroup publishes it when that launch starts (the GPU keeps
- * working meanwhile). */
+ * working meanwhile). If the plan is not published within 120 s (a stream
+ * blocked on something that never comes) the call fails with MRAFT_E_HIP and
+ * the handle is poisoned: the queued launches may still change state when the
+ * stream unblocks, the batch's deferred items never run, and every later call
+ * on the handle fails with MRAFT_E_HIP. */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,
@@ -343,6 +358,29 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items,
  * group_flags (optional, [G]) gets MRAFT_G_* bits. */
 int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer,
                          int32_t *group_flags, int32_t where);
+
+/* Tick group shards (one handle standing for many Raft instances, `Make`
+ * raft.go:51-87, whose groups share nothing: raft.go:16-40). With shards >= 2
+ * the engine creates that many hardware queues of its own (CU-masked streams:
+ * every CU, or every CU the fan-in has not reserved, mraft_fanin_reserve_cus),
+ * owned and destroyed by mraft_destroy, and every mraft_replicate_tick[_export]
+ * splits the groups into `shards` contiguous ranges (shard s = groups
+ * [G*s/S, G*(s+1)/S)), launching shard s on queue s. Each queue first waits for
+ * the work already on the engine stream (the tick's inputs), but NOT for the
+ * other shards: shard s's tick i+1 follows only its own tick i, so one shard's
+ * last waves run beside another shard's steady state instead of the device
+ * idling through a launch's ramp-down. Every other call (including a
+ * host-buffer tick's copy-back, mraft_synchronize and a non-overlapped fan-in)
+ * first orders the engine stream after the outstanding shard launches (a
+ * device-side wait, no host wait); an overlapped fan-in waits for them on the
+ * fan-in stream only. Decisions are identical to one launch (the groups are
+ * independent). shards = 1 (the default) restores one launch on the engine
+ * stream. Waits for all outstanding work first. shards in [1, 8], <= G. */
+int mraft_set_tick_shards(mraft_engine *h, int32_t shards);
+int32_t mraft_get_tick_shards(const mraft_engine *h);
+/* The hipStream_t of tick shard `shard` (the engine stream when shards == 1;
+ * NULL when out of range): for events that time or order against a shard. */
+void *mraft_shard_stream(mraft_engine *h, int32_t shard);
 
 /* mraft_replicate_tick followed by mraft_export_group_status for the same
  * leader_peer, fused into the one launch (the words the shard router
@@ -586,11 +624,13 @@ int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local,
 int mraft_fanin_synchronize(mraft_engine *h);
 /* The fan-in stream (a hipStream_t), e.g. for events. */
 void *mraft_fanin_stream(mraft_engine *h);
-/* Reserve n_cus compute units for the fan-in: the engine's own stream becomes
- * a stream whose kernels (the tick) may use every CU but those, and the
- * fan-in stream one limited to those, so an overlapped gather does not queue
- * for CU slots behind a tick that fills the device. n_cus = 0 restores the
- * unmasked streams. Replaces a stream set with mraft_set_stream. */
+/* Reserve n_cus compute units for the fan-in: the engine's own stream (with
+ * tick shards: every shard queue instead) becomes a stream whose kernels (the
+ * tick) may use every CU but those, and the fan-in stream one limited to those,
+ * so an overlapped gather does not queue for CU slots behind a tick that fills
+ * the device. n_cus = 0 restores the unmasked streams. Replaces a stream set
+ * with mraft_set_stream (one shard). Hardware queues the engine then owns: the
+ * fan-in's, and the tick's (one, or one per shard). */
 int mraft_fanin_reserve_cus(mraft_engine *h, int32_t n_cus);
 
 #ifdef __cplusplus

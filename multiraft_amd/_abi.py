@@ -19,6 +19,7 @@ SYNTH_PATH = os.path.join(_HERE, "libmraft_synth.so")
 LEADER, CANDIDATE, FOLLOWER = 1, 2, 3
 HOST, DEVICE = 0, 1
 CREATE_NO_ALLOC = 1
+CREATE_DEDICATED_QUEUE = 2
 OK, E_INVAL, E_NOMEM, E_HIP, E_NOSTATE = 0, -1, -2, -3, -4
 (ITEM_OK, ITEM_PREV_BEYOND_LAST, ITEM_BELOW_DUMMY, ITEM_LOG_FULL, ITEM_NEED_SNAPSHOT,
  ITEM_DUP_SLOT, ITEM_BAD_SLOT, ITEM_BAD_STATE) = range(8)
@@ -28,7 +29,7 @@ G_SNAPSHOT_INSTALLED = 256
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
  G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 FANIN_OVERLAP = 1
 FANIN_ORDERED = 2
 COMM_ID_BYTES = 128
@@ -94,6 +95,7 @@ ABI_SYMBOLS = (
     "mraft_collect_apply_compact",
     "mraft_comm_unique_id", "mraft_comm_init", "mraft_comm_destroy", "mraft_allgather_status",
     "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
+    "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -143,6 +145,9 @@ _SIGS = {
     "mraft_fanin_synchronize": (ctypes.c_int, [_vp]),
     "mraft_fanin_stream": (_vp, [_vp]),
     "mraft_fanin_reserve_cus": (ctypes.c_int, [_vp, _i32]),
+    "mraft_set_tick_shards": (ctypes.c_int, [_vp, _i32]),
+    "mraft_get_tick_shards": (_i32, [_vp]),
+    "mraft_shard_stream": (_vp, [_vp, _i32]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

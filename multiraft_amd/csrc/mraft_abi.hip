@@ -18,6 +18,8 @@
 #include "mraft_device.h"
 #include "mraft_internal.h"
 
+constexpr int kMaxShards = 8;
+
 struct mraft_engine {
   int32_t G = 0, P = 0, L = 0, device = 0;
   bool owned = false, bound = false;
@@ -27,6 +29,20 @@ struct mraft_engine {
   // stream by an event; optional CU-masked pair (mraft_fanin_reserve_cus)
   hipStream_t fanin_own = nullptr, fanin_masked = nullptr, tick_masked = nullptr;
   hipEvent_t fanin_ev = nullptr;
+  int32_t fan_cus = 0;  // CUs reserved for the fan-in (the tick side's masks leave them out)
+  // Tick group shards (mraft_set_tick_shards): S dedicated hardware queues the
+  // engine owns; a tick forks onto them from the engine stream (fork_ev) and
+  // the next call of any other kind joins them back (shard_ev), so one shard's
+  // tick i+1 follows only its own tick i.
+  int32_t nshards = 1;
+  hipStream_t shard_q[kMaxShards] = {};
+  hipEvent_t shard_ev[kMaxShards] = {};
+  hipEvent_t fork_ev = nullptr;
+  bool shards_pending = false;
+  // a call that failed with work still queued that may change state later
+  // (the handle call's plan-poll timeout): every later call fails
+  bool poisoned = false;
+  std::string poison_msg;
   unsigned long long *claim = nullptr;
   uint32_t *srcmark = nullptr;             // per slot: epoch of the last call that read its row while writing it
   uint32_t epoch = 0;
@@ -64,6 +80,12 @@ int fail(int code, const char *fmt, ...) {
       return fail(MRAFT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));          \
   } while (0)
 
+#define TRY(expr)          \
+  do {                     \
+    int rc_ = (expr);      \
+    if (rc_) return rc_;   \
+  } while (0)
+
 int64_t gp_of(const mraft_engine *h) { return (int64_t)h->G * h->P; }
 
 mraft::Dev dev_of(const mraft_engine *h) {
@@ -94,7 +116,115 @@ size_t arr_bytes(const mraft_engine *h, int kind) {
 
 int check(const mraft_engine *h) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (h->poisoned) return fail(MRAFT_E_HIP, "engine unusable after an earlier failure: %s", h->poison_msg.c_str());
   if (!h->bound) return fail(MRAFT_E_NOSTATE, "engine has no device state bound");
+  return MRAFT_OK;
+}
+
+// Orders the engine stream after every shard launch still outstanding (no
+// host wait): the shard queues record their join events and the engine
+// stream waits on them.
+int join_shards(mraft_engine *h) {
+  if (!h->shards_pending) return MRAFT_OK;
+  for (int s = 0; s < h->nshards; ++s) {
+    HIP_TRY(hipEventRecord(h->shard_ev[s], h->shard_q[s]));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->shard_ev[s], 0));
+  }
+  h->shards_pending = false;
+  return MRAFT_OK;
+}
+
+// Every entry point but the sharded tick: the handle is usable and earlier
+// sharded ticks are ordered before this call's work on the engine stream.
+int enter(mraft_engine *h) {
+  int rc = check(h);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(h->device));
+  return join_shards(h);
+}
+
+// Host wait for everything the engine has enqueued (engine, shard and fan-in
+// streams). Errors are ignored (teardown paths).
+void drain(mraft_engine *h) {
+  (void)hipStreamSynchronize(h->stream);
+  for (int s = 0; s < h->nshards; ++s)
+    if (h->shard_q[s]) (void)hipStreamSynchronize(h->shard_q[s]);
+  h->shards_pending = false;
+}
+
+// A stream on a hardware queue of its own (hipExtStreamCreateWithCUMask: a
+// CU-masked stream gets a dedicated queue, a pooled stream may share one with
+// another stream, and two launches on one queue run one after the other).
+// tick_side: every CU but the fan-in's reserved ones; otherwise only those.
+int make_queue(mraft_engine *h, bool tick_side, hipStream_t *out) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, h->device));
+  const int ncu = prop.multiProcessorCount, nw = (ncu + 31) / 32;
+  std::vector<uint32_t> mask(nw, 0);
+  // the highest fan_cus CU bits go to the fan-in, the rest to the tick
+  for (int cu = 0; cu < ncu; ++cu)
+    if ((cu >= ncu - h->fan_cus) != tick_side) mask[cu / 32] |= 1u << (cu % 32);
+  HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)nw, mask.data()));
+  return MRAFT_OK;
+}
+
+void destroy_shard_queues(mraft_engine *h) {
+  for (int s = 0; s < kMaxShards; ++s) {
+    if (h->shard_q[s]) {
+      (void)hipStreamSynchronize(h->shard_q[s]);
+      (void)hipStreamDestroy(h->shard_q[s]);
+      h->shard_q[s] = nullptr;
+    }
+    if (h->shard_ev[s]) (void)hipEventDestroy(h->shard_ev[s]);
+    h->shard_ev[s] = nullptr;
+  }
+  h->shards_pending = false;
+}
+
+int create_shard_queues(mraft_engine *h, int n) {
+  for (int s = 0; s < n; ++s) {
+    TRY(make_queue(h, true, &h->shard_q[s]));
+    HIP_TRY(hipEventCreateWithFlags(&h->shard_ev[s], hipEventDisableTiming));
+  }
+  if (!h->fork_ev) HIP_TRY(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  return MRAFT_OK;
+}
+
+// Groups [g0, g1) of the engine's state as a state of their own (the SoA
+// arrays are group-major: no copies).
+mraft::Dev dev_slice(const mraft_engine *h, int32_t g0, int32_t g1) {
+  mraft::Dev d = dev_of(h);
+  const int64_t s0 = (int64_t)g0 * h->P;
+  for (int32_t **p : {&d.term, &d.voted, &d.role, &d.commit, &d.applied, &d.dummy, &d.last, &d.votes, &d.pdirty,
+                      &d.head, &d.hsnap})
+    if (*p) *p += s0;
+  d.log += s0 * h->L;
+  d.match += s0 * h->P;
+  d.next += s0 * h->P;
+  d.G = g1 - g0;
+  return d;
+}
+
+int32_t *off(int32_t *p, int64_t k) { return p ? p + k : nullptr; }
+
+// The tick launch(es): one launch on the engine stream, or with S tick shards
+// one launch per contiguous group range on its own queue, each queue first
+// waiting for the engine stream's prior work (one event, fork_ev).
+int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, int32_t *et) {
+  if (h->nshards <= 1) {
+    mraft::launch_replicate_tick(dev_of(h), lp, gf, ec, et, h->stream);
+    HIP_TRY(hipGetLastError());
+    return MRAFT_OK;
+  }
+  HIP_TRY(hipEventRecord(h->fork_ev, h->stream));
+  for (int s = 0; s < h->nshards; ++s) HIP_TRY(hipStreamWaitEvent(h->shard_q[s], h->fork_ev, 0));
+  for (int s = 0; s < h->nshards; ++s) {
+    const int32_t g0 = (int32_t)((int64_t)h->G * s / h->nshards), g1 = (int32_t)((int64_t)h->G * (s + 1) / h->nshards);
+    if (g1 <= g0) continue;
+    mraft::launch_replicate_tick(dev_slice(h, g0, g1), lp + g0, off(gf, g0), off(ec, g0), off(et, g0), h->shard_q[s]);
+  }
+  h->shards_pending = true;
+  HIP_TRY(hipGetLastError());
   return MRAFT_OK;
 }
 
@@ -153,11 +283,6 @@ struct Stage {
   }
 };
 
-#define TRY(expr)          \
-  do {                     \
-    int rc_ = (expr);      \
-    if (rc_) return rc_;   \
-  } while (0)
 
 int ensure_claim(mraft_engine *h) {
   if (!h->claim) {
@@ -206,7 +331,13 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
   HIP_TRY(hipSetDevice(device));
   mraft_engine *h = new mraft_engine();
   h->G = groups; h->P = peers; h->L = log_capacity; h->device = device;
-  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+  if (flags & MRAFT_CREATE_DEDICATED_QUEUE) {
+    const int rc = make_queue(h, true, &h->own_stream);
+    if (rc) {
+      delete h;
+      return rc;
+    }
+  } else if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete h;
     return fail(MRAFT_E_HIP, "hipStreamCreate failed");
   }
@@ -244,7 +375,7 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
 int mraft_destroy(mraft_engine *h) {
   if (!h) return MRAFT_OK;
   (void)hipSetDevice(h->device);
-  (void)hipStreamSynchronize(h->stream);
+  drain(h);
   free_owned(h);
   for (void *p : h->scratch_ptr)
     if (p) (void)hipFree(p);
@@ -254,9 +385,11 @@ int mraft_destroy(mraft_engine *h) {
   if (h->plan_dev) (void)hipFree(h->plan_dev);
   if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
   if (h->fanin_masked) (void)hipStreamSynchronize(h->fanin_masked);
+  destroy_shard_queues(h);
   for (hipStream_t s : {h->own_stream, h->fanin_own, h->fanin_masked, h->tick_masked})
     if (s) (void)hipStreamDestroy(s);
   if (h->fanin_ev) (void)hipEventDestroy(h->fanin_ev);
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
   delete h;
   return MRAFT_OK;
 }
@@ -264,7 +397,8 @@ int mraft_destroy(mraft_engine *h) {
 int mraft_set_stream(mraft_engine *h, void *stream) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
   h->stream = stream ? (hipStream_t)stream : (h->tick_masked ? h->tick_masked : h->own_stream);
-  return MRAFT_OK;
+  // outstanding shard ticks are ordered before the new stream's work
+  return join_shards(h);
 }
 
 void *mraft_get_stream(mraft_engine *h) { return h ? (void *)h->stream : nullptr; }
@@ -272,6 +406,7 @@ void *mraft_get_stream(mraft_engine *h) { return h ? (void *)h->stream : nullptr
 int mraft_synchronize(mraft_engine *h) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
   HIP_TRY(hipSetDevice(h->device));
+  TRY(join_shards(h));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return MRAFT_OK;
 }
@@ -285,7 +420,7 @@ int mraft_dims(const mraft_engine *h, int32_t *g, int32_t *p, int32_t *l) {
 }
 
 int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!src) return fail(MRAFT_E_INVAL, "src is null");
   HIP_TRY(hipSetDevice(h->device));
   const hipMemcpyKind k = where == MRAFT_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
@@ -298,7 +433,7 @@ int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where) {
 }
 
 int mraft_store_state(mraft_engine *h, const mraft_soa *dst, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!dst) return fail(MRAFT_E_INVAL, "dst is null");
   HIP_TRY(hipSetDevice(h->device));
   const hipMemcpyKind k = where == MRAFT_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -310,7 +445,7 @@ int mraft_store_state(mraft_engine *h, const mraft_soa *dst, int32_t where) {
 }
 
 int mraft_state_view(mraft_engine *h, mraft_soa *out) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!out) return fail(MRAFT_E_INVAL, "out is null");
   *out = h->dev;
   return MRAFT_OK;
@@ -322,7 +457,7 @@ int mraft_bind_state(mraft_engine *h, const mraft_soa *d) {
   for (const auto &a : kArrays)
     if (!(d->*(a.ptr))) return fail(MRAFT_E_INVAL, "bind_state: every array is required");
   if (h->owned) {
-    (void)hipStreamSynchronize(h->stream);
+    drain(h);
     free_owned(h);
   }
   h->dev = *d;
@@ -332,6 +467,9 @@ int mraft_bind_state(mraft_engine *h, const mraft_soa *d) {
 
 // ---------------------------------------------------------------- hot path
 
+// The ticks do not join earlier shard launches (launch_tick forks from the
+// engine stream instead): with tick shards, shard s's tick follows its own
+// previous tick only. A host-buffer tick joins them before its copies back.
 int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer, int32_t *group_flags,
                          int32_t where) {
   TRY(check(h));
@@ -341,8 +479,8 @@ int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer, int32_t *g
   void *lp, *gf;
   TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
   TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
-  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, nullptr, nullptr,
-                               h->stream);
+  TRY(launch_tick(h, (const int32_t *)lp, (int32_t *)gf, nullptr, nullptr));
+  if (where == MRAFT_HOST) TRY(join_shards(h));
   return sg.finish();
 }
 
@@ -357,14 +495,14 @@ int mraft_replicate_tick_export(mraft_engine *h, const int32_t *leader_peer, int
   TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
   TRY(sg.map(commit, sizeof(int32_t) * h->G, false, true, &c));
   TRY(sg.map(term_leader, sizeof(int32_t) * h->G, false, true, &t));
-  mraft::launch_replicate_tick(dev_of(h), (const int32_t *)lp, (int32_t *)gf, (int32_t *)c,
-                               (int32_t *)t, h->stream);
+  TRY(launch_tick(h, (const int32_t *)lp, (int32_t *)gf, (int32_t *)c, (int32_t *)t));
+  if (where == MRAFT_HOST) TRY(join_shards(h));
   return sg.finish();
 }
 
 int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer, int64_t out_words[3],
                                int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!leader_peer || !out_words) return fail(MRAFT_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
@@ -384,7 +522,7 @@ int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer, int6
 
 int mraft_gather_append_args(mraft_engine *h, const int32_t *slots, const int32_t *peers,
                              int64_t n, mraft_ae_args *out_args, int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !peers || !out_args || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -403,7 +541,7 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots, const int32_
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int64_t n,
                                 const int32_t *entry_terms, int64_t n_entry_terms,
                                 mraft_ae_reply *replies, int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -464,8 +602,16 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
       if (q == hipErrorNotReady) {
         // work queued ahead of the plan may take a while, but not forever (e.g.
         // a stream waiting on a host-side dependency that never comes)
-        if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(kPlanPollSeconds))
-          return fail(MRAFT_E_HIP, "append plan not published after %d s (stream blocked?)", kPlanPollSeconds);
+        if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(kPlanPollSeconds)) {
+          // the claim, plan and main launch stay queued and will still change
+          // follower state when the stream unblocks, while the deferred items
+          // never run: the batch would be half-applied, so the engine refuses
+          // every later call
+          h->poisoned = true;
+          h->poison_msg = "an AppendEntries batch was left half-applied (plan-poll timeout)";
+          return fail(MRAFT_E_HIP, "append plan not published after %d s (stream blocked?); engine poisoned",
+                      kPlanPollSeconds);
+        }
         continue;
       }
       HIP_TRY(q);
@@ -489,7 +635,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
 int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, int64_t n,
                                  const int64_t *seg_begin, int64_t n_seg, int32_t *out_flags,
                                  int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
@@ -517,7 +663,7 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
 int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts, int64_t n,
                 int32_t *out_index, int32_t *out_term, int32_t *out_is_leader, int32_t *item_err,
                 int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !out_index || !out_term || !out_is_leader || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -540,7 +686,7 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts, in
 
 int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int32_t *out_snap_index,
                         int32_t *out_snap_term, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!out_from || !out_to) return fail(MRAFT_E_INVAL, "null argument");
   if (!out_snap_index != !out_snap_term) return fail(MRAFT_E_INVAL, "snapshot outputs: both or neither");
   HIP_TRY(hipSetDevice(h->device));
@@ -557,7 +703,7 @@ int mraft_collect_apply(mraft_engine *h, int32_t *out_from, int32_t *out_to, int
 int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *out_snap_index,
                                 int32_t *out_snap_term, int32_t *out_from, int32_t *out_to, int64_t cap,
                                 int64_t *out_n, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (cap < 0 || !out_n || (cap > 0 && (!out_slots || !out_from || !out_to)) ||
       (!out_snap_index) != (!out_snap_term))
     return fail(MRAFT_E_INVAL, "null argument");
@@ -578,7 +724,7 @@ int mraft_collect_apply_compact(mraft_engine *h, int32_t *out_slots, int32_t *ou
 
 int mraft_snapshot(mraft_engine *h, const int32_t *slots, const int32_t *index, int64_t n,
                    int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !index || !item_err))) return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
   HIP_TRY(hipSetDevice(h->device));
@@ -597,7 +743,7 @@ int mraft_snapshot(mraft_engine *h, const int32_t *slots, const int32_t *index, 
 int mraft_gather_install_snapshot_args(mraft_engine *h, const int32_t *slots, const int32_t *peers,
                                        int64_t n, mraft_is_args *out_args, int32_t *item_err,
                                        int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !peers || !out_args || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -616,7 +762,7 @@ int mraft_gather_install_snapshot_args(mraft_engine *h, const int32_t *slots, co
 int mraft_handle_install_snapshot(mraft_engine *h, const mraft_is_args *args, int64_t n,
                                   mraft_is_reply *replies, int32_t *out_flags, int32_t *item_err,
                                   int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !out_flags || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -638,7 +784,7 @@ int mraft_handle_install_snapshot(mraft_engine *h, const mraft_is_args *args, in
 int mraft_process_install_snapshot_replies(mraft_engine *h, const mraft_is_result *items, int64_t n,
                                            const int64_t *seg_begin, int64_t n_seg,
                                            int32_t *out_flags, int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
@@ -665,7 +811,7 @@ int mraft_process_install_snapshot_replies(mraft_engine *h, const mraft_is_resul
 
 int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n, mraft_rv_args *out_args,
                          int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !out_args || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -685,7 +831,7 @@ int mraft_start_election(mraft_engine *h, const int32_t *slots, int64_t n, mraft
 
 int mraft_handle_request_vote(mraft_engine *h, const mraft_rv_args *args, int64_t n,
                               mraft_rv_reply *replies, int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -706,7 +852,7 @@ int mraft_handle_request_vote(mraft_engine *h, const mraft_rv_args *args, int64_
 int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items, int64_t n,
                                const int64_t *seg_begin, int64_t n_seg, int32_t *out_flags,
                                int32_t *item_err, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!items || !out_flags || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
   if (seg_begin && n_seg < 0) return fail(MRAFT_E_INVAL, "n_seg < 0");
@@ -733,7 +879,7 @@ int mraft_process_vote_replies(mraft_engine *h, const mraft_rv_result *items, in
 
 int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask, int32_t rounds,
                           int32_t *group_flags, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!cand_mask || rounds < 0) return fail(MRAFT_E_INVAL, "null mask or negative rounds");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
@@ -747,7 +893,7 @@ int mraft_election_rounds(mraft_engine *h, const uint8_t *cand_mask, int32_t rou
 // ---------------------------------------------------------------- persistence
 
 int mraft_collect_persist(mraft_engine *h, int32_t *out_bits, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!out_bits) return fail(MRAFT_E_INVAL, "out_bits is null");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
@@ -759,7 +905,7 @@ int mraft_collect_persist(mraft_engine *h, int32_t *out_bits, int32_t where) {
 
 int mraft_read_persistent(mraft_engine *h, const int32_t *slots, int64_t n, mraft_persistent *out,
                           int32_t *out_terms, int64_t terms_cap) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!slots || !out))) return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
   for (int64_t i = 0; i < n; ++i)
@@ -793,7 +939,7 @@ int mraft_read_persistent(mraft_engine *h, const int32_t *slots, int64_t n, mraf
 
 int mraft_restore(mraft_engine *h, const mraft_persistent *in, int64_t n, const int32_t *terms,
                   int64_t n_terms, int32_t *item_err) {
-  TRY(check(h));
+  TRY(enter(h));
   if (n < 0 || (n > 0 && (!in || !item_err || (n_terms > 0 && !terms))))
     return fail(MRAFT_E_INVAL, "null argument");
   if (n == 0) return MRAFT_OK;
@@ -830,7 +976,7 @@ int mraft_restore(mraft_engine *h, const mraft_persistent *in, int64_t n, const 
 
 int mraft_export_group_status(mraft_engine *h, const int32_t *leader_peer, int32_t *commit,
                               int32_t *term_leader, int32_t where) {
-  TRY(check(h));
+  TRY(enter(h));
   if (!commit || !term_leader) return fail(MRAFT_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
   Stage sg(h, where);
@@ -903,6 +1049,10 @@ int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local, in
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
   if (!comm || !local || !gathered) return fail(MRAFT_E_INVAL, "null argument");
   HIP_TRY(hipSetDevice(h->device));
+  // Without OVERLAP/ORDERED the gather runs on the engine stream, after the
+  // shard launches (joined). With OVERLAP it waits for them on the fan-in
+  // stream only, so the next tick's shards do not wait for this tick's others.
+  if (where == MRAFT_HOST || !(flags & (MRAFT_FANIN_OVERLAP | MRAFT_FANIN_ORDERED))) TRY(join_shards(h));
   ncclComm_t c = (ncclComm_t)comm;
   int nranks = 0;
   NCCL_TRY(ncclCommCount(c, &nranks));
@@ -923,6 +1073,11 @@ int mraft_allgather_status(mraft_engine *h, void *comm, const int32_t *local, in
     if (!h->fanin_ev) HIP_TRY(hipEventCreateWithFlags(&h->fanin_ev, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(h->fanin_ev, h->stream));
     HIP_TRY(hipStreamWaitEvent(st, h->fanin_ev, 0));
+    if (h->shards_pending)
+      for (int k = 0; k < h->nshards; ++k) {
+        HIP_TRY(hipEventRecord(h->shard_ev[k], h->shard_q[k]));
+        HIP_TRY(hipStreamWaitEvent(st, h->shard_ev[k], 0));
+      }
   }
   NCCL_TRY(ncclAllGather(local, gathered, words, ncclInt32, c, st));
   HIP_TRY(hipGetLastError());
@@ -952,25 +1107,63 @@ int mraft_fanin_reserve_cus(mraft_engine *h, int32_t n_cus) {
   HIP_TRY(hipGetDeviceProperties(&prop, h->device));
   const int ncu = prop.multiProcessorCount;
   if (n_cus < 0 || n_cus >= ncu) return fail(MRAFT_E_INVAL, "n_cus %d of %d CUs", n_cus, ncu);
-  HIP_TRY(hipStreamSynchronize(h->stream));
+  drain(h);
   for (hipStream_t *s : {&h->fanin_masked, &h->tick_masked})
     if (*s) {
       HIP_TRY(hipStreamSynchronize(*s));
       HIP_TRY(hipStreamDestroy(*s));
       *s = nullptr;
     }
+  h->fan_cus = n_cus;
+  // tick shards: their queues take the tick side's mask; the engine stream
+  // carries no tick and stays as it is
+  const int S = h->nshards;
+  if (S > 1) {
+    destroy_shard_queues(h);
+    TRY(create_shard_queues(h, S));
+  }
   if (n_cus == 0) {
-    h->stream = h->own_stream;
+    if (S <= 1) h->stream = h->own_stream;
     return MRAFT_OK;
   }
-  // The highest n_cus CU bits go to the fan-in, the rest to the tick.
-  const int nw = (ncu + 31) / 32;
-  std::vector<uint32_t> tick(nw, 0), fan(nw, 0);
-  for (int cu = 0; cu < ncu; ++cu) (cu >= ncu - n_cus ? fan : tick)[cu / 32] |= 1u << (cu % 32);
-  HIP_TRY(hipExtStreamCreateWithCUMask(&h->tick_masked, (uint32_t)nw, tick.data()));
-  HIP_TRY(hipExtStreamCreateWithCUMask(&h->fanin_masked, (uint32_t)nw, fan.data()));
-  h->stream = h->tick_masked;
+  if (S <= 1) {
+    TRY(make_queue(h, true, &h->tick_masked));
+    h->stream = h->tick_masked;
+  }
+  TRY(make_queue(h, false, &h->fanin_masked));
   return MRAFT_OK;
+}
+
+int mraft_set_tick_shards(mraft_engine *h, int32_t shards) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (shards < 1 || shards > kMaxShards || shards > h->G)
+    return fail(MRAFT_E_INVAL, "shards %d (need 1..%d and at most G = %d)", shards, kMaxShards, h->G);
+  HIP_TRY(hipSetDevice(h->device));
+  drain(h);
+  destroy_shard_queues(h);
+  h->nshards = 1;
+  if (shards > 1) {
+    TRY(create_shard_queues(h, shards));
+    h->nshards = shards;
+    // the masked tick stream of a one-shard engine (mraft_fanin_reserve_cus)
+    // is not needed: the shard queues carry the mask
+    if (h->tick_masked) {
+      if (h->stream == h->tick_masked) h->stream = h->own_stream;
+      HIP_TRY(hipStreamDestroy(h->tick_masked));
+      h->tick_masked = nullptr;
+    }
+  } else if (h->fan_cus > 0 && !h->tick_masked) {
+    TRY(make_queue(h, true, &h->tick_masked));
+    if (h->stream == h->own_stream) h->stream = h->tick_masked;
+  }
+  return MRAFT_OK;
+}
+
+int32_t mraft_get_tick_shards(const mraft_engine *h) { return h ? h->nshards : 0; }
+
+void *mraft_shard_stream(mraft_engine *h, int32_t shard) {
+  if (!h || shard < 0 || shard >= h->nshards) return nullptr;
+  return h->nshards > 1 ? (void *)h->shard_q[shard] : (void *)h->stream;
 }
 
 }  // extern "C"

@@ -109,12 +109,13 @@ def synth_fold_batch(st: dict, G: int, P: int, L: int, leader_peer: np.ndarray, 
 class Engine:
     """One engine handle per GPU (calls must be serialized by the caller)."""
 
-    def __init__(self, G: int, P: int, L: int, device: int = 0, alloc: bool = True):
+    def __init__(self, G: int, P: int, L: int, device: int = 0, alloc: bool = True,
+                 dedicated_queue: bool = False):
         self.G, self.P, self.L = G, P, L
         self._lib = _abi.lib()
         h = ctypes.c_void_p()
-        _ck(self._lib.mraft_create(G, P, L, device, 0 if alloc else _abi.CREATE_NO_ALLOC,
-                                   ctypes.byref(h)), "mraft_create")
+        flags = (0 if alloc else _abi.CREATE_NO_ALLOC) | (_abi.CREATE_DEDICATED_QUEUE if dedicated_queue else 0)
+        _ck(self._lib.mraft_create(G, P, L, device, flags, ctypes.byref(h)), "mraft_create")
         self._h = h
 
     # ---- lifetime --------------------------------------------------------
@@ -143,6 +144,16 @@ class Engine:
 
     def synchronize(self):
         _ck(self._lib.mraft_synchronize(self._h), "mraft_synchronize")
+
+    def set_tick_shards(self, shards: int):
+        """Tick group shards on engine-owned hardware queues (mraft_set_tick_shards)."""
+        _ck(self._lib.mraft_set_tick_shards(self._h, shards), "mraft_set_tick_shards")
+
+    def tick_shards(self) -> int:
+        return int(self._lib.mraft_get_tick_shards(self._h))
+
+    def shard_stream(self, shard: int) -> int:
+        return self._lib.mraft_shard_stream(self._h, shard) or 0
 
     # ---- state -----------------------------------------------------------
     def load_state(self, st: dict, where: int = HOST):

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared(header):
     txt = open(os.path.join(ROOT, "include", header)).read()
-    return set(re.findall(r"^\s*(?:int|int64_t|void\s*\*|const char\s*\*)\s*\*?\s*(mraft_\w+)\s*\(",
+    return set(re.findall(r"^\s*(?:int|int32_t|int64_t|void\s*\*|const char\s*\*)\s*\*?\s*(mraft_\w+)\s*\(",
                           txt, re.M))
 
 
@@ -32,7 +32,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_struct_sizes():
     lib = _abi.lib()
-    assert lib.mraft_abi_version() == _abi.ABI_VERSION == 3
+    assert lib.mraft_abi_version() == _abi.ABI_VERSION == 4
     assert _abi.AE_ARGS.itemsize == 40
     assert _abi.AE_REPLY.itemsize == 16
     assert _abi.RV_RESULT.itemsize == 20

@@ -46,3 +46,23 @@ def test_gpus4_weak_when_groups_given():
     out = _run("--gpus", "4", "--dry-run", "--dist-backend", "gloo", "--groups", "512", "--log", "32")
     assert out["n_gpus"] == 4 and out["scaling"] == "weak"
     assert out["config"]["global_groups"] == 2048
+
+
+def test_gpus2_rank_stream_plan_two_shards_rccl_fanin():
+    """The N > 1 default per rank (verdict r3 #5): 2 tick shards on engine-owned
+    queues masked off the fan-in's 8 CUs, the RCCL fan-in on its own 8-CU queue
+    waiting for every shard's end marker, no masked tick stream on the engine
+    stream, and no more dedicated hardware queues than the box's 4 per process.
+    The plan is computed by every rank (gloo, world size 2) and gathered."""
+    out = _run("--gpus", "2", "--dry-run", "--log", "64")  # default --dist-backend nccl: the RCCL plan
+    c = out["config"]
+    assert c["shards_per_gpu"] == 2
+    plans = c["stream_plan_by_rank"]
+    assert len(plans) == 2 and plans[0] == plans[1]
+    p = plans[0]
+    assert p["tick_queues"] == 2 and p["tick_queue_mask"] == "every CU but the fan-in's 8"
+    assert p["fanin_queue"] == 1 and p["fanin_on"] == "fan-in queue (8 CUs)"
+    assert p["fanin_waits_for"] == "the end marker of every shard's tick"
+    assert p["dedicated_queues"] == 3 <= 4
+    ref = out["strong_scaling_reference"]
+    assert ref.get("shards_per_gpu", 2) == 2 or "2 tick shard" in ref["what"]

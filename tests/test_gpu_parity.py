@@ -12,7 +12,9 @@ from kat_runner import kat_state, load_kats, run_kat  # noqa: E402
 from make_golden import check_kat  # noqa: E402
 from oracle_lib import Oracle, assert_states_equal  # noqa: E402
 
-from multiraft_amd import Engine, entry_positions, synth_fold_batch, synth_seed, synth_tick_state  # noqa: E402
+from multiraft_amd import (Engine, entry_positions, synth_fold_batch, synth_seed, synth_tick_state,  # noqa: E402
+                           )
+from multiraft_amd.engine import export_group_status_into  # noqa: E402
 from multiraft_amd._abi import AE_ARGS, AE_RESULT, RV_ARGS, RV_RESULT  # noqa: E402
 
 pytestmark = pytest.mark.gpu
@@ -475,53 +477,63 @@ def test_applier_compact_snapshot_outputs_gpu():
         assert_states_equal(e.store_state(), o.state(), G, P, L, "applier compact, snapshots")
 
 
-def test_tick_shards_on_dedicated_queues_gpu():
-    """bench.py --shards: engines over contiguous group ranges of one state
-    image (SoA slices, no copies), each on a stream of its own hardware queue,
-    their launches overlapping over several fresh copies, give the same flags,
-    export words and state as one launch over every group (and the oracle)."""
+@pytest.mark.parametrize("S,G", [(2, 4096), (3, 4099), (8, 1031)])
+def test_tick_shards_on_engine_queues_gpu(S, G):
+    """mraft_set_tick_shards: one engine splits every tick into S contiguous
+    group ranges on S hardware queues it owns (uneven ranges when S does not
+    divide G); several ticks over fresh copies overlap on the queues, a
+    following one-launch call (the export) joins them, and every copy's flags,
+    export words and state equal the oracle's (compared directly, not only
+    against one launch)."""
     import torch
 
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from bench import destroy_stream, full_mask_stream
     from multiraft_amd import DEVICE
 
-    G, P, L, S, C = 4096, 5, 256, 2, 3
+    P, L, C = 5, 256, 3
     st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3))
     dev = torch.device("cuda", 0)
     master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
-    per = {k: v.numel() // G for k, v in master.items()}
     lp_d = torch.from_numpy(lp).to(dev)
-    gs = G // S
     copies = [{k: v.clone() for k, v in master.items()} for _ in range(C)]
     flags = [torch.zeros(G, dtype=torch.int32, device=dev) for _ in range(C)]
     exp = [torch.zeros(2 * G, dtype=torch.int32, device=dev) for _ in range(C)]
-    engines, streams = [], []
-    for s in range(S):
-        e = Engine(gs, P, L, alloc=False)
-        streams.append(full_mask_stream(0))
-        e.set_stream(streams[-1])
-        engines.append(e)
-    for c in range(C):
-        for s, e in enumerate(engines):
-            sl = slice(s * gs, (s + 1) * gs)
-            e.bind({k: v[s * gs * per[k]:(s + 1) * gs * per[k]] for k, v in copies[c].items()})
-            e.replicate_tick_export(lp_d[sl], flags[c][sl], exp[c][:G][sl], exp[c][G:][sl], where=DEVICE)
+    after = [torch.zeros(2 * G, dtype=torch.int32, device=dev) for _ in range(C)]
     torch.cuda.synchronize()
-    for e in engines:
-        e.close()
-    for h in streams:
-        destroy_stream(h)
-    with _engine(G, P, L, st) as one:
-        f1, c1, t1 = one.replicate_tick_export(lp)
-        want = one.store_state()
+    with Engine(G, P, L, alloc=False) as e:
+        e.set_tick_shards(S)
+        assert e.tick_shards() == S and all(e.shard_stream(s) for s in range(S)) and not e.shard_stream(S)
+        for c in range(C):
+            e.bind(copies[c])
+            e.replicate_tick_export(lp_d, flags[c], exp[c][:G], exp[c][G:], where=DEVICE)
+        for c in range(C):  # joins the shards: reads every copy's post-tick state
+            e.bind(copies[c])
+            export_group_status_into(e, lp_d, after[c][:G], after[c][G:])
+        e.synchronize()
     o = Oracle(G, P, L, st)
     of = o.replicate_tick(lp)
-    assert np.array_equal(f1, of)
+    oc, ot = o.export_group_status(lp)
     for c in range(C):
-        assert np.array_equal(flags[c].cpu().numpy(), f1)
-        assert np.array_equal(exp[c][:G].cpu().numpy(), c1) and np.array_equal(exp[c][G:].cpu().numpy(), t1)
+        assert np.array_equal(flags[c].cpu().numpy(), of), c
+        assert np.array_equal(exp[c][:G].cpu().numpy(), oc) and np.array_equal(exp[c][G:].cpu().numpy(), ot)
+        assert np.array_equal(after[c][:G].cpu().numpy(), oc) and np.array_equal(after[c][G:].cpu().numpy(), ot)
         got = {k: v.cpu().numpy() for k, v in copies[c].items()}
-        for k in want:
-            if k in got:
-                assert np.array_equal(got[k], want[k]), k
+        assert_states_equal(got, o.state(), G, P, L, f"sharded tick, copy {c}")
+
+
+def test_tick_shards_host_buffers_and_reset_gpu():
+    """A host-buffer tick with shards (staged on the engine stream, forked,
+    joined before the copy-back), then shards = 1 again: both equal the
+    oracle's ticks."""
+    G, P, L = 2048, 5, 128
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + 7)
+    o = Oracle(G, P, L, st)
+    with _engine(G, P, L, st) as e:
+        e.set_tick_shards(4)
+        f1, c1, t1 = e.replicate_tick_export(lp)
+        of = o.replicate_tick(lp)
+        oc, ot = o.export_group_status(lp)
+        assert np.array_equal(f1, of) and np.array_equal(c1, oc) and np.array_equal(t1, ot)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "sharded host tick")
+        e.set_tick_shards(1)
+        assert np.array_equal(e.replicate_tick(lp), o.replicate_tick(lp))
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "tick after shards reset")

@@ -1,0 +1,28 @@
+"""One-screen summary of a bench.py result line (the headline, its roofline
+and, when present, the secondary lines)."""
+import json
+import sys
+
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r, c = d["roofline"], d["config"]
+print(f"value {d['value']:.4g} {d['unit']}  ms/step {d['ms_per_step']:.4f}  device ms {r['kernel_ms_mean']:.4f}  "
+      f"frac {r['frac']:.3f}  shards {c.get('shards_per_gpu')}  step-kernel {c['step_minus_kernel_ms']:.4f}")
+print("launch_ms_mean", r.get("launch_ms_mean"), "traffic", r.get("traffic"), r.get("traffic_source"))
+pp = r.get("placement_probe") or {}
+if pp.get("populations"):
+    print("populations", json.dumps(pp["populations"]))
+s = d.get("secondary") or {}
+if "message_path_config3" in s:
+    m = s["message_path_config3"]
+    print("message path ms", m["ms_per_call"], "handle frac", round(m["roofline"]["frac"], 3),
+          "fold frac", round(m["fold_roofline"]["frac"], 3))
+if "election_storm_config5" in s:
+    e = s["election_storm_config5"]
+    print("config5 ms", round(e["kernel_ms_mean"], 4), {k: v for k, v in e.items() if k == "roofline"})
+if "config4_one_gpu" in s:
+    for k, v in s["config4_one_gpu"]["by_shards"].items():
+        print(f"config4 S={k}: ms/step {v['ms_per_step']:.4f} device {v['roofline']['kernel_ms_mean']:.4f} "
+              f"frac {v['roofline']['frac']:.3f}")
+cb = d.get("cpu_baseline")
+if cb:
+    print("cpu baseline", f"{cb['value']:.4g}", cb["cores"])
