@@ -144,7 +144,33 @@ typedef struct {
   int32_t *has_snapshot;  /* hasSnapshot (raft.go:36,157,168-177): set by an
                              installing HandleInstallSnapshot
                              (raft_snapshot.go:49), consumed by the applier */
+  int32_t *terms_sorted;  /* 1: the terms of the entries after the dummy,
+                             Index dummy+1 .. last, are non-decreasing (a
+                             proof the engine keeps, MRAFT_TERMS_SORTED
+                             below); 0: not known */
 } mraft_soa;
+
+/* terms_sorted (engine bookkeeping, not a Raft field). The leader's commit
+ * rule (advanceCommitIndexForLeader, raft_append_entry.go:89-105) looks for the
+ * highest Index i <= min(M*, last) above commitIndex with term(i) ==
+ * currentTerm, M* being the matchIndex order statistic. When the log's terms
+ * never decrease, term(min(M*, last)) < currentTerm settles it — no lower entry
+ * can carry currentTerm — so the engine reads that one term instead of Go's
+ * downward loop (the decision is identical). Every Raft log the reference can
+ * reach is sorted this way; the engine does not assume it, it keeps a proof
+ * per replica:
+ *   Make (mraft_create), InstallSnapshot installing a new log: 1;
+ *   mraft_load_state, mraft_restore: computed from the terms;
+ *   Start (raft.go:96-100): cleared when term(last) > currentTerm;
+ *   HandleAppendEntries appending from Index k (truncate + append,
+ *   raft_append_entry.go:149-155): set to the args' MRAFT_AE_ENTRIES_SORTED
+ *   flag when k - 1 is the dummy (the new entries are the whole log), else
+ *   cleared unless that flag is set;
+ *   Snapshot / InstallSnapshot's sliceFrom (a suffix of a sorted log is
+ *   sorted): unchanged.
+ * mraft_bind_state takes the caller's array as it is: 1 must only be set
+ * where the terms are non-decreasing (0 everywhere is always correct). */
+enum { MRAFT_TERMS_SORTED = 1 };
 
 /* Persistence (SURVEY.md §5 "Checkpoint / resume", §8f #4). The reference
  * persists currentTerm, votedFor and the log (raft.go:205-216) at fixed call
@@ -181,7 +207,11 @@ typedef struct {
 /* AppendEntriesArgs, raft_rpc.go:55-62. Entries are passed by reference:
  * entry k (0 <= k < n_entries) has Index prev_log_index+1+k (as built by
  * appendOneRound, raft_append_entry.go:50-54) and Term
- * entry_terms[entries_offset + k]. `slot` is the receiving replica. */
+ * entry_terms[entries_offset + k]. `slot` is the receiving replica.
+ * `flags` (not a Go field): MRAFT_AE_ENTRIES_SORTED when the terms
+ * prev_log_term, entry 0, ..., entry n_entries-1 are non-decreasing, set by
+ * mraft_gather_append_args from the leader's terms_sorted; 0 is always
+ * correct. A host that ships args over the network forwards it unchanged. */
 typedef struct {
   int32_t slot;
   int32_t term;
@@ -190,9 +220,11 @@ typedef struct {
   int32_t prev_log_term;
   int32_t leader_commit;
   int32_t n_entries;
-  int32_t _pad;
+  int32_t flags;
   int64_t entries_offset;
 } mraft_ae_args;
+
+enum { MRAFT_AE_ENTRIES_SORTED = 1 };
 
 /* AppendEntriesReply, raft_rpc.go:64-69 (`Conflict` is never set by the
  * reference and is always 0 here). */
@@ -295,12 +327,14 @@ int mraft_abi_version(void);
 /* ---- state transfer (readPersist / SaveState analogues, raft.go:205-235) --- */
 
 /* Copy a full state image into / out of the engine. All arrays required for
- * load; NULL entries are skipped on store. */
+ * load (terms_sorted is recomputed from the logs on load, whatever the source
+ * holds); NULL entries are skipped on store. */
 int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where);
 int mraft_store_state(mraft_engine *h, const mraft_soa *dst, int32_t where);
 /* Device pointers of the state the engine currently works on (zero-copy). */
 int mraft_state_view(mraft_engine *h, mraft_soa *out_device_ptrs);
-/* Bind caller-owned device buffers (all required) as the working state. */
+/* Bind caller-owned device buffers (all required) as the working state
+ * (terms_sorted as the caller holds it: see MRAFT_TERMS_SORTED). */
 int mraft_bind_state(mraft_engine *h, const mraft_soa *device_ptrs);
 
 /* ---- hot path: replication & commit ----------- */

@@ -29,6 +29,8 @@ G_SNAPSHOT_INSTALLED = 256
 (G_ACTIVE, G_COMMITTED, G_STEPPED_DOWN, G_NEED_SNAPSHOT, G_ERROR, G_FOLLOWER_COMMIT,
  G_LOG_FULL, G_ELECTED) = 1, 2, 4, 8, 16, 32, 64, 128
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
+TERMS_SORTED = 1
+AE_ENTRIES_SORTED = 1
 ABI_VERSION = 4
 FANIN_OVERLAP = 1
 FANIN_ORDERED = 2
@@ -45,7 +47,7 @@ _P32 = ctypes.POINTER(ctypes.c_int32)
 
 STATE_FIELDS = ("current_term", "voted_for", "state", "commit_index", "last_applied",
                 "dummy_index", "last_index", "granted_votes", "log_term", "match_index",
-                "next_index", "persist_dirty", "log_head", "has_snapshot")
+                "next_index", "persist_dirty", "log_head", "has_snapshot", "terms_sorted")
 
 
 class MraftSoa(ctypes.Structure):
@@ -54,7 +56,7 @@ class MraftSoa(ctypes.Structure):
 
 AE_ARGS = np.dtype([("slot", "<i4"), ("term", "<i4"), ("leader_id", "<i4"),
                     ("prev_log_index", "<i4"), ("prev_log_term", "<i4"),
-                    ("leader_commit", "<i4"), ("n_entries", "<i4"), ("_pad", "<i4"),
+                    ("leader_commit", "<i4"), ("n_entries", "<i4"), ("flags", "<i4"),
                     ("entries_offset", "<i8")])
 AE_REPLY = np.dtype([("term", "<i4"), ("success", "<i4"), ("conflict_index", "<i4"),
                      ("conflict", "<i4")])

@@ -94,7 +94,7 @@ mraft::Dev dev_of(const mraft_engine *h) {
   d.commit = h->dev.commit_index; d.applied = h->dev.last_applied; d.dummy = h->dev.dummy_index;
   d.last = h->dev.last_index; d.votes = h->dev.granted_votes; d.log = h->dev.log_term;
   d.match = h->dev.match_index; d.next = h->dev.next_index; d.pdirty = h->dev.persist_dirty;
-  d.head = h->dev.log_head; d.hsnap = h->dev.has_snapshot;
+  d.head = h->dev.log_head; d.hsnap = h->dev.has_snapshot; d.srt = h->dev.terms_sorted;
   d.G = h->G; d.P = h->P; d.L = h->L;
   return d;
 }
@@ -106,7 +106,7 @@ const ArrDesc kArrays[] = {
     {&mraft_soa::commit_index, 0}, {&mraft_soa::last_applied, 0}, {&mraft_soa::dummy_index, 0},
     {&mraft_soa::last_index, 0},   {&mraft_soa::granted_votes, 0}, {&mraft_soa::log_term, 1},
     {&mraft_soa::match_index, 2},  {&mraft_soa::next_index, 2},  {&mraft_soa::persist_dirty, 0},
-    {&mraft_soa::log_head, 0},     {&mraft_soa::has_snapshot, 0}};
+    {&mraft_soa::log_head, 0},     {&mraft_soa::has_snapshot, 0}, {&mraft_soa::terms_sorted, 0}};
 
 size_t arr_bytes(const mraft_engine *h, int kind) {
   int64_t gp = gp_of(h);
@@ -196,7 +196,7 @@ mraft::Dev dev_slice(const mraft_engine *h, int32_t g0, int32_t g1) {
   mraft::Dev d = dev_of(h);
   const int64_t s0 = (int64_t)g0 * h->P;
   for (int32_t **p : {&d.term, &d.voted, &d.role, &d.commit, &d.applied, &d.dummy, &d.last, &d.votes, &d.pdirty,
-                      &d.head, &d.hsnap})
+                      &d.head, &d.hsnap, &d.srt})
     if (*p) *p += s0;
   d.log += s0 * h->L;
   d.match += s0 * h->P;
@@ -428,6 +428,8 @@ int mraft_load_state(mraft_engine *h, const mraft_soa *src, int32_t where) {
     if (!(src->*(a.ptr))) return fail(MRAFT_E_INVAL, "load_state: every array is required");
   for (const auto &a : kArrays)
     HIP_TRY(hipMemcpyAsync(h->dev.*(a.ptr), src->*(a.ptr), arr_bytes(h, a.kind), k, h->stream));
+  mraft::launch_terms_sorted(dev_of(h), h->stream);  // the engine's own proof, not the source's claim
+  HIP_TRY(hipGetLastError());
   if (where == MRAFT_HOST) HIP_TRY(hipStreamSynchronize(h->stream));
   return MRAFT_OK;
 }

@@ -28,6 +28,7 @@ struct Dev {
   int32_t *pdirty;  // persist_dirty (include/mraft.h MRAFT_PERSIST_*); may be null
   int32_t *head;    // log_head: ring position of each replica's dummy entry
   int32_t *hsnap;   // has_snapshot (raft.go:158): set by an installing InstallSnapshot
+  int32_t *srt;     // terms_sorted (include/mraft.h MRAFT_TERMS_SORTED): the terms after the dummy never decrease
   int32_t G, P, L;
 };
 
@@ -184,6 +185,19 @@ __device__ __forceinline__ void wave_copy_from_ring(const int32_t *__restrict__ 
       if (k < cnt) dst[k] = v[u];
     }
   }
+}
+
+// Whether the terms of Index [lo, hi] of a ring row (dummy `base` at `head`)
+// never decrease (wave-cooperative; terms_sorted, include/mraft.h). Not on a
+// hot path: load_state and restore only.
+__device__ __forceinline__ bool wave_terms_sorted(const int32_t *__restrict__ row, int base, int head, int L,
+                                                  int lo, int hi) {
+  for (int b = lo; b < hi; b += kWave) {
+    const int idx = b + lane_id();
+    const bool bad = idx < hi && row[ring(idx - base + head, L)] > row[ring(idx + 1 - base + head, L)];
+    if (__ballot(bad)) return false;
+  }
+  return true;
 }
 
 __device__ __forceinline__ int shfl_i(int v, int src) { return __shfl(v, src, 64); }

@@ -15,6 +15,7 @@ void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned lo
                                  hipStream_t st);
 
 void launch_init_state(const Dev &s, hipStream_t st);
+void launch_terms_sorted(const Dev &s, hipStream_t st);  // terms_sorted recomputed from the logs
 
 // Duplicate-slot claims: item i (slot read at byte offset slot_off of a record
 // of `stride` bytes; or, with seg_begin, the slot of segment i's first item)

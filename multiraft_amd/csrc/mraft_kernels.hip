@@ -28,6 +28,7 @@ __global__ void k_init_state(Dev s) {
     // commitIndex = lastApplied = dummyIndex.
     s.term[i] = 0; s.voted[i] = -1; s.role[i] = kFollower; s.commit[i] = 0; s.applied[i] = 0;
     s.dummy[i] = 0; s.last[i] = 0; s.votes[i] = 0; s.head[i] = 0; s.hsnap[i] = 0;
+    s.srt[i] = 1;  // [dummy] only: nothing after the dummy to be out of order
     if (s.pdirty) s.pdirty[i] = 0;
   }
 }
@@ -112,6 +113,7 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
     // check does not gate the loads: one dependent round trip fewer)
     const int role = s.role[slot], dummy = s.dummy[slot], last = s.last[slot], head = s.head[slot];
     const int nxt = s.next[(int64_t)slot * P + peer], term = s.term[slot], commit = s.commit[slot];
+    const int srt = s.srt[slot];
     const int prev = nxt - 1;                                          // :26
     if (role != kLeader) e = MRAFT_ITEM_BAD_STATE;                     // raft_append_entry.go:22-25
     else if (prev < dummy) e = MRAFT_ITEM_NEED_SNAPSHOT;               // :27
@@ -123,6 +125,11 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
       a.prev_log_index = prev;
       a.prev_log_term = s.log[(int64_t)slot * L + ring(prev - dummy + head, L)];  // :49
       a.n_entries = last - prev;                                       // :50
+      // prevLogTerm, entries: non-decreasing when the leader's terms after its
+      // dummy are; prevLogTerm at the dummy itself is compared explicitly
+      a.flags = (srt && (prev > dummy || prev == last ||
+                         a.prev_log_term <= s.log[(int64_t)slot * L + ring(prev + 1 - dummy + head, L)]))
+                    ? MRAFT_AE_ENTRIES_SORTED : 0;
       a.leader_commit = commit;                                        // :51
       a.entries_offset = (int64_t)slot * L + (prev + 1 - dummy);       // :54 (by reference: logical)
     }
@@ -393,7 +400,7 @@ __device__ __forceinline__ HsArgs reload_hs() {
   k.s.term = kp->s.term; k.s.voted = kp->s.voted; k.s.role = kp->s.role; k.s.commit = kp->s.commit;
   k.s.applied = kp->s.applied; k.s.dummy = kp->s.dummy; k.s.last = kp->s.last; k.s.votes = kp->s.votes;
   k.s.log = kp->s.log; k.s.match = kp->s.match; k.s.next = kp->s.next; k.s.pdirty = kp->s.pdirty;
-  k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
+  k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.srt = kp->s.srt; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
   k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
   k.n_stage = kp->n_stage; k.soff = kp->soff; k.sets = kp->sets; k.n_sets = kp->n_sets;
   k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err; k.host_total = kp->host_total; k.seq = kp->seq;
@@ -483,8 +490,11 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   // :146-155 through the streaming pass the tick uses: compare entries with
   // every merging follower's terms, truncate-and-append from the first
   // mismatch. All messages of a set end at the same Index (AeKey).
-  int newlast = -1, fcommit_new = -1;
+  int newlast = -1, fcommit_new = -1, srt_new = -1;
   const int merge_m = (int)(__ballot(cls == AE_MERGE) & ((1ull << NI) - 1));
+  // terms_sorted after an append from Index k (include/mraft.h): the args'
+  // flag when k - 1 is the dummy, cleared without it, else unchanged
+  int shint = (a.flags & MRAFT_AE_ENTRIES_SORTED) ? fdummy + 1 : -1;
   if (merge_m) {
     Fol<NI, true> fo;
     fo.log = s.log;
@@ -545,11 +555,12 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     // (plain LDS stores and loads across a compiler memory barrier: a
     // volatile generic pointer made them flat accesses with 64-bit addresses
     // the compiler hoisted and spilled)
-    __shared__ int stash[11][64];
+    __shared__ int stash[12][64];
     stash[0][lane] = cls; stash[1][lane] = f; stash[2][lane] = fterm; stash[3][lane] = flast;
     stash[4][lane] = fc; stash[5][lane] = a.term; stash[6][lane] = a.leader_commit;
     stash[7][lane] = r.conflict_index; stash[8][lane] = r.term;
     stash[9][lane] = (int)(uint32_t)(uint64_t)i; stash[10][lane] = (int)((uint64_t)i >> 32);
+    stash[11][lane] = shint;
     asm volatile("" ::: "memory");
 #endif
     if (vec) {
@@ -571,6 +582,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     fc = stash[4][lane]; a.term = stash[5][lane]; a.leader_commit = stash[6][lane];
     r.conflict_index = stash[7][lane]; r.term = stash[8][lane];
     i = (int64_t)(((uint64_t)(uint32_t)stash[10][lane] << 32) | (uint32_t)stash[9][lane]);
+    shint = stash[11][lane];
 #endif
 #if MRAFT_AE_RELOAD
     const HsArgs kr = reload_hs();
@@ -589,7 +601,10 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
         rep[i] = r;
       } else {
         int last_after = flast;
-        if (fo.cfrom[q] > 0) newlast = last_after = phi;               // truncated and appended
+        if (fo.cfrom[q] > 0) {                                         // truncated and appended
+          newlast = last_after = phi;
+          srt_new = shint < 0 ? 0 : (fo.cfrom[q] == shint ? 1 : -1);
+        }
         if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160
         r.term = a.term; r.success = 1;                                // :161
       }
@@ -617,6 +632,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     if (a.term > fterm) { s2.term[f] = a.term; s2.voted[f] = -1; }    // :116-118
     s2.role[f] = kFollower;                                            // :120
     if (newlast >= 0) s2.last[f] = newlast;
+    if (srt_new >= 0) s2.srt[f] = srt_new;
     if (fcommit_new >= 0) s2.commit[f] = fcommit_new;
     mark_persist_ae(s2, f, MRAFT_PERSIST_STATE);                       // deferred :111
     rep2[i] = r;
@@ -821,6 +837,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   else if (lane == 19) src = s.last;
   else if (lane == 20) src = s.dummy;
   else if (lane == 21) src = s.head;
+  else if (lane == 22) src = s.srt;
   const int vs = (src && !bad) ? src[si] : 0;
   // items addressed to one replica slot in several segments: the lowest
   // segment wins (k_claim_zero's atomicMax on the inverted index), the others
@@ -831,7 +848,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
   int term = __builtin_amdgcn_readlane(vs, 16), role = __builtin_amdgcn_readlane(vs, 17),
       commit = __builtin_amdgcn_readlane(vs, 18);
   const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20),
-            head = __builtin_amdgcn_readlane(vs, 21);
+            head = __builtin_amdgcn_readlane(vs, 21), srt = __builtin_amdgcn_readlane(vs, 22);
   FOLD_STAMP(2, term + role + commit + last + dummy);
   for (int64_t base = 0; base < cnt; base += 64) {
     const int64_t i = base + lane;
@@ -898,9 +915,15 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
     const unsigned long long rm = __ballot(plo <= phi);  // replies whose evaluation has a range
     if (MRAFT_FOLD_SPLIT) {
-      // probes here, scans in k_fold_scan (as fold_group4)
-      if (MRAFT_FOLD_PROBE && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
-      if (plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
+      // probes here, scans in k_fold_scan (as fold_group4); with sorted terms
+      // a top term below currentTerm settles the range (include/mraft.h)
+      bool settled = false;
+      if (MRAFT_FOLD_PROBE && plo <= phi) {
+        const int pv = lrow[ring(phi - dummy + head, s.L)];
+        if (pv == t0) x = phi;                                           // :98
+        else settled = srt && pv < t0;
+      }
+      if (plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled) {
         pend[2 * (b + base + lane)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
         pend[2 * (b + base + lane) + 1] = make_int4(dummy, head, 0, 0);
         pmark[b + base + lane] = 1;
@@ -914,8 +937,13 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);
       if (lane == src && r >= lo) x = r;
     } else {
-      if (plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0) x = phi;  // :98
-      unsigned long long pend = __ballot(plo < phi && x < 0);
+      bool settled = false;
+      if (plo <= phi) {
+        const int pv = lrow[ring(phi - dummy + head, s.L)];
+        if (pv == t0) x = phi;                                           // :98
+        else settled = srt && pv < t0;
+      }
+      unsigned long long pend = __ballot(plo < phi && x < 0 && !settled);
       while (pend) {
         const int src = first_lane(pend);
         pend &= pend - 1;
@@ -1013,7 +1041,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
                                             int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
   constexpr int NG = 64 / GW;
-  static_assert(GW >= P && GW >= 6, "a group holds the replica's match / next rows and six scalars");
+  static_assert(GW >= P && GW >= 7, "a group holds the replica's match / next rows and seven scalars");
   const int lane = lane_id(), gl = lane & (GW - 1);
   const int64_t sg = sg0 + lane / GW;
   const bool live = sg < n_seg;
@@ -1046,7 +1074,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
       vn = s.next[mrow + gl];
     }
     const int32_t *src = gl == 0 ? s.term : gl == 1 ? s.role : gl == 2 ? s.commit : gl == 3 ? s.last
-                         : gl == 4 ? s.dummy : gl == 5 ? s.head : nullptr;
+                         : gl == 4 ? s.dummy : gl == 5 ? s.head : gl == 6 ? s.srt : nullptr;
     if (src) vb = src[slot];
   }
   // a slot claimed by an earlier segment of the batch: rejected (k_fold's check)
@@ -1055,6 +1083,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     bad = MRAFT_ITEM_DUP_SLOT;
   int term = gw_bcast<GW>(vb, 0), role = gw_bcast<GW>(vb, 1), commit = gw_bcast<GW>(vb, 2);
   const int last = gw_bcast<GW>(vb, 3), dummy = gw_bcast<GW>(vb, 4), head = gw_bcast<GW>(vb, 5);
+  const int srt = gw_bcast<GW>(vb, 6);
   if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)))
     bad = MRAFT_ITEM_BAD_SLOT;
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
@@ -1112,16 +1141,22 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     }
   }
   // a1's ranges of each group: every top word probed at once, the others scanned
+  // With sorted terms (include/mraft.h MRAFT_TERMS_SORTED) a top term below
+  // currentTerm settles the range: no lower entry carries currentTerm.
   int x = -1;
-  if ((MRAFT_FOLD_PROBE || !MRAFT_FOLD_SPLIT) && go && plo <= phi && lrow[ring(phi - dummy + head, s.L)] == t0)
-    x = phi;  // :98
+  bool settled = false;
+  if ((MRAFT_FOLD_PROBE || !MRAFT_FOLD_SPLIT) && go && plo <= phi) {
+    const int pv = lrow[ring(phi - dummy + head, s.L)];
+    if (pv == t0) x = phi;  // :98
+    else settled = srt && pv < t0;
+  }
   if (MRAFT_FOLD_SPLIT) {
     // the ranges whose top word differs are scanned by k_fold_scan, after this
     // launch: it ORs MRAFT_F_COMMITTED into the reply's flags and raises the
     // replica's commitIndex to the highest index it finds (the ranges of a
     // segment are disjoint and ascending, so "the latest range that found
     // one" is the maximum over all of them, probes included)
-    if (go && plo + MRAFT_FOLD_PROBE <= phi && x < 0) {
+    if (go && plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled) {
       pend[2 * (b + gl)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
       pend[2 * (b + gl) + 1] = make_int4(dummy, head, 0, 0);
       pmark[b + gl] = 1;
@@ -1130,7 +1165,8 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   // the ranges whose top word differs, of all four groups, one after another
   // with the whole wave (a 16-lane scan moves a quarter of the terms per round
   // trip and measured 33 % slower over the call)
-  for (unsigned long long pw = MRAFT_FOLD_SPLIT ? 0ull : __ballot(go && plo < phi && x < 0); pw; pw &= pw - 1) {
+  for (unsigned long long pw = MRAFT_FOLD_SPLIT ? 0ull : __ballot(go && plo < phi && x < 0 && !settled); pw;
+       pw &= pw - 1) {
     const int src = first_lane(pw);
     const int lo = __builtin_amdgcn_readlane(plo, src), hi = __builtin_amdgcn_readlane(phi, src) - 1;
     const int sslot = __builtin_amdgcn_readlane(slot, src), sd = __builtin_amdgcn_readlane(dummy, src),
@@ -1199,6 +1235,8 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
       if ((int64_t)last + k - dummy > (int64_t)s.L - 1) {
         err[i] = MRAFT_ITEM_LOG_FULL;
       } else {
+        // terms_sorted: k entries of currentTerm after the last one
+        if (last > dummy && s.log[(int64_t)sl * s.L + ring(last - dummy + h, s.L)] > t) s.srt[sl] = 0;
         for (int j = 1; j <= k; ++j) s.log[(int64_t)sl * s.L + ring(last + j - dummy + h, s.L)] = t;  // :96-100
         s.last[sl] = last + k;
         mark_persist(s, sl, MRAFT_PERSIST_STATE);                      // :101
@@ -1382,8 +1420,8 @@ __global__ __launch_bounds__(256) void k_handle_is(Dev s, const mraft_is_args *_
     // :35-37 a new log [dummy] keeps its head; :38-40 sliceFrom moves it
     const int nh = lii > flast ? fh : ring(fh + (lii - fd), s.L);
     s.log[(int64_t)f * s.L + nh] = a.last_included_term;               // :44-45
-    if (lii > flast) s.last[f] = lii;
-    else s.head[f] = nh;
+    if (lii > flast) { s.last[f] = lii; s.srt[f] = 1; }                // [dummy] only
+    else s.head[f] = nh;                                               // a suffix: terms_sorted unchanged
     s.hsnap[f] = 1;                                                    // :52 hasSnapshot
     s.dummy[f] = lii;
     s.commit[f] = lii;                                                 // :42
@@ -1600,7 +1638,9 @@ __global__ __launch_bounds__(256) void k_restore(Dev s, const mraft_persistent *
   const mraft_persistent r = in[i];
   const int64_t sl = r.slot;
   wave_copy(terms + r.terms_offset, s.log + sl * s.L, r.last_index - r.dummy_index + 1);  // :233
+  const bool srt = wave_terms_sorted(terms + r.terms_offset, 0, 0, INT32_MAX, 1, r.last_index - r.dummy_index);
   if (lane_id() == 0) {
+    s.srt[sl] = srt ? 1 : 0;
     s.term[sl] = r.current_term;                                       // :231
     s.voted[sl] = r.voted_for;                                         // :232
     s.role[sl] = kFollower;                                            // :58
@@ -1619,6 +1659,17 @@ __global__ __launch_bounds__(256) void k_restore(Dev s, const mraft_persistent *
   }
 }
 
+// terms_sorted of every replica from its log (mraft_load_state): wave per slot.
+__global__ __launch_bounds__(256) void k_terms_sorted(Dev s) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  for (int64_t sl = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; sl < gp;
+       sl += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int d = s.dummy[sl], last = s.last[sl], h = s.head[sl];
+    const bool ok = last - d < s.L && wave_terms_sorted(s.log + sl * s.L, d, h, s.L, d + 1, last);
+    if (lane_id() == 0) s.srt[sl] = ok ? 1 : 0;
+  }
+}
+
 // ---------------------------------------------------------------- GetState
 __global__ void k_export(Dev s, const int32_t *__restrict__ lpeer, int32_t *__restrict__ commit,
                          int32_t *__restrict__ term_leader) {
@@ -1632,6 +1683,13 @@ __global__ void k_export(Dev s, const int32_t *__restrict__ lpeer, int32_t *__re
 }
 
 }  // namespace
+
+void launch_terms_sorted(const Dev &s, hipStream_t st) {
+  const int64_t gp = (int64_t)s.G * s.P;
+  int blocks = blocks_for(gp * 64);
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(k_terms_sorted, dim3(blocks), dim3(kBlock), 0, st, s);
+}
 
 void launch_init_state(const Dev &s, hipStream_t st) {
   const int64_t gp = (int64_t)s.G * s.P;

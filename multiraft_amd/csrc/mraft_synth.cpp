@@ -41,6 +41,14 @@ int32_t quorum_match(const int32_t *m, int32_t P, int32_t lp) {
   return v[(size_t)h - 1];
 }
 
+// terms_sorted (include/mraft.h) of a replica whose ring starts at 0: the
+// terms of Index dummy+1 .. last never decrease.
+int32_t sorted_after_dummy(const int32_t *row, int32_t dummy, int32_t last) {
+  for (int32_t i = 1; i < last - dummy; ++i)
+    if (row[i] > row[i + 1]) return 0;
+  return 1;
+}
+
 void gen_group(uint64_t seed, int32_t g, int32_t gl, int32_t P, int32_t L,
                const mraft_soa *st, int32_t *leader_peer, int32_t *item_class) {
   Rng rng(seed, (uint64_t)g);
@@ -168,6 +176,10 @@ void gen_group(uint64_t seed, int32_t g, int32_t gl, int32_t P, int32_t L,
     std::memset(st->match_index + f * P, 0, sizeof(int32_t) * (size_t)P);
     std::memset(st->next_index + f * P, 0, sizeof(int32_t) * (size_t)P);
   }
+  if (st->terms_sorted)
+    for (int32_t p = 0; p < P; ++p)
+      st->terms_sorted[sb + p] =
+          sorted_after_dummy(st->log_term + (sb + p) * L, st->dummy_index[sb + p], st->last_index[sb + p]);
 }
 
 }  // namespace
@@ -274,6 +286,7 @@ extern "C" int mraft_synth_election_state(uint64_t seed, int32_t G, int32_t P, i
         row[0] = 0;
         for (int32_t k = 1; k <= last; ++k) row[k] = std::max(1, lt - (last - k) / 2);
         for (int32_t k = last + 1; k < L; ++k) row[k] = 0;
+        if (st->terms_sorted) st->terms_sorted[s] = sorted_after_dummy(row, 0, last);
         std::memset(st->match_index + s * P, 0, sizeof(int32_t) * (size_t)P);
         std::memset(st->next_index + s * P, 0, sizeof(int32_t) * (size_t)P);
       }

@@ -95,7 +95,7 @@ __device__ __forceinline__ Dev reload_dev() {
   d.term = kp->term; d.voted = kp->voted; d.role = kp->role; d.commit = kp->commit;
   d.applied = kp->applied; d.dummy = kp->dummy; d.last = kp->last; d.votes = kp->votes;
   d.log = kp->log; d.match = kp->match; d.next = kp->next; d.pdirty = kp->pdirty;
-  d.head = kp->head; d.hsnap = kp->hsnap; d.G = kp->G; d.P = kp->P; d.L = kp->L;
+  d.head = kp->head; d.hsnap = kp->hsnap; d.srt = kp->srt; d.G = kp->G; d.P = kp->P; d.L = kp->L;
   return d;
 }
 
@@ -278,7 +278,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const long long lrow = ld * L;
   // Every load that depends only on the leader index, issued together.
   const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
-            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]), lhead = uni(s.head[ld]);
+            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]), lhead = uni(s.head[ld]),
+            lsrt = uni(s.srt[ld]);
   const int lb = lhead - ldummy;  // leader Index i at lrow + ring(i + lb): the log ring
   int mm[P];
 #pragma unroll
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
     return;
   }
-  hR = 5 + NI;
+  hR = 6 + NI;  // role, term, commit, last, dummy, terms_sorted, nextIndex[q]
 
   // ------------------------------------------------------------ phase A
   int icls = IC_NONE;
@@ -454,6 +455,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // commit scan of a Figure-8 group rides along the same streaming pass.
   Fold<P, COUNT> fd;
   int commit = c0, top = 0, slo = 1, shi = 0;
+  int settled = 0;  // a1 decided by its top term alone (sorted terms, include/mraft.h)
   const int is_m = (int)__ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
   const int have0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
   const int succ0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
@@ -464,6 +466,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       if (top > c0) {
         const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
         if (t == T) commit = top;
+        else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
         else { slo = c0 + 1; shi = top - 1; }
       }
     }
@@ -517,8 +520,11 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        if (uni(s2.log[lrow + ring(top + lb, L)]) == T) {
+        const int t = uni(s2.log[lrow + ring(top + lb, L)]);
+        if (t == T) {
           commit = top;
+        } else if (uni(s2.srt[ld]) && t < T) {
+          settled = 1;
         } else {
           const int i = wave_scan_down_eq(s2.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
           if (i > c0) commit = i;
@@ -553,6 +559,18 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
             newlast = prev + n;
             if (!COUNT) s2.last[f] = newlast;
             cW += (n - mk) + 1;
+            // terms_sorted after appending from Index prev+1+mk: the args'
+            // flag (prevLogTerm, entries sorted: the leader's proof, with the
+            // dummy's term compared explicitly), or the new entries are the
+            // whole log when that Index is the dummy's successor
+            bool fl = s2.srt[ld] != 0;
+            if (fl && prev == ldummy)
+              fl = s2.log[lrow + ring(prev + lb, L)] <= s2.log[lrow + ring(prev + 1 + lb, L)];
+            const int sw = !fl ? 0 : (mk == 0 && prev == s2.dummy[f]) ? 1 : -1;
+            if (sw >= 0) {
+              if (!COUNT) s2.srt[f] = sw;
+              cW += 1;
+            }
           }
         }
         cR += 1;                                                         // :157-160
@@ -585,8 +603,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         const int fh = s2.head[f], nh = newlog ? fh : ring(fh + (ldummy - s2.dummy[f]), L);
         if (!COUNT) {
           s2.log[f * L + nh] = lit;                                       // :44-45 dummy term
-          if (newlog) s2.last[f] = ldummy;
-          else s2.head[f] = nh;
+          if (newlog) { s2.last[f] = ldummy; s2.srt[f] = 1; }           // [dummy] only: sorted
+          else s2.head[f] = nh;                                           // a suffix: unchanged
           s2.hsnap[f] = 1;                                                // raft_snapshot.go:52 hasSnapshot
           s2.dummy[f] = ldummy;
           s2.commit[f] = ldummy;                                          // :42
@@ -595,7 +613,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         cR += 1;                                                         // last
         cW += 3;
         if (newlog) {
-          cW += 2;                                                       // dummy term, last
+          cW += 3;                                                       // dummy term, last, terms_sorted
         } else {
           cR += 1;                                                       // dummy
           cW += 1;                                                       // dummy term
@@ -647,7 +665,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     long long a1lo = 1, a1hi = 0;
     if (fd.any && top > c0) {
       a1hi = top;
-      a1lo = (commit != c0) ? commit : c0 + 1;
+      a1lo = (commit != c0) ? commit : settled ? top : c0 + 1;
     }
     long long u = interval_len(A, last) + interval_len(a1lo, a1hi);
     u -= interval_len(max(A, a1lo), min((long long)last, a1hi));

@@ -39,6 +39,7 @@ def new_state(G: int, P: int, L: int) -> dict:
     st = {f: np.zeros(n, dtype=np.int32) for f, n in state_sizes(G, P, L).items()}
     st["voted_for"][:] = -1
     st["state"][:] = _abi.FOLLOWER
+    st["terms_sorted"][:] = 1  # [dummy] only
     return st
 
 
@@ -157,8 +158,8 @@ class Engine:
 
     # ---- state -----------------------------------------------------------
     def load_state(self, st: dict, where: int = HOST):
-        if where == HOST:  # images made before the ring / hasSnapshot: head 0, no snapshot pending
-            for f in ("log_head", "has_snapshot"):
+        if where == HOST:  # images made before the ring / hasSnapshot / terms_sorted (recomputed on load)
+            for f in ("log_head", "has_snapshot", "terms_sorted"):
                 if f not in st:
                     st = dict(st, **{f: np.zeros(self.G * self.P, np.int32)})
         soa = soa_of(st)

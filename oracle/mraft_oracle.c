@@ -23,7 +23,7 @@
 /* ------------------------------------------------------------------------ */
 
 enum { A_TERM, A_VOTED, A_ROLE, A_COMMIT, A_APPLIED, A_DUMMY, A_LAST, A_VOTES,
-       A_LOG, A_MATCH, A_NEXT, A_COUNT };
+       A_LOG, A_MATCH, A_NEXT, A_SORTED, A_COUNT };
 
 static struct {
   int on;
@@ -34,7 +34,7 @@ static struct {
 int ora_count_enable(ora_engine *e) {
   int64_t gp = (int64_t)e->G * e->P;
   int64_t sizes[A_COUNT] = {gp, gp, gp, gp, gp, gp, gp, gp,
-                            gp * e->L, gp * e->P, gp * e->P};
+                            gp * e->L, gp * e->P, gp * e->P, gp};
   int64_t b = 0;
   for (int a = 0; a < A_COUNT; ++a) { cnt.base[a] = b; b += sizes[a]; }
   cnt.base[A_COUNT] = b;
@@ -107,6 +107,24 @@ static void copy_terms(const ora_engine *e, int64_t slot, int32_t index, int32_t
 
 static inline int32_t imin(int32_t a, int32_t b) { return a < b ? a : b; } /* utility.go:41-46 */
 
+/* terms_sorted (include/mraft.h MRAFT_TERMS_SORTED; engine bookkeeping, not a
+ * Go field): whether the terms of Index dummy+1 .. last never decrease. The
+ * oracle keeps it with the engine's rules (Make 1, load / restore computed,
+ * Start, the AppendEntries append, InstallSnapshot's new log) so the states
+ * compare equal; its own a1 (advance_commit) is Go's loop and never reads it. */
+static int32_t sorted_after_dummy(const ora_engine *e, int64_t slot) {
+  const int32_t d = S.dummy_index[slot], last = S.last_index[slot];
+  for (int32_t i = d + 1; i < last; ++i)
+    if (term_at(e, slot, i) > term_at(e, slot, i + 1)) return 0;
+  return 1;
+}
+
+void ora_compute_terms_sorted(ora_engine *e) {
+  const int64_t gp = (int64_t)e->G * e->P;
+  for (int64_t s = 0; s < gp; ++s)
+    S.terms_sorted[s] = (S.last_index[s] - S.dummy_index[s] < e->L) ? sorted_after_dummy(e, s) : 0;
+}
+
 /* Duplicate-slot claim: lowest item index wins (include/mraft.h). */
 static int32_t *claim_slots(ora_engine *e, const int32_t *slot_of, int64_t n,
                             size_t stride_bytes, int32_t *item_err) {
@@ -142,7 +160,11 @@ static int32_t gather_one(ora_engine *e, int32_t slot, int32_t peer,
   a->prev_log_term = term_at(e, slot, prev);                           /* :49 */
   a->n_entries = S.last_index[slot] - prev;                            /* :50 */
   a->leader_commit = S.commit_index[slot];                             /* :51 */
-  a->_pad = 0;
+  /* flags: prevLogTerm, entries non-decreasing (the leader's terms_sorted,
+   * the dummy's own term compared explicitly) */
+  a->flags = (S.terms_sorted[slot] && (prev > S.dummy_index[slot] || prev == S.last_index[slot] ||
+                                       a->prev_log_term <= term_at(e, slot, prev + 1)))
+                 ? MRAFT_AE_ENTRIES_SORTED : 0;
   a->entries_offset = (int64_t)slot * e->L + (prev + 1 - S.dummy_index[slot]); /* :54 */
   return MRAFT_ITEM_OK;
 }
@@ -253,6 +275,10 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
       }
       S.last_index[f] = prev + n;
       CW(A_LAST, f);
+      /* terms_sorted: the args' flag; the new entries are the whole log when
+       * the first appended Index is the dummy's successor */
+      if (!(a->flags & MRAFT_AE_ENTRIES_SORTED)) { S.terms_sorted[f] = 0; CW(A_SORTED, f); }
+      else if (index == dummy + 1) { S.terms_sorted[f] = 1; CW(A_SORTED, f); }
       break;
     }
   }
@@ -536,7 +562,8 @@ static int32_t handle_is_one(ora_engine *e, int32_t f, const mraft_is_args *a, m
     S.log_term[at] = a->last_included_term;
     S.last_index[f] = lii;
     S.dummy_index[f] = lii;
-    CW(A_LOG, at); CW(A_LAST, f);
+    S.terms_sorted[f] = 1;                                            /* [dummy] only */
+    CW(A_LOG, at); CW(A_LAST, f); CW(A_SORTED, f);
   } else {                                                            /* :38-40 */
     CR(A_DUMMY, f);
     slice_from(e, f, lii);                                            /* O(1) ring rebase */
@@ -637,6 +664,7 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
     if (group_flags) group_flags[g] = MRAFT_G_ERROR;
     return;
   }
+  CR(A_SORTED, ld);
   int32_t ok[8] = {0};  /* 1: AppendEntries, 2: InstallSnapshot */
   for (int32_t p = 0; p < P; ++p) {
     if (p == lp) continue;
@@ -718,6 +746,8 @@ static void tick_group(ora_engine *e, const int32_t *leader_peer,
     for (int32_t i = top; i > commit0; --i) {
       CR(A_LOG, lpos(e, ld, i));
       if (term_at(e, ld, i) == term0) break;
+      /* sorted terms: a top term below currentTerm settles it */
+      if (i == top && S.terms_sorted[ld] && term_at(e, ld, i) < term0) break;
     }
   }
   if (group_flags) group_flags[g] = flags;
@@ -786,6 +816,7 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
     if (S.state[s] != MRAFT_LEADER) continue;                         /* :93-95 */
     int32_t last = S.last_index[s], dummy = S.dummy_index[s];
     if ((int64_t)last + k - dummy > (int64_t)e->L - 1) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
+    if (last > dummy && term_at(e, s, last) > S.current_term[s]) S.terms_sorted[s] = 0;
     for (int32_t j = 1; j <= k; ++j)                                  /* :96-100 */
       S.log_term[lpos(e, s, last + j)] = S.current_term[s];
     S.last_index[s] = last + k;
@@ -1093,6 +1124,7 @@ int ora_restore(ora_engine *e, const mraft_persistent *in, int64_t n, const int3
     S.has_snapshot[s] = 0;                                            /* Make: no snapshot pending */
     S.dummy_index[s] = r->dummy_index;
     S.last_index[s] = r->last_index;
+    S.terms_sorted[s] = sorted_after_dummy(e, s);
     S.commit_index[s] = r->dummy_index;                               /* :79 */
     S.last_applied[s] = r->dummy_index;                               /* :80 */
     S.granted_votes[s] = 0;

@@ -35,6 +35,8 @@ typedef struct {
 /* Algorithmic word counting. When enabled, the tick marks every
  * state word the minimal exact algorithm must read / write in two bitmaps. */
 int ora_count_enable(ora_engine *e);
+/* terms_sorted of every replica from its log (what mraft_load_state does). */
+void ora_compute_terms_sorted(ora_engine *e);
 void ora_count_disable(void);
 void ora_count_result(int64_t out_words[2]);
 

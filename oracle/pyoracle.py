@@ -385,7 +385,7 @@ def to_soa(rafts: List[Raft], st: dict, G: int, P: int, L: int) -> dict:
     their previous contents, like the device arrays). The object model has no
     ring: each log is written from the replica's existing log_head, so the
     result equals the engine's logically (tests compare logical logs)."""
-    out = {k: np.array(v, copy=True) for k, v in st.items()}
+    out = {k: np.array(v, copy=True) for k, v in st.items() if k != "terms_sorted"}  # engine bookkeeping
     for s, rf in enumerate(rafts):
         out["current_term"][s] = rf.currentTerm
         out["voted_for"][s] = rf.votedFor

@@ -31,6 +31,7 @@ def lib():
         E = ctypes.POINTER(OraEngine)
         sigs = {
             "ora_count_enable": [E], "ora_count_disable": [], "ora_count_result": [vp],
+            "ora_compute_terms_sorted": [E],
             "ora_gather_append_args": [E, vp, vp, i64, vp, vp],
             "ora_handle_append_entries": [E, vp, i64, vp, i64, vp, vp],
             "ora_process_append_replies": [E, vp, i64, vp, i64, vp, vp],
@@ -61,7 +62,7 @@ def lib():
             f = getattr(l, n)
             f.argtypes = a
             f.restype = None if n in ("ora_count_disable", "ora_count_result", "goshape_store",
-                                      "goshape_free", "goshape_reset") else ctypes.c_int
+                                      "goshape_free", "goshape_reset", "ora_compute_terms_sorted") else ctypes.c_int
         l.goshape_build.restype = ctypes.c_void_p
         l.goshape_tick.restype = ctypes.c_int64
         _lib = l
@@ -77,7 +78,9 @@ class Oracle:
         self.st = copy_state(st)
         self.st.setdefault("log_head", np.zeros(G * P, np.int32))  # fixtures made before the ring
         self.st.setdefault("has_snapshot", np.zeros(G * P, np.int32))
+        self.st["terms_sorted"] = np.zeros(G * P, np.int32)
         self._e = OraEngine(G, P, L, soa_of(self.st))
+        lib().ora_compute_terms_sorted(ctypes.byref(self._e))  # as mraft_load_state does
 
     def state(self) -> dict:
         return self.st
@@ -272,6 +275,8 @@ def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = "",
     live entries [dummy, last] of every replica (slots past lastIndex are dead:
     the reference's slice has no such slots). heads=False skips the ring
     positions themselves (the Python restatement has no ring)."""
+    for st in (a, b):
+        assert_terms_sorted_sound(st, G, P, L, ctx)
     for k in a:
         if k == "log_term" or (k == "log_head" and not heads) or k not in b:
             continue
@@ -285,6 +290,26 @@ def assert_states_equal(a: dict, b: dict, G: int, P: int, L: int, ctx: str = "",
     if not np.array_equal(np.where(mask, la, 0), np.where(mask, lb, 0)):
         rows = np.nonzero((np.where(mask, la, 0) != np.where(mask, lb, 0)).any(axis=1))[0][:8]
         raise AssertionError(f"{ctx}: log_term differs in replicas {rows}")
+
+
+def terms_sorted_exact(st: dict, G: int, P: int, L: int) -> np.ndarray:
+    """Whether each replica's terms of Index dummy+1 .. last never decrease."""
+    logs = logical_logs(st, G, P, L).astype(np.int64)
+    live = (st["last_index"] - st["dummy_index"]).astype(np.int64)  # entries after the dummy
+    k = np.arange(1, L)[None, :]
+    desc = (logs[:, 1:-1] > logs[:, 2:]) if L > 2 else np.zeros((G * P, 0), bool)
+    desc = desc & (k[:, :-1] < live[:, None]) if L > 2 else desc
+    return (~desc.any(axis=1)).astype(np.int32)
+
+
+def assert_terms_sorted_sound(st: dict, G: int, P: int, L: int, ctx: str = ""):
+    """terms_sorted is a proof (include/mraft.h): 1 only where the terms after
+    the dummy really never decrease."""
+    if "terms_sorted" not in st:
+        return
+    bad = np.nonzero((st["terms_sorted"] != 0) & (terms_sorted_exact(st, G, P, L) == 0))[0]
+    if len(bad):
+        raise AssertionError(f"{ctx}: terms_sorted claims sorted terms in replicas {bad[:8]}")
 
 
 def rotate_rings(st: dict, G: int, P: int, L: int, rng, frac: float = 1.0) -> dict:

@@ -36,7 +36,7 @@ def test_abi_version_and_struct_sizes():
     assert _abi.AE_ARGS.itemsize == 40
     assert _abi.AE_REPLY.itemsize == 16
     assert _abi.RV_RESULT.itemsize == 20
-    assert ctypes.sizeof(_abi.MraftSoa) == 14 * 8
+    assert ctypes.sizeof(_abi.MraftSoa) == 15 * 8
     assert _abi.PERSISTENT.itemsize == 32
 
 

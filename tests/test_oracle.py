@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "gol
 import pyoracle as po  # noqa: E402
 from kat_runner import kat_state, load_kats, run_kat  # noqa: E402
 from make_golden import check_kat, run_py  # noqa: E402
-from oracle_lib import Oracle, assert_states_equal  # noqa: E402
+from oracle_lib import terms_sorted_exact, Oracle, assert_states_equal  # noqa: E402
 
 from multiraft_amd import synth_fold_batch, synth_tick_state  # noqa: E402
 from multiraft_amd._abi import AE_ARGS, RV_ARGS, RV_RESULT  # noqa: E402
@@ -58,6 +58,12 @@ def test_synth_matches_fixture_inputs():
         for k, v in st.items():
             if k in ("log_head", "has_snapshot") and f"v{i}_in_{k}" not in z.files:
                 assert not v.any()  # fixture made before these arrays: all zero
+                continue
+            if k == "terms_sorted" and f"v{i}_in_{k}" not in z.files:
+                # fixture made before this array: it is the logs' own sortedness
+                fx = {kk: z[f"v{i}_in_{kk}"] for kk in ("log_term", "dummy_index", "last_index")}
+                fx["log_head"] = np.zeros(G * P, np.int32)
+                assert np.array_equal(v, terms_sorted_exact(fx, G, P, L))
                 continue
             assert np.array_equal(v, z[f"v{i}_in_{k}"]), k
 

@@ -51,6 +51,10 @@ def test_many_groups_oracle(names, groups):
     sim = run_many(_oracle, names, groups)
     assert sim.G == groups and not sim.failures
     _batched(sim, groups)
+    # every log a Raft run reaches is sorted, and the engine's rules keep the
+    # proof through appends, Start, snapshots, installs and restarts
+    # (include/mraft.h MRAFT_TERMS_SORTED): a1 never needs Go's downward scan
+    assert (sim.eng.store_state()["terms_sorted"] == 1).all()
 
 
 @pytest.mark.gpu
@@ -59,6 +63,7 @@ def test_many_groups_oracle(names, groups):
 def test_many_groups_gpu(names, groups):
     sim = run_many(_gpu, names, groups, compact_apply=True)
     assert sim.G == groups and not sim.failures
+    assert (sim.eng.store_state()["terms_sorted"] == 1).all()
     calls = _batched(sim, 10 * groups)
     installs = sum(g.installs for g in sim.groups)
     restores = calls.get("restore", [0])[0]

@@ -8,7 +8,8 @@ ring head (5) read; log[prev] (1) when prev lies inside the follower's log;
 the ConflictIndex scan's words; for a merge, the follower's terms compared up
 to the first mismatch and the entries written from there; the state words a
 follower's reply changes (role; term and votedFor on adoption; last on
-truncation; commit when it moves; the persist-flag read-modify-write).
+truncation; terms_sorted when an append changes it (include/mraft.h); commit
+when it moves; the persist-flag read-modify-write).
 Per set (messages reading the same entries): the shared entries once, from
 the lowest compared Index to the highest one any message of the set needs,
 plus the set record (2). raft_append_entry.go:108-162, raft_log.go:92-96."""
@@ -81,6 +82,10 @@ def handle_words(st, args, rep, herr, G, P, L, chunk=2048):
     newlast = np.zeros(len(args), bool)
     newlast[mi[copies]] = True
     words += int(newlast.sum())
+    # terms_sorted after an append from Index m: cleared without the args'
+    # flag, set with it when m - 1 is the dummy (k_handle_set)
+    flag = (args["flags"][mi] & 1) != 0
+    words += int((copies & (~flag | (m == fd[mi] + 1))).sum())
     last_after = np.where(newlast, prev + n, fl)
     words += int((merge & (args["leader_commit"] > fc) & (np.minimum(args["leader_commit"], last_after) >= 0)).sum())
     return {"words": words, "sets": n_sets, "merges": int(merge.sum()), "copied": int(np.where(copies, phi - m + 1, 0).sum())}
@@ -98,18 +103,22 @@ def fold_words(st, res, seg, P, L):
     from the state before the call and the reply records, whatever kernel
     runs it. Per reply: its record (8 words) read, its flag and error word
     written. Per segment (one leader replica): the segment bounds (int64),
-    the replica's term, role, commit, last, dummy and ring head; nextIndex of
-    every replying peer (the gate, :73-74); matchIndex of every peer but the
-    leader's when a1 runs (:91-97); a1's log words: for each evaluation (:78)
-    the terms from min(M*, last) down to the first one equal to currentTerm,
-    or to the highest Index an earlier evaluation of the segment examined
-    (each word read once per segment); written: nextIndex (and matchIndex on
+    the replica's term, role, commit, last, dummy, ring head and
+    terms_sorted; nextIndex of every replying peer (the gate, :73-74);
+    matchIndex of every peer but the leader's when a1 runs (:91-97); a1's log
+    words: for each evaluation (:78) the term of min(M*, last) and, unless it
+    settles the evaluation (it equals currentTerm, or the replica's terms are
+    sorted and it is below currentTerm: include/mraft.h), the terms below it
+    down to the first one equal to currentTerm, or to the highest Index an
+    earlier evaluation of the segment examined (each word read once per
+    segment); written: nextIndex (and matchIndex on
     success) of every reply that passes the gate, commitIndex when it moves,
     term / role / votedFor and the persist flag on a step-down.
     Returns {"words", "a1_log_words", "segments", "evaluations"}."""
     log = st["log_term"].reshape(-1)
     head, dummy, last = st["log_head"], st["dummy_index"], st["last_index"]
     term, role, commit = st["current_term"], st["state"], st["commit_index"]
+    srt = st["terms_sorted"]
     match = st["match_index"].reshape(-1, P)
     nxt = st["next_index"].reshape(-1, P)
     n_seg = len(seg) - 1
@@ -125,7 +134,7 @@ def fold_words(st, res, seg, P, L):
         T, r, c = int(term[s]), int(role[s]), int(commit[s])
         lst, d, h = int(last[s]), int(dummy[s]), int(head[s])
         m, nx = [int(x) for x in match[s]], [int(x) for x in nxt[s]]
-        words += 6 + len(set(int(x) for x in res["peer"][b:e]))
+        words += 7 + len(set(int(x) for x in res["peer"][b:e]))
         t, H, a1 = T, c, False
         wrote = 0
         for i in range(b, e):
@@ -143,10 +152,15 @@ def fold_words(st, res, seg, P, L):
                     evals += 1
                     top = min(_quorum(m, me, P), lst)
                     if top > H:                                   # a1: (H, top], currentTerm = T here
-                        idx = np.arange(H + 1, top + 1)
-                        hit = np.nonzero(log[s * L + (h + idx - d) % L] == T)[0]
-                        k = int(idx[hit[-1]]) if len(hit) else H
-                        a1w += top - max(k, H + 1) + 1
+                        tt = int(log[s * L + (h + top - d) % L])
+                        if tt != T and srt[s] and tt < T:          # settled by the top term
+                            k = H
+                            a1w += 1
+                        else:
+                            idx = np.arange(H + 1, top + 1)
+                            hit = np.nonzero(log[s * L + (h + idx - d) % L] == T)[0]
+                            k = int(idx[hit[-1]]) if len(hit) else H
+                            a1w += top - max(k, H + 1) + 1
                         if k > H:
                             c = k
                         H = top
