@@ -75,101 +75,187 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
-    """The survey's other configurations, measured in the same run so they are
-    on the driver's record (rank 0, one GPU, after the headline's timed
-    region; never part of `value`):
-      * the message-level path at config #3 (gather -> handle by reference ->
-        fold) on a fresh copy per step, with the handler's
-        roofline from its algorithmic bytes (tools/msg_words.py);
-      * config #5, the election storm (65,536 x 7, 64 rounds per launch);
-      * config #2 (1,024 x 3 x 256: cache-resident, launch-bound).
-    Each timed with HIP events on the engine's stream; `copies` are the state
-    copies the headline already used, step i of the message path on copy i
-    restored from `master` (so its steps see both memory populations, like
-    the headline's)."""
+def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
+    """The config #3 message-level path (gather -> HandleAppendEntries by
+    reference -> processAppendEntriesReply + a1) as S shard
+    pipelines: shard s = groups [G*s/S, G*(s+1)/S) of every state copy (SoA
+    slices, no copies), its own engine on a hardware queue of its own
+    (MRAFT_CREATE_DEDICATED_QUEUE) driven by its own host thread — the Go
+    host's goroutine per shard: ctypes releases the GIL in
+    the engine calls, so one shard's host-side waits (the handle call waits
+    for its plan) do not hold the other back. Step i runs on copy i restored
+    from `master`; the warm-up on copy `steps`.
+    S = 1: one event between consecutive calls (the per-call split);
+    S > 1: one event per step on each queue (the device span per step).
+    words=True: the algorithmic words of one batch (tools/msg_words.py) from
+    the warm-up's inputs (S = 1 only)."""
+    import threading
+
     import torch
 
-    from multiraft_amd import DEVICE, Engine, _abi, synth_election_state, synth_seed, synth_tick_state
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from msg_words import fold_words, handle_words
-
-    out = {}
+    from multiraft_amd import DEVICE, Engine, _abi
     lib = _abi.lib()
-
-    def ev():
-        return torch.cuda.Event(enable_timing=True)
 
     def ck(rc, what):
         assert rc == 0, (what, _abi.last_error())
 
-    # -- message-level path, config #3
-    eng = Engine(G, P, L, device=dev.index or 0, alloc=False)
-    eng.set_stream(stream.cuda_stream)
-    ldr = (np.arange(G) * P + lp).repeat(P - 1).astype(np.int32)
-    q = np.tile(np.arange(P - 1), G)
-    peers = np.where(q < np.repeat(lp, P - 1), q, q + 1).astype(np.int32)
-    keep = np.repeat(lp >= 0, P - 1)
-    ldr, peers = ldr[keep], peers[keep]
-    n = len(ldr)
-    slots_d, peers_d = torch.from_numpy(ldr).to(dev), torch.from_numpy(peers).to(dev)
-    args = torch.zeros((n, 10), dtype=torch.int32, device=dev)
-    gerr, herr, ferr, flags = (torch.zeros(n, dtype=torch.int32, device=dev) for _ in range(4))
-    rep = torch.zeros((n, 4), dtype=torch.int32, device=dev)
-    res = torch.zeros((n, 8), dtype=torch.int32, device=dev)
-    seg = torch.from_numpy(np.concatenate([[0], np.cumsum(np.bincount(ldr // P, minlength=G)[lp >= 0])])
-                           .astype(np.int64)).to(dev)
-    t_call = {"gather": [], "handle": [], "fold": []}
-    hw = None
-    for i in range(steps + 1):
-        copy = copies[i % len(copies)]
+    for c in copies[:steps + 1]:
         for k, v in master.items():
-            copy[k].copy_(v)
-        eng.bind(copy)
-        # one event between consecutive calls (each event is a marker packet
-        # on the queue: DESIGN.md §7)
-        e = [ev() for _ in range(5)]
-        e[0].record(stream)
-        ck(lib.mraft_gather_append_args(eng._h, slots_d.data_ptr(), peers_d.data_ptr(), n, args.data_ptr(),
-                                        gerr.data_ptr(), DEVICE), "gather")
-        e[1].record(stream)
-        ck(lib.mraft_handle_append_entries(eng._h, args.data_ptr(), n, None, 0, rep.data_ptr(), herr.data_ptr(),
-                                           DEVICE), "handle")
-        e[2].record(stream)
-        res[:, 0], res[:, 1], res[:, 2], res[:, 3], res[:, 4] = slots_d, peers_d, args[:, 1], args[:, 3], args[:, 6]
-        res[:, 5:8] = rep[:, 0:3]
-        e[3].record(stream)
-        ck(lib.mraft_process_append_replies(eng._h, res.data_ptr(), n, seg.data_ptr(), len(seg) - 1,
-                                            flags.data_ptr(), ferr.data_ptr(), DEVICE), "fold")
-        e[4].record(stream)
-        torch.cuda.synchronize()
-        if i == 0:  # the first pass is warm-up; its inputs give the algorithmic bytes
-            assert int(gerr.abs().sum()) == 0 and int(herr.abs().sum()) == 0 and int(ferr.abs().sum()) == 0
-            host = {k: v.cpu().numpy() for k, v in master.items()}
-            args_h = args.cpu().numpy().view(_abi.AE_ARGS).reshape(-1)
-            hw = handle_words(host, args_h, rep.cpu().numpy().view(_abi.AE_REPLY).reshape(-1), herr.cpu().numpy(),
-                              G, P, L)
-            # the fold reads only leader replicas, which no message of this
-            # batch targets: their pre-handle state is the fold's input
-            res_h = res.cpu().numpy().view(_abi.AE_RESULT).reshape(-1)
-            assert not np.isin(res_h["slot"], args_h["slot"]).any()
-            fw = fold_words(host, res_h, seg.cpu().numpy(), P, L)
-            ld_sl = np.unique(res_h["slot"])
-            assert np.array_equal(fw["commit"][ld_sl], copy["commit_index"].cpu().numpy()[ld_sl]), \
-                "fold word count: replayed commits differ from the device's"
-            del host
-            continue
-        t_call["gather"].append(e[0].elapsed_time(e[1]))
-        t_call["handle"].append(e[1].elapsed_time(e[2]))
-        t_call["fold"].append(e[3].elapsed_time(e[4]))
-    ms = {k: float(np.mean(v)) for k, v in t_call.items()}
-    step_ms = sum(ms.values())
+            c[k].copy_(v)
+    torch.cuda.synchronize()
+    per_group = {k: v.numel() // G for k, v in master.items()}
+    shards = []
+    for si in range(S):
+        g0, g1 = G * si // S, G * (si + 1) // S
+        n_g = g1 - g0
+        e = Engine(n_g, P, L, device=dev.index or 0, alloc=False, dedicated_queue=True)
+        st = torch.cuda.ExternalStream(e.stream(), device=dev)
+        lps = lp[g0:g1]
+        ldr = (np.arange(n_g) * P + lps).repeat(P - 1)
+        q = np.tile(np.arange(P - 1), n_g)
+        peers = np.where(q < np.repeat(lps, P - 1), q, q + 1)
+        keep = np.repeat(lps >= 0, P - 1)
+        ldr, peers = ldr[keep].astype(np.int32), peers[keep].astype(np.int32)
+        n = len(ldr)
+        z = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+        sh = {"eng": e, "st": st, "g": (g0, g1), "n": n,
+              "slots": torch.from_numpy(ldr).to(dev), "peers": torch.from_numpy(peers).to(dev),
+              "args": z(n, 10), "gerr": z(n), "herr": z(n), "ferr": z(n), "flags": z(n), "rep": z(n, 4),
+              "res": z(n, 8),
+              "seg": torch.from_numpy(np.concatenate([[0], np.cumsum(np.bincount(ldr // P, minlength=n_g)[lps >= 0])])
+                                      .astype(np.int64)).to(dev),
+              "views": [{k: v[g0 * per_group[k]:g1 * per_group[k]] for k, v in c.items()} for c in copies[:steps + 1]]}
+        shards.append(sh)
+    torch.cuda.synchronize()
+
+    def run(sh, i, marks):
+        e, st, n, a = sh["eng"], sh["st"], sh["n"], sh["args"]
+        e.bind(sh["views"][i])
+        if marks is not None:
+            marks[0].record(st)
+        ck(lib.mraft_gather_append_args(e._h, sh["slots"].data_ptr(), sh["peers"].data_ptr(), n, a.data_ptr(),
+                                        sh["gerr"].data_ptr(), DEVICE), "gather")
+        if marks is not None and len(marks) > 2:
+            marks[1].record(st)
+        ck(lib.mraft_handle_append_entries(e._h, a.data_ptr(), n, None, 0, sh["rep"].data_ptr(),
+                                           sh["herr"].data_ptr(), DEVICE), "handle")
+        if marks is not None and len(marks) > 2:
+            marks[2].record(st)
+        # the fold's reply records from (args, reply): host glue, one kernel
+        with torch.cuda.stream(st):
+            torch.cat([sh["slots"][:, None], sh["peers"][:, None], a[:, 1:2], a[:, 3:4], a[:, 6:7], sh["rep"][:, 0:3]],
+                      dim=1, out=sh["res"])
+        if marks is not None and len(marks) > 2:
+            marks[3].record(st)
+        ck(lib.mraft_process_append_replies(e._h, sh["res"].data_ptr(), n, sh["seg"].data_ptr(),
+                                            len(sh["seg"]) - 1, sh["flags"].data_ptr(), sh["ferr"].data_ptr(),
+                                            DEVICE), "fold")
+        if marks is not None:
+            marks[-1].record(st)
+
+    out = {}
+    # warm-up (and the algorithmic words) on copy `steps`
+    for sh in shards:
+        run(sh, steps, None)
+    for sh in shards:
+        sh["eng"].synchronize()
+    for sh in shards:
+        assert int(sh["gerr"].abs().sum()) == 0 and int(sh["herr"].abs().sum()) == 0
+        assert int(sh["ferr"].abs().sum()) == 0
+    if words:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from msg_words import fold_words, handle_words
+        sh = shards[0]
+        host = {k: v.cpu().numpy() for k, v in master.items()}
+        args_h = sh["args"].cpu().numpy().view(_abi.AE_ARGS).reshape(-1)
+        hw = handle_words(host, args_h, sh["rep"].cpu().numpy().view(_abi.AE_REPLY).reshape(-1),
+                          sh["herr"].cpu().numpy(), G, P, L)
+        # the fold reads only leader replicas, which no message of this batch
+        # targets: their pre-handle state is the fold's input
+        res_h = sh["res"].cpu().numpy().view(_abi.AE_RESULT).reshape(-1)
+        assert not np.isin(res_h["slot"], args_h["slot"]).any()
+        fw = fold_words(host, res_h, sh["seg"].cpu().numpy(), P, L)
+        ld_sl = np.unique(res_h["slot"])
+        assert np.array_equal(fw["commit"][ld_sl], copies[steps]["commit_index"].cpu().numpy()[ld_sl]), \
+            "fold word count: replayed commits differ from the device's"
+        out["hw"], out["fw"] = hw, fw
+    nm = 5 if S == 1 else 1
+    marks = [[[torch.cuda.Event(enable_timing=True) for _ in range(nm)] for _ in range(steps)] for _ in range(S)]
+    t_begin = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t_begin.record()
+    for sh in shards:
+        sh["st"].wait_event(t_begin)
+
+    def worker(si):
+        for i in range(steps):
+            run(shards[si], i, marks[si][i])
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=worker, args=(si,)) for si in range(S)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for sh in shards:
+        sh["eng"].synchronize()
+    torch.cuda.synchronize()
+    out["wall_ms_per_step"] = (time.perf_counter() - t0) / steps * 1e3
+    out["device_ms_per_step"] = max(t_begin.elapsed_time(marks[si][-1][-1]) for si in range(S)) / steps
+    if S == 1:
+        m = marks[0]
+        out["ms_per_call"] = {"gather": float(np.mean([x[0].elapsed_time(x[1]) for x in m])),
+                              "handle": float(np.mean([x[1].elapsed_time(x[2]) for x in m])),
+                              "fold": float(np.mean([x[3].elapsed_time(x[4]) for x in m])),
+                              "reply_assembly": float(np.mean([x[2].elapsed_time(x[3]) for x in m]))}
+    for sh in shards:
+        assert int(sh["gerr"].abs().sum()) == 0 and int(sh["herr"].abs().sum()) == 0
+        assert int(sh["ferr"].abs().sum()) == 0
+        sh["eng"].close()
+    return out
+
+
+def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
+    """The survey's other configurations, measured in the same run so they are
+    on the driver's record (rank 0, one GPU, after the headline's timed
+    region; never part of `value`):
+      * the message-level path at config #3 (gather -> handle by reference ->
+        fold) on a fresh copy per step, one pipeline and two
+        shard pipelines (message_path), with the handler's and the fold's
+        rooflines from their algorithmic bytes (tools/msg_words.py);
+      * config #5, the election storm (65,536 x 7, 64 rounds per launch);
+      * config #2 (1,024 x 3 x 256: cache-resident, launch-bound).
+    `copies` are the state copies the headline already used, step i of the
+    message path on copy i restored from `master` (so its steps see both
+    memory populations, like the headline's)."""
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, synth_election_state, synth_seed, synth_tick_state
+
+    out = {}
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    # -- message-level path, config #3
+    one = message_path(master, copies, lp, G, P, L, dev, 1, steps, words=True)
+    two = message_path(master, copies, lp, G, P, L, dev, 2, steps)
+    hw, fw, ms = one["hw"], one["fw"], one["ms_per_call"]
+    n = 4 * int((lp >= 0).sum())
+    step_ms = ms["gather"] + ms["handle"] + ms["fold"]
     hb = 4 * hw["words"]
     out["message_path_config3"] = {
         "workload": "config #3 message-level path: gather -> HandleAppendEntries (entries by reference, "
                     "message sets) -> processAppendEntriesReply + advanceCommitIndex, fresh copy per step",
         "messages": n, "steps": steps, "ms_per_call": {k: round(v, 4) for k, v in ms.items()},
         "decisions_per_s": G / (step_ms / 1e3),
+        "calls_ms_sum_vs_headline": step_ms / headline_ms,
+        "shards_2": {"what": "two shard pipelines: one engine per half of the groups on a hardware queue of its "
+                             "own, one host thread each (the Go goroutine per shard); one event per step per queue",
+                     "device_ms_per_step": two["device_ms_per_step"], "wall_ms_per_step": two["wall_ms_per_step"],
+                     "decisions_per_s": G / (two["device_ms_per_step"] / 1e3),
+                     "vs_headline": two["device_ms_per_step"] / headline_ms},
+        "one_pipeline_device_ms_per_step": one["device_ms_per_step"],
         "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
@@ -179,10 +265,10 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
                           "achieved": 4 * fw["words"] / ms["fold"] / 1e6, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                           "frac": 4 * fw["words"] / (ms["fold"] / 1e3) / HBM_PEAK,
                           "segments": fw["segments"], "a1_evaluations": fw["evaluations"],
-                          "note": "tools/msg_words.py fold_words: a1's log words (the Figure-8 gate's scans "
-                                  "down to the commit index) are most of the bytes; k_fold folds the replies and "
+                          "note": "tools/msg_words.py fold_words: a1 reads each range's top term and, unless it "
+                                  "settles the range (currentTerm, or below it on a replica whose terms_sorted "
+                                  "proof holds: include/mraft.h), Go's downward scan; k_fold folds the replies and "
                                   "probes each range's top word, k_fold_scan scans the ranges the probes left open"}}
-    eng.close()
 
     # -- config #5 election storm
     Ge, Pe, R = 65536, 7, 64
@@ -208,7 +294,8 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
     out["election_storm_config5"] = {
         "workload": "config #5: 65,536 groups x 7 peers, 64 election rounds per launch (mraft_election_rounds)",
         "kernel_ms_mean": float(np.mean(t5)), "group_rounds_per_s": Ge * R / (float(np.mean(t5)) / 1e3),
-        "groups_with_new_leader": int(((gf5.cpu().numpy() & 128) != 0).sum()), "bound": "valu"}
+        "groups_with_new_leader": int(((gf5.cpu().numpy() & 128) != 0).sum()), "bound": "valu",
+        "roofline": valu_roofline(float(np.mean(t5)))}
     e5.close()
 
     # -- config #2
@@ -240,6 +327,36 @@ def secondary(master, copies, lp, G, P, L, stream, dev, steps=8):
 
 
 CONFIG4_ANCHOR = os.path.join(ROOT, "profiles", "config4_n1_anchor.json")
+VALU_PMC = os.path.join(ROOT, "profiles", "pmc_valu_config5.json")
+
+
+def elect_src_sha() -> str:
+    import hashlib
+    h = hashlib.sha1()
+    for f in ("mraft_elect.hip", "mraft_device.h"):
+        h.update(open(os.path.join(ROOT, "multiraft_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:12]
+
+
+def valu_roofline(kernel_ms: float) -> dict:
+    """Config #5's roofline: VALU issue (tools/pmc_valu.py). The wave-level
+    VALU instruction count of one k_election_rounds<7> launch, from the
+    committed PMC pass of the same kernel source, over the chip's issue rate
+    (1,024 SIMD-32, 2 cycles per wave64 instruction, 2.4 GHz) in this run's
+    kernel time. None when no pass matches the source."""
+    if not os.path.exists(VALU_PMC):
+        return {"bound": "valu", "frac": None, "why": "no VALU PMC pass committed"}
+    pm = json.load(open(VALU_PMC))
+    insts = pm.get("counters_per_launch", {}).get("SQ_INSTS_VALU")
+    if pm.get("kernel_src_sha") != elect_src_sha() or not insts:
+        return {"bound": "valu", "frac": None, "why": "the committed VALU PMC pass is of another kernel source"}
+    peak = 1024 * 2.4e9 / 2  # wave-instructions per second
+    achieved = insts / (kernel_ms / 1e3)
+    return {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9,
+            "unit": "G wave-instructions/s (VALU issue)", "frac": achieved / peak,
+            "valu_insts_per_launch": insts, "valu_busy_pmc": pm.get("valu_busy"),
+            "source": f"profiles/{os.path.basename(VALU_PMC)} ({pm.get('tag')})",
+            "model": pm.get("model")}
 
 
 def pmc_json_path(G: int, S: int) -> str:
@@ -289,7 +406,8 @@ def config4_one_gpu(dev, stream, steps=10, shards=(1, 2)):
         if os.path.exists(pj):
             pm = json.load(open(pj))
             if pm.get("kernel_src_sha") == kernel_src_sha() and pm.get("shards", 1) == S:
-                pj_traffic[S] = (pm.get("hbm_bytes_per_launch"), f"profiles/{os.path.basename(pj)} ({pm.get('tag')})")
+                pj_traffic[S] = (pm.get("hbm_bytes_per_step", pm.get("hbm_bytes_per_launch")),
+                                 f"profiles/{os.path.basename(pj)} ({pm.get('tag')})")
     for n, S in enumerate(shards):
         eng.set_tick_shards(S)
         qs = [stream] if S == 1 else [torch.cuda.ExternalStream(eng.shard_stream(s), device=dev) for s in range(S)]
@@ -930,7 +1048,7 @@ def main():
             pm = json.load(open(args.pmc_json))
             if ((pm.get("groups"), pm.get("peers"), pm.get("log"), pm.get("shards", 1)) == (G, P, L, S)
                     and pm.get("kernel_src_sha") == kernel_src_sha()):
-                traffic = pm.get("hbm_bytes_per_launch")
+                traffic = pm.get("hbm_bytes_per_step", pm.get("hbm_bytes_per_launch"))
                 traffic_src = f"profiles/{os.path.basename(args.pmc_json)} ({pm.get('tag')})"
         except Exception:
             traffic = None
@@ -971,7 +1089,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK,
                      "traffic": traffic,
-                     "traffic_unit": "HBM bytes per launch (FETCH_SIZE+WRITE_SIZE, calibrated)",
+                     "traffic_unit": ("HBM bytes per step: FETCH_SIZE+WRITE_SIZE, calibrated, summed over the "
+                                      f"step's {S} launch(es)"),
                      "traffic_source": traffic_src,
                      "kernel": f"k_tick_group<{P},false>",
                      "algorithmic_read_bytes": 4 * rd, "algorithmic_write_bytes": 4 * wr,
@@ -1030,7 +1149,8 @@ def main():
             out["roofline"]["placement_probe"] = pp
     if (world == 1 and args.config == 3 and not args.no_secondary and G == 65536 and P == 5 and L == 4096
             and fan is None):
-        out["secondary"] = secondary(master, clones, lp, G, P, L, stream, dev)  # reuses the spent copies
+        out["secondary"] = secondary(master, clones, lp, G, P, L, stream, dev,
+                                     dt / K * 1e3)  # reuses the spent copies
         # config #4's N = 1 anchor: free config #3's copies, then all 262,144 groups on this GPU
         eng.close()
         del clones, master

@@ -59,6 +59,7 @@ def main():
     ker = float(np.mean([x.elapsed_time(y) for x, y in ev])) / 1e3
     # words touched per launch: 6 scalars + last term per replica read, 4 written,
     # the round masks, and matchIndex/nextIndex rows of elected replicas.
+    from bench import valu_roofline  # the VALU-issue roofline from the committed PMC pass
     flags = gf.cpu().numpy()
     bytes_launch = G * P * (7 + 4) * 4 + mask.size + int(((flags & 128) != 0).sum()) * P * 2 * 4
     out = {"metric": "election-storm rounds/sec @64k groups×7 peers (R=64 per launch)",
@@ -76,6 +77,7 @@ def main():
                                  "registers for all R rounds (HBM touched once in, once out); the GB/s "
                                  "here are only the state bytes per launch")},
            "requestvotes_per_sec": rv_upper * K / dt,
+           "valu_roofline": valu_roofline(ker * 1e3),
            "cpu_baseline": None}
     if not a.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))

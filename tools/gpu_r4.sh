@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 GPU pass, parametrised: TAG names the output directory
-# (gpurun_out/$TAG); STEPS lists what to run (tests, bench, prof, pmc, el).
+# (gpurun_out/$TAG); DO lists what to run (tests bench pmc valu trace smoke).
 #   TESTS   pytest selection (-k expression) for the tests step ("" = all -m gpu)
 #   BENCH   extra bench.py arguments
 set -uo pipefail
@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r4_dev}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-for st in ${STEPS:-tests bench}; do
+for st in ${DO:-tests bench}; do
   case $st in
     tests)
       echo "== tests ${TESTS:-all}"
@@ -20,6 +20,32 @@ for st in ${STEPS:-tests bench}; do
       timeout -k 10 600 python3 -u bench.py ${BENCH:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; tail -4 "$OUT/bench.err"; [ $rc -eq 0 ] || exit 1
       python3 tools/summarize_bench.py "$OUT/bench.json" ;;
+    pmc)
+      # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
+      echo "== pmc ${BENCH_EXTRA:-}"
+      rm -rf gpurun_out/prof
+      BENCH_EXTRA="--no-secondary ${BENCH_EXTRA:-}" bash tools/profile_round.sh > "$OUT/profile.log" 2>&1 || { tail -5 "$OUT/profile.log"; exit 1; }
+      python3 tools/pmc_summary.py "$TAG" > "$OUT/pmc_summary.log" 2>&1 || { tail -5 "$OUT/pmc_summary.log"; exit 1; }
+      mkdir -p "$OUT/pmc"; cp profiles/pmc_traffic*.json profiles/${TAG}_*.csv "$OUT/pmc/" 2>/dev/null
+      grep -E '"(hbm_bytes_per_step|traffic_over_algorithmic|shards|groups)"' "$OUT/pmc_summary.log" ;;
+    valu)
+      # SQ counters of the election storm (config #5) -> profiles/pmc_valu_config5.json
+      echo "== valu"
+      timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+      timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/valu" -o valu -- python3 bench_election.py --no-cpu-baseline --steps 5 \
+        > "$OUT/valu_bench.json" 2> "$OUT/valu_bench.err" || { tail -5 "$OUT/valu_bench.err"; exit 1; }
+      timeout -k 10 300 python3 bench_election.py --no-cpu-baseline > "$OUT/election_bench.json" 2> "$OUT/election_bench.err" || exit 1
+      python3 tools/pmc_valu.py "$TAG" "$OUT/valu" "$OUT/election_bench.json" | tee "$OUT/pmc_valu.log" | grep -E "frac|busy|SQ_INSTS_VALU" ;;
+    trace)
+      # kernel trace + stats of the bench (BENCH) -> $OUT/kt
+      echo "== trace ${BENCH:-}"
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt -- python3 bench.py ${BENCH:-} \
+        > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err" || { tail -5 "$OUT/kt_bench.err"; exit 1; }
+      python3 tools/summarize_bench.py "$OUT/kt_bench.json" ;;
+    smoke)
+      echo "== smoke"
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1; rc=$?; tail -2 "$OUT/smoke.txt"; [ $rc -eq 0 ] || exit 1 ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done

@@ -82,25 +82,36 @@ def main():
         except Exception:
             bench = {}
     cfg = bench.get("config", {})
+    S = int(cfg.get("shards_per_gpu", 1) or 1)
+    groups = cfg.get("groups_per_gpu", 65536)
+    # With S tick shards every step is S launches over G/S groups each (the
+    # same kernel): the per-dispatch average times S is one step's traffic.
     out = {
         "tag": tag,
         "kernel": k,
         "kernel_src_sha": kernel_src_sha(),
-        "groups": cfg.get("groups_per_gpu", 65536),
+        "groups": groups,
         "peers": cfg.get("peers", 5),
         "log": cfg.get("log_capacity", 4096),
+        "shards": S,
+        "launches_per_step": S,
         "fetch_size_kb": fv,
         "write_size_kb": wv,
         "fetch_factor": fetch_factor,
         "write_factor": write_factor,
-        "hbm_read_bytes_per_launch": fv * 1024 * fetch_factor,
-        "hbm_write_bytes_per_launch": wv * 1024 * write_factor,
-        "hbm_bytes_per_launch": fv * 1024 * fetch_factor + wv * 1024 * write_factor,
+        "hbm_read_bytes_per_dispatch": fv * 1024 * fetch_factor,
+        "hbm_write_bytes_per_dispatch": wv * 1024 * write_factor,
+        "hbm_bytes_per_dispatch": fv * 1024 * fetch_factor + wv * 1024 * write_factor,
+        "hbm_bytes_per_step": S * (fv * 1024 * fetch_factor + wv * 1024 * write_factor),
+        "hbm_bytes_per_launch": S * (fv * 1024 * fetch_factor + wv * 1024 * write_factor),  # per step (older name)
         "algorithmic_bytes_per_launch": bench.get("roofline", {}).get("algorithmic_bytes_per_launch"),
     }
+    alg = out["algorithmic_bytes_per_launch"]
+    if alg:
+        out["traffic_over_algorithmic"] = out["hbm_bytes_per_step"] / alg
     # the headline config keeps the plain name; other group counts (config #4
-    # on one GPU) get their own file, which bench.py picks by group count
-    name = "pmc_traffic.json" if out["groups"] == 65536 else f"pmc_traffic_g{out['groups']}.json"
+    # on one GPU) and shard counts get their own file (bench.pmc_json_path)
+    name = ("pmc_traffic" + ("" if groups == 65536 else f"_g{groups}") + ("" if S == 1 else f"_s{S}") + ".json")
     json.dump(out, open(os.path.join(dst, name), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
