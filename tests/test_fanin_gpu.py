@@ -68,3 +68,46 @@ def test_one_rank_rccl_gather_equals_export(mode):
                 assert (c_, t_, ldr) == (int(oc[g]), int(otl[g]) >> 1, bool(otl[g] & 1))
         finally:
             fan.close()
+
+
+@pytest.mark.parametrize("mode", ["inline", "overlap", "reserved_cus"])
+def test_rccl_gather_after_sharded_ticks(mode):
+    """The fan-in after ticks split over the engine's two shard queues
+    (mraft_set_tick_shards): the engine itself orders the gather after every
+    shard's launch (inline: the engine stream joins the shards; overlap: the
+    fan-in stream waits on each shard queue), so several ticks and gathers
+    enqueued back to back with no host-side event each gather exactly what
+    its tick exported (round 3's ADVICE: the bench's unordered warm-up
+    gathers)."""
+    import torch
+    G, P, L, C = 4096, 5, 256, 4
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + 1)
+    o = Oracle(G, P, L, st)
+    o.replicate_tick(lp)
+    oc, otl = o.export_group_status(lp)
+    dev = torch.device("cuda", 0)
+    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    copies = [{k: v.clone() for k, v in master.items()} for _ in range(C)]
+    lp_d = torch.from_numpy(lp).to(dev)
+    status = torch.zeros((C, 2 * G), dtype=torch.int32, device=dev)
+    out = torch.full((C, 2 * G), -7, dtype=torch.int32, device=dev)
+    flags = torch.zeros((C, G), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    with Engine(G, P, L, device=0, alloc=False) as e:
+        e.set_tick_shards(2)
+        if mode == "reserved_cus":
+            e.fanin_reserve_cus(8)
+        fan = RcclFanIn(e, rank=0, world=1)
+        try:
+            for c in range(C):
+                e.bind(copies[c])
+                e.replicate_tick_export(lp_d, flags[c], status[c, :G], status[c, G:], where=DEVICE)
+                fan.gather(status[c], out[c], overlap=(mode != "inline"))
+            e.synchronize()
+            e.fanin_synchronize()
+        finally:
+            fan.close()
+    want = np.concatenate([oc, otl])
+    for c in range(C):
+        assert np.array_equal(status[c].cpu().numpy(), want)
+        assert np.array_equal(out[c].cpu().numpy(), want), c

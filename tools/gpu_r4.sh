@@ -20,6 +20,13 @@ for st in ${DO:-tests bench}; do
       timeout -k 10 600 python3 -u bench.py ${BENCH:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
       rc=$?; tail -4 "$OUT/bench.err"; [ $rc -eq 0 ] || exit 1
       python3 tools/summarize_bench.py "$OUT/bench.json" ;;
+    bench2|bench3)
+      # another bench line in the same call (A/B on the same box): BENCH2 / BENCH3 arguments
+      eval "args=\${$(echo $st | tr a-z A-Z):-}"
+      echo "== $st $args"
+      timeout -k 10 600 python3 -u bench.py $args > "$OUT/$st.json" 2> "$OUT/$st.err"
+      rc=$?; tail -2 "$OUT/$st.err"; [ $rc -eq 0 ] || exit 1
+      python3 tools/summarize_bench.py "$OUT/$st.json" ;;
     pmc)
       # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
       echo "== pmc ${BENCH_EXTRA:-}"
