@@ -131,7 +131,7 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
     def run(sh, i, marks):
         e, st, n, a = sh["eng"], sh["st"], sh["n"], sh["args"]
         e.bind(sh["views"][i])
-        if marks is not None:
+        if marks is not None and len(marks) > 1:
             marks[0].record(st)
         ck(lib.mraft_gather_append_args(e._h, sh["slots"].data_ptr(), sh["peers"].data_ptr(), n, a.data_ptr(),
                                         sh["gerr"].data_ptr(), DEVICE), "gather")
@@ -187,9 +187,14 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
     for sh in shards:
         sh["st"].wait_event(t_begin)
 
+    errors = []
+
     def worker(si):
-        for i in range(steps):
-            run(shards[si], i, marks[si][i])
+        try:
+            for i in range(steps):
+                run(shards[si], i, marks[si][i])
+        except BaseException as x:  # re-raised after the join
+            errors.append(x)
 
     t0 = time.perf_counter()
     th = [threading.Thread(target=worker, args=(si,)) for si in range(S)]
@@ -197,6 +202,8 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
         t.start()
     for t in th:
         t.join()
+    if errors:
+        raise errors[0]
     for sh in shards:
         sh["eng"].synchronize()
     torch.cuda.synchronize()
