@@ -205,3 +205,75 @@ def test_withheld_proof_same_decisions_gpu(what):
         items, seg = synth_fold_batch(st, Gs, Ps, Ls, lp, seed=7)
         assert np.array_equal(r1, o.process_append_replies(items, seg)[0])
     assert_states_equal(s1, o.state(), Gs, Ps, Ls, f"{what} vs oracle")
+
+
+def _history(mk, monotone, seed, steps=6):
+    """Random sequences of every call that touches the logs — the fused tick,
+    the message path by reference and by value (entries with their args'
+    flag), Start, Snapshot, the InstallSnapshot exchange, restarts — on
+    adversarial states (non-monotone terms unless `monotone`). Returns the
+    backend and the states after each step."""
+    from message_cases import all_follower_items, external_entries, results_of
+    from random_states import random_tick_state
+    from snapshot_cases import run_snapshot_scenario
+    rng = np.random.default_rng(seed)
+    Gh, Ph, Lh = 96, 5, 64
+    st, lp = random_tick_state(rng, Gh, Ph, Lh, monotone=monotone)
+    e = mk(Gh, Ph, Lh, st)
+    seen = []
+    for k in range(steps):
+        op = k % 6
+        if op == 0:
+            e.replicate_tick(lp)
+        elif op in (1, 2):
+            lpv = np.where((lp >= 0) & (lp < Ph), lp, -1).astype(np.int32)
+            slots, peers = all_follower_items(lpv, Gh, Ph)
+            args, gerr = e.gather_append_args(slots, peers)
+            ok = gerr == 0
+            if op == 1:
+                rep, herr = e.handle_append_entries(args[ok], None)
+            else:
+                a2, buf = external_entries(args[ok], np.ones(int(ok.sum()), bool), e.store_state(), Lh)
+                rep, herr = e.handle_append_entries(a2, buf)
+            res, seg = results_of(slots[ok], peers[ok], args[ok], rep, herr, Gh, Ph)
+            e.process_append_replies(res, seg)
+        elif op == 3:
+            ld = np.array([g * Ph + lp[g] for g in range(Gh) if 0 <= lp[g] < Ph], np.int32)
+            e.start(ld, rng.integers(1, 4, size=len(ld)).astype(np.int32))
+        elif op == 4:
+            run_snapshot_scenario(e, e.store_state(), Gh, Ph, Lh, np.where(lp < Ph, lp, -1), seed + k)
+        else:
+            sl = rng.choice(Gh * Ph, size=Gh // 4, replace=False).astype(np.int32)
+            hdr, terms = e.read_persistent(sl)
+            e.restore(hdr, terms)
+        s = e.store_state()
+        assert_terms_sorted_sound(s, Gh, Ph, Lh, f"step {k}")
+        seen.append(s)
+    return e, seen, (Gh, Ph, Lh)
+
+
+@pytest.mark.parametrize("monotone", [True, False])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_history_oracle(monotone, seed):
+    """Every call keeps the proof sound on the oracle; on monotone states most
+    replicas keep it."""
+    e, seen, (Gh, Ph, Lh) = _history(lambda G_, P_, L_, st: Oracle(G_, P_, L_, st), monotone, seed)
+    if monotone:
+        assert seen[-1]["terms_sorted"].mean() > 0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("monotone", [True, False])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_history_gpu_equals_oracle(monotone, seed):
+    """The same histories on libmraft_hip.so: identical state after every
+    step, the proof included."""
+    def gpu(G_, P_, L_, st):
+        e = Engine(G_, P_, L_)
+        e.load_state(st)
+        return e
+    _, so, dims = _history(lambda G_, P_, L_, st: Oracle(G_, P_, L_, st), monotone, seed)
+    eg, sg, _ = _history(gpu, monotone, seed)
+    for k, (a, b) in enumerate(zip(sg, so)):
+        assert_states_equal(a, b, *dims, f"history step {k}")
+    eg.close()
