@@ -706,7 +706,7 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
     if (s.role[g] == kLeader) {
       R = 5;
       if (s.commit[g] < s.dummy[g]) fl = MRAFT_G_ERROR;
-      else { fl = MRAFT_G_ACTIVE; A = 1; }
+      else { fl = MRAFT_G_ACTIVE; A = 1; R = 6; }  // + terms_sorted (DESIGN.md §4 header words)
     }
   }
   if (count) {
