@@ -75,7 +75,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
+def sleep_cycles_per_ms(stream) -> float:
+    """torch.cuda._sleep's units on this device (a spin on the GPU clock
+    counter), measured once with HIP events."""
+    import torch
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        a.record()
+        torch.cuda._sleep(int(1e6))
+        b.record()
+    b.synchronize()
+    return 1e6 / max(a.elapsed_time(b), 1e-3)
+
+
+def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset_ms=0.0):
     """The config #3 message-level path (gather -> HandleAppendEntries by
     reference -> processAppendEntriesReply + a1) as S shard
     pipelines: shard s = groups [G*s/S, G*(s+1)/S) of every state copy (SoA
@@ -86,7 +99,11 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
     for its plan) do not hold the other back. Step i runs on copy i restored
     from `master`; the warm-up on copy `steps`.
     S = 1: one event between consecutive calls (the per-call split);
-    S > 1: one event per step on each queue (the device span per step).
+    S > 1: one event per step on each queue (the device span per step);
+    shard s > 0 starts `offset_ms` * s / (S - 1) after shard 0 (a device
+    spin on its queue), so the shards' short latency-bound calls (gather,
+    claim, plan, fold) can run beside another shard's streaming handler
+    instead of in lock-step with it.
     words=True: the algorithmic words of one batch (tools/msg_words.py) from
     the warm-up's inputs (S = 1 only)."""
     import threading
@@ -185,11 +202,15 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False):
     # spin on torch's stream, so all threads have enqueued their first step
     # when the device starts on them (thread start-up is not device time).
     t_begin = torch.cuda.Event(enable_timing=True)
+    cpm = sleep_cycles_per_ms(torch.cuda.current_stream()) if offset_ms > 0 and S > 1 else 0.0
     torch.cuda.synchronize()
     torch.cuda._sleep(int(12e6))
     t_begin.record()
-    for sh in shards:
+    for si, sh in enumerate(shards):
         sh["st"].wait_event(t_begin)
+        if cpm and si > 0:
+            with torch.cuda.stream(sh["st"]):
+                torch.cuda._sleep(int(cpm * offset_ms * si / (S - 1)))
 
     errors = []
 
@@ -250,6 +271,8 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     # -- message-level path, config #3
     one = message_path(master, copies, lp, G, P, L, dev, 1, steps, words=True)
     two = message_path(master, copies, lp, G, P, L, dev, 2, min(2 * steps, len(copies) - 1))
+    half = message_path(master, copies, lp, G, P, L, dev, 2, min(2 * steps, len(copies) - 1),
+                        offset_ms=one["device_ms_per_step"] / 2)
     hw, fw, ms = one["hw"], one["fw"], one["ms_per_call"]
     n = 4 * int((lp >= 0).sum())
     step_ms = ms["gather"] + ms["handle"] + ms["fold"]
@@ -266,6 +289,11 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                      "steps": two["steps"], "device_ms_per_step": two["device_ms_per_step"],
                      "decisions_per_s": G / (two["device_ms_per_step"] / 1e3),
                      "vs_headline": two["device_ms_per_step"] / headline_ms},
+        "shards_2_offset": {"what": "as shards_2, shard 1 started half a step after shard 0 (a device spin on its "
+                                    "queue before its first call; in the span)",
+                            "offset_ms": one["device_ms_per_step"] / 2, "steps": half["steps"],
+                            "device_ms_per_step": half["device_ms_per_step"],
+                            "vs_headline": half["device_ms_per_step"] / headline_ms},
         "one_pipeline_device_ms_per_step": one["device_ms_per_step"],
         "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,

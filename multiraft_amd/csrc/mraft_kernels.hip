@@ -60,13 +60,13 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
                              const int64_t *__restrict__ seg_begin, int64_t gp,
                              unsigned long long *__restrict__ claim, uint32_t epoch,
                              int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
-                             int32_t *__restrict__ z1, int32_t *__restrict__ z2) {
+                             int32_t *__restrict__ z1, unsigned *__restrict__ zc) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < nz) {
     z0[i] = 0;
     z1[i] = 0;
-    if (z2) z2[i] = 0;  // no a1 range pending for k_fold_scan
   }
+  if (i == 0 && zc) *zc = 0;  // no a1 range pending for k_fold_scan yet
   if (i >= n) return;
   int64_t rec = i;
   if (seg_begin) {
@@ -806,13 +806,31 @@ __device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row
 // ascending: their top words are probed in parallel (one round trip; on a
 // log whose last entries carry the current term, every range ends there) and
 // only ranges whose top word differs are scanned, wave-cooperatively.
+// Appends the lanes' pending a1 ranges (pred) to k_fold_scan's compact list:
+// one atomic per wave on the list's counter. Record: {lo, hi, slot,
+// currentTerm}, {dummy, ring head, reply index, 0}. Wave-uniform call.
+__device__ __forceinline__ void push_pending(int4 *__restrict__ pend, unsigned *__restrict__ pcount, bool pred,
+                                             int4 ra, int4 rb) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return;
+  const int l0 = first_lane(m);
+  unsigned base = 0;
+  if (lane_id() == l0) base = atomicAdd(pcount, (unsigned)__popcll(m));
+  base = (unsigned)__shfl((int)base, l0, 64);
+  if (pred) {
+    const unsigned k = base + (unsigned)__popcll(m & ((1ull << lane_id()) - 1));
+    pend[2 * (int64_t)k] = ra;
+    pend[2 * (int64_t)k + 1] = rb;
+  }
+}
+
 template <int P>
 __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result *__restrict__ items,
                                              const int64_t *__restrict__ seg_begin, int64_t sg,
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
+                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   int bad = uni(seg_err[sg]);  // the claim verdict: a bad segment's slot may be out of range
@@ -923,11 +941,9 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
         if (pv == t0) x = phi;                                           // :98
         else settled = srt && pv < t0;
       }
-      if (plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled) {
-        pend[2 * (b + base + lane)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
-        pend[2 * (b + base + lane) + 1] = make_int4(dummy, head, 0, 0);
-        pmark[b + base + lane] = 1;
-      }
+      push_pending(pend, pcount, plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled,
+                   make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0),
+                   make_int4(dummy, head, (int)(b + base + lane), 0));
     } else if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
       // One range (the usual batch): no separate probe of its top word — the
       // scan's first window starts there (one round trip fewer when the top
@@ -988,32 +1004,32 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
 // and raises the replica's commitIndex (atomicMax: several waves may hold
 // ranges of one segment).
 __global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend,
-                                                     const int32_t *__restrict__ pmark, int64_t n,
+                                                     const unsigned *__restrict__ pcount,
                                                      int32_t *__restrict__ flags) {
   const int lane = lane_id();
-  const int64_t i = (int64_t)blockIdx.x * MRAFT_FSCAN_W + lane;
-  // the reply's marker and record in one round trip: {lo, hi, slot,
-  // currentTerm}, {dummy, head} (marker 0: nothing pending, the record is
-  // stale)
-  int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0);
-  int mk = 0;
-  if (lane < MRAFT_FSCAN_W && i < n) {
-    mk = pmark[i];
-    ra = pend[2 * i];
-    rb = pend[2 * i + 1];
-  }
-  const int lo = ra.x, hi = mk ? ra.y : ra.x - 1;
+  const int64_t cnt = (int64_t)*pcount;  // k_fold's compact list: nothing pending, nothing to do
   const int L = s.L;
-  for (unsigned long long m = __ballot(hi >= lo); m; m &= m - 1) {
-    const int k = first_lane(m);
-    const int klo = __builtin_amdgcn_readlane(lo, k), khi = __builtin_amdgcn_readlane(hi, k);
-    const int kslot = __builtin_amdgcn_readlane(ra.z, k), kt0 = __builtin_amdgcn_readlane(ra.w, k);
-    const int kd = __builtin_amdgcn_readlane(rb.x, k), kh = __builtin_amdgcn_readlane(rb.y, k);
-    const int x = fold_scan_down_eq<MRAFT_FSCAN_U1, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
-                                                                   kt0);  // klo - 1 if none
-    if (lane == k && x >= klo) {
-      flags[i] |= MRAFT_F_COMMITTED;                                     // :99-100
-      atomicMax(&s.commit[kslot], x);
+  for (int64_t b0 = (int64_t)blockIdx.x * MRAFT_FSCAN_W; b0 < cnt; b0 += (int64_t)gridDim.x * MRAFT_FSCAN_W) {
+    const int64_t i = b0 + lane;
+    // the record in one round trip: {lo, hi, slot, currentTerm}, {dummy,
+    // head, reply index}
+    int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0);
+    if (lane < MRAFT_FSCAN_W && i < cnt) {
+      ra = pend[2 * i];
+      rb = pend[2 * i + 1];
+    }
+    const int lo = ra.x, hi = ra.y;
+    for (unsigned long long m = __ballot(hi >= lo); m; m &= m - 1) {
+      const int k = first_lane(m);
+      const int klo = __builtin_amdgcn_readlane(lo, k), khi = __builtin_amdgcn_readlane(hi, k);
+      const int kslot = __builtin_amdgcn_readlane(ra.z, k), kt0 = __builtin_amdgcn_readlane(ra.w, k);
+      const int kd = __builtin_amdgcn_readlane(rb.x, k), kh = __builtin_amdgcn_readlane(rb.y, k);
+      const int x = fold_scan_down_eq<MRAFT_FSCAN_U1, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
+                                                                     kt0);  // klo - 1 if none
+      if (lane == k && x >= klo) {
+        flags[rb.z] |= MRAFT_F_COMMITTED;                                // :99-100
+        atomicMax(&s.commit[kslot], x);
+      }
     }
   }
 }
@@ -1039,7 +1055,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
                                             int64_t n_seg, const int32_t *__restrict__ seg_err,
                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                            int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
+                                            int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
   constexpr int NG = 64 / GW;
   static_assert(GW >= P && GW >= 7, "a group holds the replica's match / next rows and seven scalars");
   const int lane = lane_id(), gl = lane & (GW - 1);
@@ -1056,7 +1072,7 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
     for (int j = 0; j < NG; ++j)
       if (sg0 + j < n_seg)
-        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend, pmark);
+        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend, pcount);
     return;
   }
   (void)n_items;
@@ -1156,11 +1172,8 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     // replica's commitIndex to the highest index it finds (the ranges of a
     // segment are disjoint and ascending, so "the latest range that found
     // one" is the maximum over all of them, probes included)
-    if (go && plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled) {
-      pend[2 * (b + gl)] = make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0);
-      pend[2 * (b + gl) + 1] = make_int4(dummy, head, 0, 0);
-      pmark[b + gl] = 1;
-    }
+    push_pending(pend, pcount, go && plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled,
+                 make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0), make_int4(dummy, head, (int)(b + gl), 0));
   }
   // the ranges whose top word differs, of all four groups, one after another
   // with the whole wave (a 16-lane scan moves a quarter of the terms per round
@@ -1201,22 +1214,22 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend, int32_t *__restrict__ pmark) {
+                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
   if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
     const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pmark);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
     return;
   }
   if constexpr (MRAFT_FOLD_GROUP > 1) {
     constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
     for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
       fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
-                         pmark);
+                         pcount);
     return;
   }
   for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pmark);
+    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
 }
 
 // ---------------------------------------------------------------- Start
@@ -1785,11 +1798,11 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   if (nt <= 0) return;
   const bool split = MRAFT_FOLD_SPLIT;  // the ABI always passes scan_buf
   if (split && !scan_buf) return;
-  int4 *pend = split ? (int4 *)scan_buf : nullptr;               // 2 int4 per reply
-  int32_t *pmark = split ? (int32_t *)(pend + 2 * n) : nullptr;  // 1 int per reply
+  int4 *pend = split ? (int4 *)scan_buf : nullptr;                          // 2 int4 per pending reply
+  unsigned *pcount = split ? (unsigned *)(pend + 2 * n) : nullptr;          // the list's length
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
-                     epoch, seg_err, n, flags, item_err, pmark);
+                     epoch, seg_err, n, flags, item_err, pcount);
   if (n_seg <= 0) return;
   const int64_t waves = (n_seg + MRAFT_FOLD_GROUP - 1) / MRAFT_FOLD_GROUP;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
@@ -1797,16 +1810,18 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err, pend, pmark);                                         \
+                       flags, item_err, pend, pcount);                                        \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
 #undef MRAFT_FOLD_CASE
     default: return;
   }
+  // the scans: grid-stride over the list k_fold left (its length read on the
+  // device); at most 8 waves per SIMD's worth of workgroups
   if (split)
-    hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W)), dim3(64), 0, st, s,
-                       pend, pmark, n, flags);
+    hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)8192)),
+                       dim3(64), 0, st, s, pend, pcount, flags);
 }
 
 size_t fold_scan_bytes(int64_t n) {

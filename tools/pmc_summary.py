@@ -33,12 +33,22 @@ def kernel_src_sha() -> str:
 
 
 def counter_avgs(path):
+    """Per (kernel, counter): the average over the dispatches of the kernel's
+    most frequent grid size — the timed steps' launches; a differently sized
+    dispatch of the same kernel (the bench's one-launch check after the
+    sharded steps) is left out."""
     out = {}
     for f in glob.glob(os.path.join(path, "*_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             k = (r["Kernel_Name"], r["Counter_Name"])
-            out.setdefault(k, []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in out.items()}
+            out.setdefault(k, []).append((int(r.get("Grid_Size") or 0), float(r["Counter_Value"])))
+    avg = {}
+    for k, v in out.items():
+        grids = [g for g, _ in v]
+        mode = max(set(grids), key=grids.count)
+        sel = [x for g, x in v if g == mode]
+        avg[k] = sum(sel) / len(sel)
+    return avg
 
 
 def main():

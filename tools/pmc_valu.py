@@ -45,12 +45,16 @@ def main():
            "simds": 1024, "clock_hz": 2.4e9, "cycles_per_valu_inst": 2}
     if len(sys.argv) > 3 and os.path.exists(sys.argv[3]):
         b = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
-        km = b.get("kernel_ms_mean")
+        km = b.get("kernel_ms_mean") or b.get("roofline", {}).get("kernel_ms_mean")
         if km and "SQ_INSTS_VALU" in avg:
             out["kernel_ms_mean_same_run"] = km
             out["frac_same_run"] = avg["SQ_INSTS_VALU"] * 2 / (1024 * 2.4e9 * km / 1e3)
-    if "SQ_ACTIVE_INST_VALU" in avg and avg.get("GRBM_GUI_ACTIVE"):
-        out["valu_busy"] = 4 * avg["SQ_ACTIVE_INST_VALU"] / (1024 * avg["GRBM_GUI_ACTIVE"])
+    if avg.get("GRBM_GUI_ACTIVE") and out.get("kernel_ms_mean_same_run"):
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs: the engine clock the
+        # launch actually ran at, and the fraction at that clock
+        clk = avg["GRBM_GUI_ACTIVE"] / 8 / (out["kernel_ms_mean_same_run"] / 1e3)
+        out["clock_hz_measured"] = clk
+        out["frac_at_measured_clock"] = avg["SQ_INSTS_VALU"] * 2 / (1024 * clk * out["kernel_ms_mean_same_run"] / 1e3)
     json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_valu_config5.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
