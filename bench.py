@@ -152,18 +152,14 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
             marks[0].record(st)
         ck(lib.mraft_gather_append_args(e._h, sh["slots"].data_ptr(), sh["peers"].data_ptr(), n, a.data_ptr(),
                                         sh["gerr"].data_ptr(), DEVICE), "gather")
-        if marks is not None and len(marks) > 2:
+        if marks is not None and len(marks) > 1:
             marks[1].record(st)
-        ck(lib.mraft_handle_append_entries(e._h, a.data_ptr(), n, None, 0, sh["rep"].data_ptr(),
-                                           sh["herr"].data_ptr(), DEVICE), "handle")
-        if marks is not None and len(marks) > 2:
+        # the handler also writes each reply's record for the leader's fold
+        # (mraft_handle_append_entries_ex: no host-side assembly)
+        ck(lib.mraft_handle_append_entries_ex(e._h, a.data_ptr(), n, None, 0, sh["rep"].data_ptr(),
+                                              sh["res"].data_ptr(), sh["herr"].data_ptr(), DEVICE), "handle")
+        if marks is not None and len(marks) > 1:
             marks[2].record(st)
-        # the fold's reply records from (args, reply): host glue, one kernel
-        with torch.cuda.stream(st):
-            torch.cat([sh["slots"][:, None], sh["peers"][:, None], a[:, 1:2], a[:, 3:4], a[:, 6:7], sh["rep"][:, 0:3]],
-                      dim=1, out=sh["res"])
-        if marks is not None and len(marks) > 2:
-            marks[3].record(st)
         ck(lib.mraft_process_append_replies(e._h, sh["res"].data_ptr(), n, sh["seg"].data_ptr(),
                                             len(sh["seg"]) - 1, sh["flags"].data_ptr(), sh["ferr"].data_ptr(),
                                             DEVICE), "fold")
@@ -196,7 +192,7 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
         assert np.array_equal(fw["commit"][ld_sl], copies[steps]["commit_index"].cpu().numpy()[ld_sl]), \
             "fold word count: replayed commits differ from the device's"
         out["hw"], out["fw"] = hw, fw
-    nm = 5 if S == 1 else 1
+    nm = 4 if S == 1 else 1
     marks = [[[torch.cuda.Event(enable_timing=True) for _ in range(nm)] for _ in range(steps)] for _ in range(S)]
     # A gate: every queue waits for an event recorded behind a ~5 ms device
     # spin on torch's stream, so all threads have enqueued their first step
@@ -237,8 +233,7 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
         m = marks[0]
         out["ms_per_call"] = {"gather": float(np.mean([x[0].elapsed_time(x[1]) for x in m])),
                               "handle": float(np.mean([x[1].elapsed_time(x[2]) for x in m])),
-                              "fold": float(np.mean([x[3].elapsed_time(x[4]) for x in m])),
-                              "reply_assembly": float(np.mean([x[2].elapsed_time(x[3]) for x in m]))}
+                              "fold": float(np.mean([x[2].elapsed_time(x[3]) for x in m]))}
     for sh in shards:
         assert int(sh["gerr"].abs().sum()) == 0 and int(sh["herr"].abs().sum()) == 0
         assert int(sh["ferr"].abs().sum()) == 0
@@ -279,7 +274,9 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     hb = 4 * hw["words"]
     out["message_path_config3"] = {
         "workload": "config #3 message-level path: gather -> HandleAppendEntries (entries by reference, "
-                    "message sets) -> processAppendEntriesReply + advanceCommitIndex, fresh copy per step",
+                    "message sets; the reply records for the fold written by the handler, "
+                    "mraft_handle_append_entries_ex) -> processAppendEntriesReply + advanceCommitIndex, fresh "
+                    "copy per step",
         "messages": n, "steps": steps, "ms_per_call": {k: round(v, 4) for k, v in ms.items()},
         "decisions_per_s": G / (step_ms / 1e3),
         "calls_ms_sum_vs_headline": step_ms / headline_ms,

@@ -372,6 +372,21 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,
                                 int32_t *item_err, int32_t where);
 
+/* mraft_handle_append_entries that also writes, per item, the reply record
+ * its co-resident leader folds (results, n records, optional): slot = the
+ * follower's group's replica args.leader_id, peer = the follower's peer
+ * index, the args' term / prevLogIndex / entry count and the reply's term /
+ * success / ConflictIndex — what mraft_process_append_replies takes, with no
+ * host-side assembly when every replica of a group lives in this engine (a
+ * Go host receiving replies over the network builds its own). Items with
+ * item_err != 0 get slot = peer = -1 and must be left out of the fold's
+ * segments. */
+int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args,
+                                   int64_t n, const int32_t *entry_terms,
+                                   int64_t n_entry_terms, mraft_ae_reply *replies,
+                                   mraft_ae_result *results, int32_t *item_err,
+                                   int32_t where);
+
 /* a2 + a1, processAppendEntriesReply + advanceCommitIndexForLeader
  * (raft_append_entry.go:66-105). Items are folded per segment in array order;
  * segment s = items [seg_begin[s], seg_begin[s+1]) all with the same leader

@@ -97,7 +97,7 @@ ABI_SYMBOLS = (
     "mraft_collect_apply_compact",
     "mraft_comm_unique_id", "mraft_comm_init", "mraft_comm_destroy", "mraft_allgather_status",
     "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
-    "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream",
+    "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream", "mraft_handle_append_entries_ex",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -148,6 +148,7 @@ _SIGS = {
     "mraft_fanin_stream": (_vp, [_vp]),
     "mraft_fanin_reserve_cus": (ctypes.c_int, [_vp, _i32]),
     "mraft_set_tick_shards": (ctypes.c_int, [_vp, _i32]),
+    "mraft_handle_append_entries_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32]),
     "mraft_get_tick_shards": (_i32, [_vp]),
     "mraft_shard_stream": (_vp, [_vp, _i32]),
 }

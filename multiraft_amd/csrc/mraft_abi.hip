@@ -543,6 +543,13 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots, const int32_
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int64_t n,
                                 const int32_t *entry_terms, int64_t n_entry_terms,
                                 mraft_ae_reply *replies, int32_t *item_err, int32_t where) {
+  return mraft_handle_append_entries_ex(h, args, n, entry_terms, n_entry_terms, replies, nullptr, item_err, where);
+}
+
+int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, int64_t n,
+                                   const int32_t *entry_terms, int64_t n_entry_terms,
+                                   mraft_ae_reply *replies, mraft_ae_result *results, int32_t *item_err,
+                                   int32_t where) {
   TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
@@ -550,11 +557,12 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   HIP_TRY(hipSetDevice(h->device));
   TRY(ensure_claim(h));
   Stage sg(h, where);
-  void *a, *en, *r, *e;
+  void *a, *en, *r, *e, *rs;
   TRY(sg.map(args, sizeof(mraft_ae_args) * n, true, false, &a));
   TRY(sg.map(entry_terms, sizeof(int32_t) * (size_t)(entry_terms ? n_entry_terms : 0), true, false,
              &en));
   TRY(sg.map(replies, sizeof(mraft_ae_reply) * n, false, true, &r));
+  TRY(sg.map(results, sizeof(mraft_ae_result) * n, false, true, &rs));
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
   const int32_t *src = en ? (const int32_t *)en : h->dev.log_term;
   const int64_t src_n = en ? n_entry_terms : gp_of(h) * h->L;
@@ -563,7 +571,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
     mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h), h->P,
                         h->claim, h->epoch, (int32_t *)e, h->stream);
     mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, nullptr, nullptr, 0,
-                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, h->stream);
+                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, (mraft_ae_result *)rs, h->stream);
     return sg.finish();
   }
   // Entries by reference into the engine's log: messages reading the same
@@ -595,7 +603,7 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
   // the totals to the host's pinned words, then the sequence word
   mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, (const int64_t *)soff,
                           (const int64_t *)sets, n, h->plan_dev + 1, ni, (mraft_ae_reply *)r, (int32_t *)e,
-                          h->plan_host_dev, ++h->plan_seq, h->stream);
+                          h->plan_host_dev, ++h->plan_seq, (mraft_ae_result *)rs, h->stream);
   volatile unsigned long long *ph = h->plan_host;
   const auto t_poll = std::chrono::steady_clock::now();
   for (unsigned spin = 1; ph[3] != h->plan_seq; ++spin) {
@@ -629,7 +637,8 @@ int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args, int6
     }
     mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
                             (int64_t)staged, (const int64_t *)soff, (const int64_t *)defer, (int64_t)n_defer,
-                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, h->stream);
+                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, (mraft_ae_result *)rs,
+                            h->stream);
   }
   return sg.finish();
 }

@@ -38,7 +38,8 @@ void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const 
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                       const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
                       int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
-                      int32_t *err, unsigned long long *host_total, unsigned long long seq, hipStream_t st);
+                      int32_t *err, unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
+                      hipStream_t st);
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
                  int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st);

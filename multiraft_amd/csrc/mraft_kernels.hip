@@ -390,6 +390,7 @@ struct HsArgs {
   int32_t *err;
   volatile unsigned long long *host_total;  // main launch: workgroup 0 publishes the plan's totals here
   unsigned long long seq;
+  mraft_ae_result *res;  // optional: each item's reply as its co-resident leader folds it
 };
 
 __device__ __forceinline__ HsArgs reload_hs() {
@@ -404,6 +405,7 @@ __device__ __forceinline__ HsArgs reload_hs() {
   k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
   k.n_stage = kp->n_stage; k.soff = kp->soff; k.sets = kp->sets; k.n_sets = kp->n_sets;
   k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err; k.host_total = kp->host_total; k.seq = kp->seq;
+  k.res = kp->res;
   return k;
 }
 
@@ -636,6 +638,32 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     if (fcommit_new >= 0) s2.commit[f] = fcommit_new;
     mark_persist_ae(s2, f, MRAFT_PERSIST_STATE);                       // deferred :111
     rep2[i] = r;
+  }
+#if MRAFT_AE_RELOAD
+  mraft_ae_result *__restrict__ res = kt.res;
+  const mraft_ae_args *__restrict__ args2 = kt.args;
+#else
+  mraft_ae_result *__restrict__ res = k0.res;
+  const mraft_ae_args *__restrict__ args2 = k0.args;
+#endif
+  if (res && cls >= AE_STALE) {
+    // the reply record the group's leader replica folds (co-resident: the
+    // leader is replica leader_id of the follower's group), for
+    // mraft_process_append_replies without a host-side assembly
+    const mraft_ae_args aa = args2[i];
+    const int PP = s2.P;
+    mraft_ae_result o;
+    o.slot = (aa.slot / PP) * PP + aa.leader_id;
+    o.peer = aa.slot % PP;
+    o.args_term = aa.term;
+    o.args_prev_log_index = aa.prev_log_index;
+    o.args_n_entries = aa.n_entries;
+    o.reply_term = r.term;
+    o.reply_success = r.success;
+    o.reply_conflict_index = r.conflict_index;
+    res[i] = o;
+  } else if (res && mine) {
+    res[i] = mraft_ae_result{-1, -1, 0, 0, 0, 0, 0, 0};  // item_err != 0 (or none written): no reply
   }
 }
 
@@ -1755,27 +1783,30 @@ template <int NI>
 static void launch_set(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                        const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
                        int64_t n_sets, const unsigned long long *set_count, mraft_ae_reply *rep, int32_t *err,
-                       unsigned long long *host_total, unsigned long long seq, hipStream_t st) {
+                       unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
+                       hipStream_t st) {
   // with the count on the device, n_sets is an upper bound: a workgroup per
   // MRAFT_AE_SPB sets of the bound (grid a multiple of 8, see k_handle_set)
   int64_t nb = sets ? n_sets : n;
   if (set_count) nb = ((nb + MRAFT_AE_SPB - 1) / MRAFT_AE_SPB + 7) / 8 * 8;
-  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, seq};
+  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, seq,
+                  res};
   hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, ka);
 }
 
 void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                       const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
                       int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
-                      int32_t *err, unsigned long long *host_total, unsigned long long seq, hipStream_t st) {
+                      int32_t *err, unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
+                      hipStream_t st) {
   if (n <= 0 || (sets && n_sets <= 0)) return;
 #define MRAFT_SET_CASE(k) \
   case k: launch_set<k>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, \
-                        seq, st); break;
+                        seq, res, st); break;
   switch (sets ? ni : 1) {
     MRAFT_SET_CASE(1) MRAFT_SET_CASE(2) MRAFT_SET_CASE(3) MRAFT_SET_CASE(4) MRAFT_SET_CASE(5) MRAFT_SET_CASE(6)
     default: launch_set<7>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total,
-                           seq, st);
+                           seq, res, st);
   }
 #undef MRAFT_SET_CASE
 }

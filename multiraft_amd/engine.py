@@ -234,16 +234,20 @@ class Engine:
                                                ptr(err), HOST), "mraft_gather_append_args")
         return out, err
 
-    def handle_append_entries(self, args: np.ndarray, entry_terms: np.ndarray | None):
+    def handle_append_entries(self, args: np.ndarray, entry_terms: np.ndarray | None, results: bool = False):
+        """HandleAppendEntries for a batch: (replies, item_err), and with
+        results=True also the reply records the co-resident leaders fold
+        (mraft_handle_append_entries_ex)."""
         args = np.ascontiguousarray(args, dtype=AE_ARGS)
         n = len(args)
         rep = np.zeros(n, dtype=AE_REPLY)
         err = np.zeros(n, dtype=np.int32)
+        res = np.zeros(n, dtype=AE_RESULT) if results else None
         et = None if entry_terms is None else np.ascontiguousarray(entry_terms, dtype=np.int32)
-        _ck(self._lib.mraft_handle_append_entries(self._h, ptr(args), n, ptr(et),
-                                                  0 if et is None else len(et), ptr(rep),
-                                                  ptr(err), HOST), "mraft_handle_append_entries")
-        return rep, err
+        _ck(self._lib.mraft_handle_append_entries_ex(self._h, ptr(args), n, ptr(et),
+                                                     0 if et is None else len(et), ptr(rep), ptr(res),
+                                                     ptr(err), HOST), "mraft_handle_append_entries_ex")
+        return (rep, err, res) if results else (rep, err)
 
     def process_append_replies(self, items: np.ndarray, seg_begin: np.ndarray | None = None):
         items = np.ascontiguousarray(items, dtype=AE_RESULT)

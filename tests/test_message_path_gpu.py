@@ -37,18 +37,24 @@ def _message_round(e, o, st, slots, peers, G, P, L, mode, equal):
     assert np.array_equal(gerr, ogerr) and np.array_equal(args, oargs)
     ok = gerr == 0
     if mode == "reference":
-        rep, herr = e.handle_append_entries(args, None)
+        rep, herr, gres = e.handle_append_entries(args, None, results=True)
         orep, oherr = o.handle_append_entries(args, None)
     else:
         a2, buf = external_entries(args, ok, st, L, misalign=(mode == "misaligned"))
         a2 = a2[ok]
-        rep, herr = e.handle_append_entries(a2, buf)
+        rep, herr, gres = e.handle_append_entries(a2, buf, results=True)
         orep, oherr = o.handle_append_entries(a2, buf)
         args, slots, peers = args[ok], slots[ok], peers[ok]
     assert np.array_equal(herr, oherr), f"{mode}: handle errors"
     assert np.array_equal(rep, orep), f"{mode}: replies"
     equal(e.store_state(), o.state(), G, P, L, f"{mode}: after handle")
     res, seg = results_of(slots, peers, args, rep, herr, G, P)
+    # the handler's own reply records (mraft_handle_append_entries_ex) are the
+    # host-assembled ones, item by item; failed items carry slot -1
+    okh = herr == 0
+    hand = gres[okh][np.argsort(gres["slot"][okh], kind="stable")]
+    assert np.array_equal(hand, res), f"{mode}: handler's reply records"
+    assert (gres["slot"][~okh] == -1).all()
     f, ferr = e.process_append_replies(res, seg)
     of, oferr = o.process_append_replies(res, seg)
     assert np.array_equal(ferr, oferr) and np.array_equal(f, of), f"{mode}: fold"
