@@ -458,6 +458,14 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   int f = a.slot;
   const int prev = a.prev_log_index, nn = a.n_entries;
   const bool live = cls == AE_DONE;
+  if (k0.res && mine) {
+    // the args half of the item's reply record for its co-resident leader's
+    // fold, stored now (no reload of the args at the wave's end); the reply
+    // half follows with the reply. Failed items: slot = peer = -1.
+    const int PP = s.P;
+    int4 *rr = reinterpret_cast<int4 *>(k0.res + i);
+    rr[0] = live ? make_int4((f / PP) * PP + a.leader_id, f % PP, a.term, prev) : make_int4(-1, -1, 0, 0);
+  }
   int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
   if (live) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
   mraft_ae_reply r = {0, 0, 0, 0};
@@ -641,29 +649,16 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   }
 #if MRAFT_AE_RELOAD
   mraft_ae_result *__restrict__ res = kt.res;
-  const mraft_ae_args *__restrict__ args2 = kt.args;
 #else
   mraft_ae_result *__restrict__ res = k0.res;
-  const mraft_ae_args *__restrict__ args2 = k0.args;
 #endif
-  if (res && cls >= AE_STALE) {
-    // the reply record the group's leader replica folds (co-resident: the
-    // leader is replica leader_id of the follower's group), for
-    // mraft_process_append_replies without a host-side assembly
-    const mraft_ae_args aa = args2[i];
-    const int PP = s2.P;
-    mraft_ae_result o;
-    o.slot = (aa.slot / PP) * PP + aa.leader_id;
-    o.peer = aa.slot % PP;
-    o.args_term = aa.term;
-    o.args_prev_log_index = aa.prev_log_index;
-    o.args_n_entries = aa.n_entries;
-    o.reply_term = r.term;
-    o.reply_success = r.success;
-    o.reply_conflict_index = r.conflict_index;
-    res[i] = o;
-  } else if (res && mine) {
-    res[i] = mraft_ae_result{-1, -1, 0, 0, 0, 0, 0, 0};  // item_err != 0 (or none written): no reply
+  if (res && mine) {
+    // the reply half of the record (nEntries, reply term, success,
+    // ConflictIndex); an item rejected after the prologue (capacity: cls
+    // AE_DONE) gets slot = peer = -1 as well
+    int4 *rr = reinterpret_cast<int4 *>(res + i);
+    if (cls == AE_DONE) rr[0] = make_int4(-1, -1, 0, 0);
+    rr[1] = cls >= AE_STALE ? make_int4(nn, r.term, r.success, r.conflict_index) : make_int4(0, 0, 0, 0);
   }
 }
 
