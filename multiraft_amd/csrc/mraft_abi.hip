@@ -662,7 +662,7 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
   TRY(scratch(h, 1, sizeof(int32_t) * (size_t)ns, &se));
   void *sc;
-  TRY(scratch(h, 7, mraft::fold_scan_bytes(n), &sc));
+  TRY(scratch(h, 7, mraft::fold_scan_bytes(n, ns), &sc));
   // three launches: the segment claims with the outputs zeroed, the fold
   // (which rejects a segment whose slot another one claimed), the a1 scans
   // its probes left open

@@ -43,7 +43,7 @@ void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const 
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
                  int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st);
-size_t fold_scan_bytes(int64_t n);  // scratch launch_fold's deferred a1 scans need for n replies
+size_t fold_scan_bytes(int64_t n, int64_t n_seg);  // scratch launch_fold needs (a1 scan list, long segments)
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
                   int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st);
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,

@@ -60,13 +60,14 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
                              const int64_t *__restrict__ seg_begin, int64_t gp,
                              unsigned long long *__restrict__ claim, uint32_t epoch,
                              int32_t *__restrict__ err, int64_t nz, int32_t *__restrict__ z0,
-                             int32_t *__restrict__ z1, unsigned *__restrict__ zc) {
+                             int32_t *__restrict__ z1, unsigned *__restrict__ zc, unsigned *__restrict__ zl) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < nz) {
     z0[i] = 0;
     z1[i] = 0;
   }
   if (i == 0 && zc) *zc = 0;  // no a1 range pending for k_fold_scan yet
+  if (i == 0 && zl) *zl = 0;  // no long segment for k_fold_long yet
   if (i >= n) return;
   int64_t rec = i;
   if (seg_begin) {
@@ -743,7 +744,7 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 // __launch_bounds__ minimum waves per SIMD of the reply fold: one segment per
 // wave, 8 (SGPRs spill to VGPR lanes; 13 % faster than 7); four per wave, 6
 // (80 VGPRs, no scratch; at 8 the per-lane fold state spills 72 B/lane)
-#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP > 1 ? 6 : 8)
+#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP > 1 && !MRAFT_FOLD_LONG_SPLIT ? 6 : 8)
 #endif
 
 #ifndef MRAFT_FOLD_EXP
@@ -775,6 +776,9 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #endif
 #ifndef MRAFT_FSCAN_W
 #define MRAFT_FSCAN_W 4     // replies per k_fold_scan wave
+#endif
+#ifndef MRAFT_FOLD_LONG_SPLIT
+#define MRAFT_FOLD_LONG_SPLIT 1  // segments longer than a lane group go to k_fold_long (k_fold without the 64-lane path)
 #endif
 #ifndef MRAFT_FSCAN_U
 #define MRAFT_FSCAN_U 8     // k_fold_scan: dword loads per lane in flight (64·U terms per round trip; 4: +7 %)
@@ -1078,7 +1082,8 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
                                             int64_t n_seg, const int32_t *__restrict__ seg_err,
                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                            int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
+                                            int4 *__restrict__ pend, unsigned *__restrict__ pcount,
+                                            unsigned *__restrict__ lcount, int64_t *__restrict__ llist) {
   constexpr int NG = 64 / GW;
   static_assert(GW >= P && GW >= 7, "a group holds the replica's match / next rows and seven scalars");
   const int lane = lane_id(), gl = lane & (GW - 1);
@@ -1091,8 +1096,21 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     e = seg_begin ? seg_begin[sg + 1] : sg + 1;
     bad = seg_err[sg];  // the claim verdict: a bad segment's slot may be out of range
   }
-  const int cnt = (int)(e > b ? min(e - b, (int64_t)(GW + 1)) : 0);  // 0: nothing to fold (empty or inverted)
-  if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
+  int cnt = (int)(e > b ? min(e - b, (int64_t)(GW + 1)) : 0);  // 0: nothing to fold (empty or inverted)
+  if constexpr (MRAFT_FOLD_LONG_SPLIT) {
+    // a segment longer than a group goes to k_fold_long's list (64-lane
+    // path, its own launch: this kernel stays at 8 waves per SIMD); its
+    // group folds nothing here
+    const unsigned long long lm = __ballot(gl == 0 && cnt > GW);
+    if (lm) {
+      const int l0 = first_lane(lm);
+      unsigned base = 0;
+      if (lane == l0) base = atomicAdd(lcount, (unsigned)__popcll(lm));
+      base = (unsigned)__shfl((int)base, l0, 64);
+      if (gl == 0 && cnt > GW) llist[base + (unsigned)__popcll(lm & ((1ull << lane) - 1))] = sg;
+    }
+    if (cnt > GW) cnt = 0;
+  } else if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
     for (int j = 0; j < NG; ++j)
       if (sg0 + j < n_seg)
         fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend, pcount);
@@ -1237,22 +1255,39 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
                                              int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
-  if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
-    const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
-    const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
-    return;
-  }
+                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount,
+                                             unsigned *__restrict__ lcount, int64_t *__restrict__ llist) {
   if constexpr (MRAFT_FOLD_GROUP > 1) {
+    // lane groups of GW lanes, one segment each (fold_groupw); with
+    // MRAFT_FOLD_LONG_SPLIT the 64-lane path is not in this kernel at all
     constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
     for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
       fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
-                         pcount);
-    return;
+                         pcount, lcount, llist);
+  } else if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
+    const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
+    const int64_t sg = x * per + min(x, rem) + (b >> 3);
+    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
+  } else {
+    for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
+      fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
   }
-  for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
+}
+
+// The segments k_fold left for the 64-lane path (longer than a lane group:
+// more replies than GW in one batch), wave per segment over its list.
+template <int P>
+__global__ __launch_bounds__(64, 8) void k_fold_long(Dev s, const mraft_ae_result *__restrict__ items,
+                                                     const int64_t *__restrict__ seg_begin,
+                                                     const int32_t *__restrict__ seg_err,
+                                                     const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                                     int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                                     int4 *__restrict__ pend, unsigned *__restrict__ pcount,
+                                                     const unsigned *__restrict__ lcount,
+                                                     const int64_t *__restrict__ llist) {
+  const int64_t cnt = (int64_t)*lcount;
+  for (int64_t k = blockIdx.x; k < cnt; k += gridDim.x)
+    fold_segment<P>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err, pend, pcount);
 }
 
 // ---------------------------------------------------------------- Start
@@ -1824,11 +1859,14 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   if (nt <= 0) return;
   const bool split = MRAFT_FOLD_SPLIT;  // the ABI always passes scan_buf
   if (split && !scan_buf) return;
+  // scan_buf: pend [2 int4 per reply] | pcount | lcount | llist [n_seg int64]
   int4 *pend = split ? (int4 *)scan_buf : nullptr;                          // 2 int4 per pending reply
-  unsigned *pcount = split ? (unsigned *)(pend + 2 * n) : nullptr;          // the list's length
+  unsigned *pcount = split ? (unsigned *)(pend + 2 * n) : nullptr;          // the a1 list's length
+  unsigned *lcount = (unsigned *)((int4 *)scan_buf + 2 * n) + 1;            // the long-segment list's length
+  int64_t *llist = (int64_t *)((int4 *)scan_buf + 2 * n + 1);
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
-                     epoch, seg_err, n, flags, item_err, pcount);
+                     epoch, seg_err, n, flags, item_err, pcount, lcount);
   if (n_seg <= 0) return;
   const int64_t waves = (n_seg + MRAFT_FOLD_GROUP - 1) / MRAFT_FOLD_GROUP;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
@@ -1836,7 +1874,10 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
 #define MRAFT_FOLD_CASE(PP)                                                                   \
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err, pend, pcount);                                        \
+                       flags, item_err, pend, pcount, lcount, llist);                         \
+    if (MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1)                                        \
+      hipLaunchKernelGGL(k_fold_long<PP>, dim3((unsigned)min(n_seg, (int64_t)4096)), bl, 0, st, s, items,  \
+                         seg_begin, seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist); \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
@@ -1850,8 +1891,9 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
                        dim3(64), 0, st, s, pend, pcount, flags);
 }
 
-size_t fold_scan_bytes(int64_t n) {
-  return n <= 0 ? 48 : (2 * sizeof(int4) + sizeof(int32_t)) * (size_t)n;
+size_t fold_scan_bytes(int64_t n, int64_t n_seg) {
+  // pend records, two counters, the long-segment list
+  return 2 * sizeof(int4) * (size_t)(n > 0 ? n : 0) + sizeof(int4) + sizeof(int64_t) * (size_t)(n_seg > 0 ? n_seg : 1);
 }
 
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,

@@ -27,6 +27,18 @@ for st in ${DO:-tests bench}; do
       timeout -k 10 600 python3 -u bench.py $args > "$OUT/$st.json" 2> "$OUT/$st.err"
       rc=$?; tail -2 "$OUT/$st.err"; [ $rc -eq 0 ] || exit 1
       python3 tools/summarize_bench.py "$OUT/$st.json" ;;
+    abmsg)
+      # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
+      echo "== abmsg $VARIANTS"
+      # (variants prebuilt here with tools/build_variants.sh travel in tools/variants/)
+      [ -z "${VARIANTS:-}" ] || { (cd tools && eval "bash build_variants.sh $VARIANTS") > "$OUT/variants_build.log" 2>&1 || { tail -5 "$OUT/variants_build.log"; exit 1; }; }
+      for pass in 1 2; do
+        for lib in tools/variants/*.so in-tree; do
+          if [ "$lib" = in-tree ]; then unset MRAFT_LIB; else export MRAFT_LIB=$PWD/$lib; fi
+          timeout -k 10 300 python3 tools/ab_message_path.py >> "$OUT/abmsg.jsonl" 2>> "$OUT/abmsg.err" || { tail -5 "$OUT/abmsg.err"; exit 1; }
+        done
+      done
+      unset MRAFT_LIB; cat "$OUT/abmsg.jsonl" ;;
     pmc)
       # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
       echo "== pmc ${BENCH_EXTRA:-}"
