@@ -63,6 +63,34 @@ void ora_count_result(int64_t out[2]) {
   }
 }
 
+/* The same counts at a memory-line granularity: the lines (line_words int32
+ * words each, counted from the start of every array — the device allocates
+ * each array line-aligned and each log row is a whole number of lines) that
+ * hold at least one counted word. out = {read lines, written lines} in
+ * lines. Used to split measured HBM traffic into line granularity and
+ * re-reads (tools/line_bound.py). */
+void ora_count_result_lines(int32_t line_words, int64_t out[2]) {
+  out[0] = out[1] = 0;
+  if (!cnt.rd || line_words <= 0) return;
+  for (int a = 0; a < A_COUNT; ++a) {
+    for (int64_t l = cnt.base[a]; l < cnt.base[a + 1]; l += line_words) {
+      int64_t e = l + line_words < cnt.base[a + 1] ? l + line_words : cnt.base[a + 1];
+      int r = 0, w = 0;
+      for (int64_t i = l; i < e && !(r && w); ++i) {
+        r |= (int)((cnt.rd[i >> 6] >> (i & 63)) & 1);
+        w |= (int)((cnt.wr[i >> 6] >> (i & 63)) & 1);
+      }
+      out[0] += r;
+      out[1] += w;
+    }
+  }
+}
+
+/* The bitmaps themselves (read: write = 0, written: write = 1), bit i of
+ * array a at ora_count_base(a) + i; ora_count_base(A_COUNT) = total words. */
+const uint64_t *ora_count_bits(int32_t write) { return write ? cnt.wr : cnt.rd; }
+int64_t ora_count_base(int32_t a) { return (a >= 0 && a <= A_COUNT) ? cnt.base[a] : -1; }
+
 static inline void CR(int a, int64_t i) {
   if (cnt.on) { int64_t w = cnt.base[a] + i; cnt.rd[w >> 6] |= 1ull << (w & 63); }
 }

@@ -39,6 +39,13 @@ int ora_count_enable(ora_engine *e);
 void ora_compute_terms_sorted(ora_engine *e);
 void ora_count_disable(void);
 void ora_count_result(int64_t out_words[2]);
+/* Lines of line_words words holding a counted word: {read, written}. */
+void ora_count_result_lines(int32_t line_words, int64_t out_lines[2]);
+/* The bitmaps (write = 0: read words) and each array's first bit; arrays in
+ * the order term, voted, role, commit, applied, dummy, last, votes, log,
+ * match, next, terms_sorted; ora_count_base(12) = total bits. */
+const uint64_t *ora_count_bits(int32_t write);
+int64_t ora_count_base(int32_t a);
 
 int ora_gather_append_args(ora_engine *e, const int32_t *slots,
                            const int32_t *peers, int64_t n,

@@ -31,6 +31,7 @@ def lib():
         E = ctypes.POINTER(OraEngine)
         sigs = {
             "ora_count_enable": [E], "ora_count_disable": [], "ora_count_result": [vp],
+            "ora_count_result_lines": [i32, vp],
             "ora_compute_terms_sorted": [E],
             "ora_gather_append_args": [E, vp, vp, i64, vp, vp],
             "ora_handle_append_entries": [E, vp, i64, vp, i64, vp, vp],
@@ -61,7 +62,7 @@ def lib():
         for n, a in sigs.items():
             f = getattr(l, n)
             f.argtypes = a
-            f.restype = None if n in ("ora_count_disable", "ora_count_result", "goshape_store",
+            f.restype = None if n in ("ora_count_disable", "ora_count_result", "ora_count_result_lines", "goshape_store",
                                       "goshape_free", "goshape_reset", "ora_compute_terms_sorted") else ctypes.c_int
         l.goshape_build.restype = ctypes.c_void_p
         l.goshape_tick.restype = ctypes.c_int64
@@ -94,18 +95,26 @@ class Oracle:
             lib().ora_replicate_tick(ctypes.byref(self._e), ptr(lp), ptr(gf))
         return gf
 
-    def replicate_tick_count(self, leader_peer):
-        """Counts on a scratch copy (the state is left untouched)."""
+    def replicate_tick_count(self, leader_peer, line_words=()):
+        """Counts on a scratch copy (the state is left untouched). With
+        line_words, also {line_words: (read lines, written lines)}."""
         scratch = Oracle(self.G, self.P, self.L, self.st)
         L = lib()
         L.ora_count_enable(ctypes.byref(scratch._e))
+        lines = {}
         try:
             gf = scratch.replicate_tick(leader_peer)
             out = (ctypes.c_int64 * 2)()
             L.ora_count_result(out)
+            for lw in line_words:
+                o2 = (ctypes.c_int64 * 2)()
+                L.ora_count_result_lines(lw, o2)
+                lines[lw] = (int(o2[0]), int(o2[1]))
         finally:
             L.ora_count_disable()
         active = int(np.count_nonzero(gf & 1))
+        if line_words:
+            return int(out[0]), int(out[1]), active, lines
         return int(out[0]), int(out[1]), active
 
     def gather_append_args(self, slots, peers):

@@ -29,7 +29,7 @@ for st in ${DO:-tests bench}; do
       python3 tools/summarize_bench.py "$OUT/$st.json" ;;
     abmsg)
       # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
-      echo "== abmsg $VARIANTS"
+      echo "== abmsg ${VARIANTS:-prebuilt}"
       # (variants prebuilt here with tools/build_variants.sh travel in tools/variants/)
       [ -z "${VARIANTS:-}" ] || { (cd tools && eval "bash build_variants.sh $VARIANTS") > "$OUT/variants_build.log" 2>&1 || { tail -5 "$OUT/variants_build.log"; exit 1; }; }
       for pass in 1 2; do
