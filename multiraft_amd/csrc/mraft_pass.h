@@ -77,6 +77,35 @@ __device__ __forceinline__ void st1(int32_t *p, int a) {
   if (MRAFT_TICK_NT & 1) __builtin_nontemporal_store(a, p);
   else *p = a;
 }
+// EPL entries (4 or 2) of one lane: one dwordx4 or dwordx2 access.
+template <int EPL>
+__device__ __forceinline__ void ldv(const int32_t *p, int (&x)[EPL]) {
+  if constexpr (EPL == 4) {
+    const int4 v = ld4(p);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+    const int2 *q = reinterpret_cast<const int2 *>(p);
+    if (MRAFT_TICK_NT & 2) {
+      x[0] = __builtin_nontemporal_load(&q->x); x[1] = __builtin_nontemporal_load(&q->y);
+    } else {
+      const int2 v = *q;
+      x[0] = v.x; x[1] = v.y;
+    }
+  }
+}
+template <int EPL>
+__device__ __forceinline__ void stv(int32_t *p, const int (&x)[EPL]) {
+  if constexpr (EPL == 4) {
+    st4(p, x[0], x[1], x[2], x[3]);
+  } else {
+    int2 *q = reinterpret_cast<int2 *>(p);
+    if (MRAFT_TICK_NT & 1) {
+      __builtin_nontemporal_store(x[0], &q->x); __builtin_nontemporal_store(x[1], &q->y);
+    } else {
+      *q = make_int2(x[0], x[1]);
+    }
+  }
+}
 
 // The followers a pass serves, with as little wave-uniform state as the pass
 // needs (it is live across the whole streaming loop; at 8 waves per SIMD every
@@ -252,52 +281,55 @@ __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int 
   }
 }
 
-// The compare chunks of the pass (VEC, 256 entries per chunk) software-
-// pipelined: chunk c is compared, then chunk c+256's loads (the leader's
-// entries and the words of every follower still comparing after chunk c) are
-// issued, then chunk c's stores, so the wave waits for the next loads without
-// waiting for its own stores (vmcnt counts both, in order). No word is loaded
-// that pass_chunk would not load. Runs while some follower compares; returns
-// the first chunk not processed (the copy-only loop continues there).
-template <bool COUNT, class Src, class F>
+// The compare chunks of the pass (VEC, 64 * EPL entries per chunk: EPL = 4,
+// one dwordx4 per lane and stream, or 2, one dwordx2) software-pipelined:
+// chunk c is compared, then chunk c+CW's loads (the leader's entries and the
+// words of every follower still comparing after chunk c) are issued, then
+// chunk c's stores, so the wave waits for the next loads without waiting for
+// its own stores (vmcnt counts both, in order). No word is loaded that
+// pass_chunk would not load at the same chunk width; a follower's terms past
+// its first mismatch are read up to the end of that chunk (the smaller EPL,
+// the fewer: DESIGN.md §5 overfetch account). Runs while some follower
+// compares; returns the first chunk not processed (the copy-only loop
+// continues there; c stays on the leader row's line grid for EPL >= 2 and
+// the caller's 32-entry chunk origin).
+template <bool COUNT, int EPL = 4, class Src, class F>
 __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int slo, int shi, int T, int &found,
                                          int c, int plo, int phi) {
   constexpr int NI = F::kNI;
-  constexpr int CW = 256;
+  constexpr int CW = 64 * EPL;
   const int lane = lane_id();
-  int e[4], f[NI][4];
-  auto load = [&](int cc, int (&ee)[4], int (&ff)[NI][4]) {
-    const int i0 = cc + 4 * lane;
-    int4 x = make_int4(0, 0, 0, 0);
-    if (i0 + 3 >= plo && i0 <= phi) x = ld4(src.at(i0));
-    ee[0] = x.x; ee[1] = x.y; ee[2] = x.z; ee[3] = x.w;
+  int e[EPL], f[NI][EPL];
+  auto load = [&](int cc, int (&ee)[EPL], int (&ff)[NI][EPL]) {
+    const int i0 = cc + EPL * lane;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) ee[u] = 0;
+    if (i0 + EPL - 1 >= plo && i0 <= phi) ldv<EPL>(src.at(i0), ee);
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
-      ff[q][0] = ff[q][1] = ff[q][2] = ff[q][3] = 0;
+#pragma unroll
+      for (int u = 0; u < EPL; ++u) ff[q][u] = 0;
       if (!fo.is_cmp(q) || fo.start[q] > cc + CW - 1 || fo.cend[q] <= cc) continue;
-      if (i0 + 3 >= fo.start[q] && i0 < fo.cend[q]) {
-        const int4 y = ld4(fo.at(q, i0));
-        ff[q][0] = y.x; ff[q][1] = y.y; ff[q][2] = y.z; ff[q][3] = y.w;
-      }
+      if (i0 + EPL - 1 >= fo.start[q] && i0 < fo.cend[q]) ldv<EPL>(fo.at(q, i0), ff[q]);
     }
   };
   load(c, e, f);
   for (;;) {
-    const int i0 = c + 4 * lane;
+    const int i0 = c + EPL * lane;
     // compare: first mismatch of every follower still comparing
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       if (!fo.is_cmp(q) || fo.start[q] > c + CW - 1) continue;
       int im = -1;
       if (fo.cend[q] > c) {
-        int first = 4;
+        int first = EPL;
 #pragma unroll
-        for (int u = 3; u >= 0; --u)
+        for (int u = EPL - 1; u >= 0; --u)
           if (i0 + u >= fo.start[q] && i0 + u < fo.cend[q] && e[u] != f[q][u]) first = u;
-        const unsigned long long m = __ballot(first < 4);
+        const unsigned long long m = __ballot(first < EPL);
         if (m) {
           const int l = first_lane(m);
-          im = c + 4 * l + __shfl(first, l, 64);
+          im = c + EPL * l + __shfl(first, l, 64);
         }
       }
       if (im < 0 && fo.cend[q] <= c + CW - 1) {
@@ -310,27 +342,27 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
     if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
       int lu = -1;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < EPL; ++u)
         if (i0 + u >= slo && i0 + u <= shi && e[u] == T) lu = u;
       const unsigned long long m = __ballot(lu >= 0);
       if (m) {
         const int l = 63 - __clzll((long long)m);
-        found = c + 4 * l + __shfl(lu, l, 64);
+        found = c + EPL * l + __shfl(lu, l, 64);
       }
     }
     const int cn = c + CW;
     const bool more = cn <= phi && fo.cmp;
-    int en[4];
+    int en[EPL];
     if (more) load(cn, en, f);
     if (!COUNT) {
 #pragma unroll
       for (int q = 0; q < NI; ++q) {
         if (!fo.is_copy(q) || fo.start[q] > c + CW - 1) continue;
-        if (i0 >= fo.cfrom[q] && i0 + 3 < nend) {
-          st4(fo.at(q, i0), e[0], e[1], e[2], e[3]);
+        if (i0 >= fo.cfrom[q] && i0 + EPL - 1 < nend) {
+          stv<EPL>(fo.at(q, i0), e);
         } else {
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < EPL; ++u)
             if (i0 + u >= fo.cfrom[q] && i0 + u < nend) st1(fo.at(q, i0 + u), e[u]);
         }
       }
@@ -341,7 +373,7 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
     if (!more) return cn;
     c = cn;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = en[u];
+    for (int u = 0; u < EPL; ++u) e[u] = en[u];
   }
 }
 

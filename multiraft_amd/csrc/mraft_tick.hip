@@ -210,6 +210,9 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #ifndef MRAFT_TICK_SCANU
 #define MRAFT_TICK_SCANU 1  // ConflictIndex scans past the probe: 64 * SCANU terms per round trip
 #endif
+#ifndef MRAFT_TICK_CMP_EPL
+#define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
+#endif
 #ifndef MRAFT_PASS_PIPE
 #define MRAFT_PASS_PIPE 1   // compare chunks software-pipelined (next chunk's loads before this chunk's stores)
 #endif
@@ -482,7 +485,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (vec) {
       int c = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
       if (MRAFT_PASS_PIPE && V == 1) {
-        if (c <= phi && fo.cmp) c = pass_pipe<COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+        if (c <= phi && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
       } else {
         for (; c <= phi && fo.cmp; c += 256 * V)
           pass_chunk<V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);

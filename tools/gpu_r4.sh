@@ -39,6 +39,11 @@ for st in ${DO:-tests bench}; do
         done
       done
       unset MRAFT_LIB; cat "$OUT/abmsg.jsonl" ;;
+    abtick)
+      # tick A/B with FETCH/WRITE passes (tools/ab_tick_pmc.sh; LIBS = variant tags)
+      echo "== abtick ${LIBS:-all}"
+      TAG=$TAG/abtick bash tools/ab_tick_pmc.sh > "$OUT/abtick.log" 2>&1; rc=$?
+      tail -40 "$OUT/abtick.log"; [ $rc -eq 0 ] || exit 1 ;;
     pmc)
       # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
       echo "== pmc ${BENCH_EXTRA:-}"
