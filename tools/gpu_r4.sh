@@ -44,6 +44,12 @@ for st in ${DO:-tests bench}; do
       echo "== abtick ${LIBS:-all}"
       TAG=$TAG/abtick bash tools/ab_tick_pmc.sh > "$OUT/abtick.log" 2>&1; rc=$?
       tail -40 "$OUT/abtick.log"; [ $rc -eq 0 ] || exit 1 ;;
+    tracemsg)
+      # message-path device timeline (tools/timeline.py): busy / idle / overlap per gated section
+      echo "== tracemsg"
+      timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/msgkt" -o msgkt -- python3 tools/ab_message_path.py \
+        > "$OUT/msgkt.json" 2> "$OUT/msgkt.err" || { tail -5 "$OUT/msgkt.err"; exit 1; }
+      python3 tools/timeline.py "$OUT/msgkt" "$OUT/timeline.json" > /dev/null && python3 -c "import json; [print({k: v for k, v in s.items() if k != 'per_kernel'}) for s in json.load(open('$OUT/timeline.json'))]" ;;
     pmc)
       # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
       echo "== pmc ${BENCH_EXTRA:-}"
