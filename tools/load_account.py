@@ -12,6 +12,9 @@ measured — and the union is rounded to lines. Two load patterns over-read:
   ([max(prev-64, dummy+2), prev-1]), then 64-term windows further down,
   however short the run of equal terms is.
 
+Also: the lines of the header's single-word log reads that the pass streams
+again (a second fetch when L2 has dropped them in between).
+
 Prints the line-granular reads (32 / 64 / 128 B) of the algorithmic words
 alone and with each pattern added, beside the PMC reads
 (profiles/pmc_traffic_s2.json).
@@ -159,6 +162,23 @@ def main():
     w1, o1 = words_of(wl, hi + 1)
     scan_words = pos(f[si][o1], w1)
 
+    # header single-word reads (leader log[prev] of every item, follower
+    # log[prev] inside its log, the leader's log[last]) whose lines the pass
+    # streams again later: fetched twice when L2 drops them in between
+    hdr = np.concatenate([pos(il, prev), pos(f[inside], prev[inside]), pos(ldl, last[ldl].astype(np.int64))])
+    gm = np.unique(ig[mi])
+    lsl = gm * P + lp[gm]
+    w_l, o_l = words_of(plo[gm], last[lsl].astype(np.int64) + 1)
+    e_f = np.where(m < cend, np.minimum(cend, cend_chunk), cend)
+    w_f, o_f = words_of(start, e_f)
+    pass_words = np.concatenate([pos(lsl[o_l], w_l), pos(f[mi][o_f], w_f), scan_words])
+    header_lines = {}
+    for lw in (8, 16, 32):
+        hl = np.unique(hdr // lw)
+        header_lines[str(4 * lw)] = {"header_line_bytes": 4 * lw * len(hl),
+                                     "also_streamed_by_the_pass": 4 * lw * len(np.intersect1d(hl, np.unique(pass_words // lw)))}
+    del pass_words
+
     def lines(extra, lw):
         b = alg_log.copy()
         for e in extra:
@@ -170,7 +190,7 @@ def main():
            "merges_with_mismatch": int((m < cend).sum()),
            "compare_overread_words": int(len(cmp_words)),
            "scans": int(len(si)), "scan_words_loaded": int(len(scan_words)),
-           "lines": {}}
+           "header_lines": header_lines, "lines": {}}
     for lw in (8, 16, 32):
         a = lines([], lw)
         c = lines([cmp_words], lw)
