@@ -1,6 +1,7 @@
 """The config #3 message path alone (bench.message_path: one pipeline with the
 per-call split, and two shard pipelines), for A/B runs of library variants
-(MRAFT_LIB=tools/variants/libmraft_hip_<tag>.so python tools/ab_message_path.py).
+(MRAFT_LIB=tools/variants/libmraft_hip_<tag>.so python tools/ab_message_path.py;
+SHARDS=2,3 also times three pipelines).
 Prints one JSON line."""
 import json
 import os
@@ -26,9 +27,12 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     one = bench.message_path(master, copies, lp, G, P, L, dev, 1, 8)
-    two = bench.message_path(master, copies, lp, G, P, L, dev, 2, copies_n - 1)
-    print(json.dumps({"lib": os.environ.get("MRAFT_LIB", "in-tree"), "ms_per_call": one["ms_per_call"],
-                      "one_pipeline_ms": one["device_ms_per_step"], "two_pipelines_ms": two["device_ms_per_step"]}))
+    out = {"lib": os.environ.get("MRAFT_LIB", "in-tree"), "ms_per_call": one["ms_per_call"],
+           "one_pipeline_ms": one["device_ms_per_step"]}
+    for S in [int(x) for x in os.environ.get("SHARDS", "2").split(",")]:
+        r = bench.message_path(master, copies, lp, G, P, L, dev, S, copies_n - 1)
+        out["two_pipelines_ms" if S == 2 else f"pipelines_{S}_ms"] = r["device_ms_per_step"]
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
