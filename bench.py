@@ -266,6 +266,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     # -- message-level path, config #3
     one = message_path(master, copies, lp, G, P, L, dev, 1, steps, words=True)
     two = message_path(master, copies, lp, G, P, L, dev, 2, len(copies) - 1)
+    three = message_path(master, copies, lp, G, P, L, dev, 3, len(copies) - 1)
     hw, fw, ms = one["hw"], one["fw"], one["ms_per_call"]
     n = 4 * int((lp >= 0).sum())
     step_ms = ms["gather"] + ms["handle"] + ms["fold"]
@@ -284,6 +285,11 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                      "steps": two["steps"], "device_ms_per_step": two["device_ms_per_step"],
                      "decisions_per_s": G / (two["device_ms_per_step"] / 1e3),
                      "vs_headline": two["device_ms_per_step"] / headline_ms},
+        "shards_3": {"what": "as shards_2 with three pipelines (a third of the groups each; three engine queues "
+                             "and torch's, which idles in the timed region: GPU_MAX_HW_QUEUES = 4)",
+                     "steps": three["steps"], "device_ms_per_step": three["device_ms_per_step"],
+                     "decisions_per_s": G / (three["device_ms_per_step"] / 1e3),
+                     "vs_headline": three["device_ms_per_step"] / headline_ms},
         "one_pipeline_device_ms_per_step": one["device_ms_per_step"],
         "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
