@@ -210,6 +210,13 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #ifndef MRAFT_TICK_SCANU
 #define MRAFT_TICK_SCANU 1  // ConflictIndex scans past the probe: 64 * SCANU terms per round trip
 #endif
+#ifndef MRAFT_TICK_TAIL_HOIST
+#define MRAFT_TICK_TAIL_HOIST 0  // phase C uses the header's terms_sorted / dummy words (no reload after the pass)
+#endif
+#ifndef MRAFT_TICK_PDIRTY
+#define MRAFT_TICK_PDIRTY 0  // follower persist marks: 0 = load-OR-store at the end, 1 = non-returning
+                             // atomic OR, 2 = the word loaded with the header, stored at the end
+#endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
 #endif
@@ -290,6 +297,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const int p = lane < lp ? lane : lane + 1;
   const long long f = (long long)g * P + p;
   int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
+  int fpd = 0;  // MRAFT_TICK_PDIRTY == 2: this lane's follower's persist word
   if (lane < NI) {
     nxt = s.next[ld * P + p];
     fterm = s.term[f];
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     flast = s.last[f];
     fcommit = s.commit[f];
     fhead = s.head[f];
+    if (MRAFT_TICK_PDIRTY == 2 && !COUNT && s.pdirty) fpd = s.pdirty[f];
   }
   long long hR = 1;  // algorithmic words of the header (wave-uniform)
   if (role != kLeader || c0 < ldummy) {
@@ -422,6 +431,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
   }
 
+  // prev == the follower's dummy, for phase C's terms_sorted rule (a ballot:
+  // no per-lane word kept live across the pass)
+  const unsigned long long pd_m = MRAFT_TICK_TAIL_HOIST ? __ballot(prev == fdummy) : 0ull;
   // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
   Fol<NI> fo;
@@ -540,7 +552,12 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   int fcadv = 0;
   long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
   if (icls >= IC_STALE && icls <= IC_HB) {
-    if (!COUNT) mark_persist(s2, f, MRAFT_PERSIST_STATE);                 // deferred :111
+    if (!COUNT) {                                                         // deferred :111
+      if (MRAFT_TICK_PDIRTY == 0) mark_persist(s2, f, MRAFT_PERSIST_STATE);
+      else if (MRAFT_TICK_PDIRTY == 1 && s2.pdirty)
+        (void)__hip_atomic_fetch_or(&s2.pdirty[f], MRAFT_PERSIST_STATE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (s2.pdirty) s2.pdirty[f] = fpd | MRAFT_PERSIST_STATE;
+    }
     if (icls == IC_STALE) {
       cR = 1;
     } else {
@@ -566,10 +583,11 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
             // flag (prevLogTerm, entries sorted: the leader's proof, with the
             // dummy's term compared explicitly), or the new entries are the
             // whole log when that Index is the dummy's successor
-            bool fl = s2.srt[ld] != 0;
+            bool fl = (MRAFT_TICK_TAIL_HOIST ? lsrt : s2.srt[ld]) != 0;
             if (fl && prev == ldummy)
               fl = s2.log[lrow + ring(prev + lb, L)] <= s2.log[lrow + ring(prev + 1 + lb, L)];
-            const int sw = !fl ? 0 : (mk == 0 && prev == s2.dummy[f]) ? 1 : -1;
+            const bool at_dummy = MRAFT_TICK_TAIL_HOIST ? ((pd_m >> lane) & 1) != 0 : prev == s2.dummy[f];
+            const int sw = !fl ? 0 : (mk == 0 && at_dummy) ? 1 : -1;
             if (sw >= 0) {
               if (!COUNT) s2.srt[f] = sw;
               cW += 1;
@@ -587,9 +605,12 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   }
   if (icls >= IC_IS_STALE && icls <= IC_IS_INSTALL) {
     cR = 1;                                                              // term
-    if (!COUNT)
-      mark_persist(s2, f, (adopt ? MRAFT_PERSIST_STATE : 0) |            // raft_snapshot.go:26
-                             (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0));  // :47
+    if (!COUNT) {
+      const int bits = (adopt ? MRAFT_PERSIST_STATE : 0) |                 // raft_snapshot.go:26
+                       (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0);  // :47
+      if (MRAFT_TICK_PDIRTY == 2) { if (s2.pdirty && bits) s2.pdirty[f] = fpd | bits; }
+      else mark_persist(s2, f, bits);
+    }
     if (icls != IC_IS_STALE) {
       if (!COUNT) {
         if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
