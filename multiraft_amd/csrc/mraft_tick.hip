@@ -215,8 +215,9 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #endif
 #ifndef MRAFT_TICK_PDIRTY
 #define MRAFT_TICK_PDIRTY 0  // follower persist marks: 0 = load-OR-store at the end, 1 = non-returning
-                             // atomic OR, 2 = the word loaded with the header, stored at the end,
-                             // 3 = a byte store (timing experiment: needs STATE alone in byte 0)
+                             // atomic OR, 2 = the word loaded with the header, stored at the end
+                             // (r4_v7: 1 no faster; 2 spills; a byte store with STATE alone in byte 0,
+                             // r4_v8, within noise)
 #endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
@@ -557,8 +558,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       if (MRAFT_TICK_PDIRTY == 0) mark_persist(s2, f, MRAFT_PERSIST_STATE);
       else if (MRAFT_TICK_PDIRTY == 1 && s2.pdirty)
         (void)__hip_atomic_fetch_or(&s2.pdirty[f], MRAFT_PERSIST_STATE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (MRAFT_TICK_PDIRTY == 2 && s2.pdirty) s2.pdirty[f] = fpd | MRAFT_PERSIST_STATE;
-      else if (s2.pdirty) reinterpret_cast<volatile uint8_t *>(s2.pdirty + f)[0] = 1;  // 3: timing experiment
+      else if (s2.pdirty) s2.pdirty[f] = fpd | MRAFT_PERSIST_STATE;
     }
     if (icls == IC_STALE) {
       cR = 1;
