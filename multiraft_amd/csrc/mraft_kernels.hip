@@ -410,6 +410,16 @@ __device__ __forceinline__ HsArgs reload_hs() {
   return k;
 }
 
+// The args half of a failed item's reply record (slot = peer = -1), built
+// where it is stored: as a plain constant the compiler kept it in four VGPRs
+// from the prologue on and spilled them (a 16-B scratch store per lane in
+// every wave of the main launch).
+__device__ __forceinline__ int4 no_record() {
+  int m = -1, z = 0;
+  asm volatile("" : "+v"(m), "+v"(z));
+  return make_int4(m, m, z, z);
+}
+
 template <int NI>
 __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int size) {
   const Dev &s = k0.s;
@@ -465,7 +475,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     // half follows with the reply. Failed items: slot = peer = -1.
     const int PP = s.P;
     int4 *rr = reinterpret_cast<int4 *>(k0.res + i);
-    rr[0] = live ? make_int4((f / PP) * PP + a.leader_id, f % PP, a.term, prev) : make_int4(-1, -1, 0, 0);
+    rr[0] = live ? make_int4((f / PP) * PP + a.leader_id, f % PP, a.term, prev) : no_record();
   }
   int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
   if (live) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
@@ -658,7 +668,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     // ConflictIndex); an item rejected after the prologue (capacity: cls
     // AE_DONE) gets slot = peer = -1 as well
     int4 *rr = reinterpret_cast<int4 *>(res + i);
-    if (cls == AE_DONE) rr[0] = make_int4(-1, -1, 0, 0);
+    if (cls == AE_DONE) rr[0] = no_record();
     rr[1] = cls >= AE_STALE ? make_int4(nn, r.term, r.success, r.conflict_index) : make_int4(0, 0, 0, 0);
   }
 }
