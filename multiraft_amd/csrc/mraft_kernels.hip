@@ -13,6 +13,15 @@ namespace {
 constexpr int kBlock = 256;
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// A pointer the wave holds in SGPRs where it is used (a per-lane address
+// hoisted out of a loop as a VGPR pair is what the register allocator spills).
+template <class T>
+__device__ __forceinline__ T *uni_ptr(T *p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return (T *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
 
 inline int blocks_for(int64_t n, int per_block = kBlock) {
   int64_t b = (n + per_block - 1) / per_block;
@@ -1128,7 +1137,14 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   }
   (void)n_items;
   mraft_ae_result it{};
-  if (gl < cnt) it = items[b + gl];
+  if (gl < cnt) {
+    // 32-bit lane offset from an SGPR base, formed here (see uni_ptr)
+    const int64_t b0 = (int64_t)(((uint64_t)(uint32_t)uni((int)((uint64_t)b >> 32)) << 32) |
+                                 (uint32_t)uni((int)(uint32_t)(uint64_t)b));  // lane 0's b
+    int64_t off = b - b0 + gl;
+    asm volatile("" : "+v"(off));
+    it = uni_ptr(items + b0)[off];
+  }
   const int slot = gw_bcast<GW>(it.slot, 0);
   const int me = cnt ? slot % P : 0;
   const int64_t mrow = (int64_t)slot * P;
