@@ -50,6 +50,14 @@ for st in ${DO:-tests bench}; do
       timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/msgkt" -o msgkt -- python3 tools/ab_message_path.py \
         > "$OUT/msgkt.json" 2> "$OUT/msgkt.err" || { tail -5 "$OUT/msgkt.err"; exit 1; }
       python3 tools/timeline.py "$OUT/msgkt" "$OUT/timeline.json" > /dev/null && python3 -c "import json; [print({k: v for k, v in s.items() if k != 'per_kernel'}) for s in json.load(open('$OUT/timeline.json'))]" ;;
+    pmcmsg)
+      # message-path HBM bytes per kernel (FETCH_SIZE / WRITE_SIZE passes, tools/pmc_msg.py)
+      echo "== pmcmsg"
+      for c in FETCH_SIZE WRITE_SIZE; do
+        SHARDS=2 timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$OUT/msgpmc_$c" -o p -- python3 tools/ab_message_path.py \
+          > "$OUT/msgpmc_$c.json" 2> "$OUT/msgpmc_$c.err" || { tail -5 "$OUT/msgpmc_$c.err"; exit 1; }
+      done
+      python3 tools/pmc_msg.py "$OUT/msgpmc_FETCH_SIZE" "$OUT/msgpmc_WRITE_SIZE" "$OUT/msgpmc.json" ;;
     pmc)
       # FETCH_SIZE / WRITE_SIZE passes of the bench (BENCH_EXTRA) + calibration -> profiles/pmc_traffic*.json
       echo "== pmc ${BENCH_EXTRA:-}"
