@@ -219,6 +219,11 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
                              // (r4_v7: 1 no faster; 2 spills; a byte store with STATE alone in byte 0,
                              // r4_v8, within noise)
 #endif
+#ifndef MRAFT_TICK_LATE
+#define MRAFT_TICK_LATE 0  // 1: the ConflictIndex scans run after the pass (their inputs parked in LDS), and with
+                           // the terms_sorted proof a1's top-term probe is only issued before it (no round
+                           // trip of either between the header and the pass)
+#endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
 #endif
@@ -389,31 +394,31 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
 
   // ------------------------------------------------------------ phase B
   int scan_extra = 0;
-  {
-    unsigned long long m = __ballot(icls == IC_SCAN);
-    if (MRAFT_TICK_EXP >= 2) m = 0;
-    // ConflictIndex scans (:136-142): the first 64 terms below prev of every
-    // scanning follower in one round trip (most runs end there), then each
-    // longer run on its own, 64 * MRAFT_TICK_SCANU terms per round trip (64
-    // measured 1.4 % faster than 256: fewer lines fetched past the run's end
-    // outweigh the extra round trips).
+  // ConflictIndex scans (:136-142): the first 64 terms below prev of every
+  // scanning follower in one round trip (most runs end there), then each
+  // longer run on its own, 64 * MRAFT_TICK_SCANU terms per round trip (64
+  // measured 1.4 % faster than 256: fewer lines fetched past the run's end
+  // outweigh the extra round trips). Nothing before phase D reads their
+  // result (the fold does not use ConflictIndex), so MRAFT_TICK_LATE runs
+  // them after the pass.
+  auto conflict_scans = [&](const int32_t *__restrict__ logp, unsigned long long m, int qdummy, int qhead, int qft) {
     int pv[NI];
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       pv[q] = 0;
       if ((m >> q) & 1) {
         const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
-                  sh = uni(__shfl(fhead, q, 64));
-        pv[q] = s.log[sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L)];  // prev >= dummy + 2: readable
+        const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
+                  sh = uni(__shfl(qhead, q, 64));
+        pv[q] = logp[sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L)];  // prev >= dummy + 2: readable
       }
     }
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       if ((m >> q) & 1) {
         const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(fdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(ft, q, 64)),
-                  sh = uni(__shfl(fhead, q, 64));
+        const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(qft, q, 64)),
+                  sh = uni(__shfl(qhead, q, 64));
         const int lo = sd + 2, hi = sp - 1;
         const unsigned long long mm = __ballot(hi - lane >= lo && pv[q] != sa);
         int ci;
@@ -422,7 +427,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         } else if (hi - 64 < lo) {
           ci = sd + 1;
         } else {
-          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU>(s.log + sf * L, sd, sh, L, lo, hi - 64, sa);
+          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
           ci = r < lo ? sd + 1 : r;
         }
         if (lane == q) {
@@ -431,7 +436,17 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         }
       }
     }
+  };
+  const unsigned long long scan_m = MRAFT_TICK_EXP >= 2 ? 0ull : __ballot(icls == IC_SCAN);
+#if MRAFT_TICK_LATE
+  __shared__ int late_stash[3][64 * MRAFT_TICK_WPB];  // the scans' per-lane inputs, parked across the pass
+  const int tid = (int)threadIdx.x;
+  if (scan_m) {
+    late_stash[0][tid] = fdummy; late_stash[1][tid] = fhead; late_stash[2][tid] = ft;
   }
+#else
+  if (scan_m) conflict_scans(s.log, scan_m, fdummy, fhead, ft);
+#endif
 
   // prev == the follower's dummy, for phase C's terms_sorted rule (a ballot:
   // no per-lane word kept live across the pass)
@@ -476,15 +491,23 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const int is_m = (int)__ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
   const int have0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
   const int succ0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
+  int late_t = 0, late_a1 = 0;  // MRAFT_TICK_LATE: a1's top term, read after the pass
   if (!maybe_full) {
     fd.run(T, lp, mm, have0, succ0, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
-        if (t == T) commit = top;
-        else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
-        else { slo = c0 + 1; shi = top - 1; }
+        if (MRAFT_TICK_LATE && lsrt && top != last) {
+          // with the proof the top term decides a1 unless it is above
+          // currentTerm: issued now, decided after the pass
+          late_t = s.log[lrow + ring(top + lb, L)];
+          late_a1 = 1;
+        } else {
+          const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
+          if (t == T) commit = top;
+          else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
+          else { slo = c0 + 1; shi = top - 1; }
+        }
       }
     }
   }
@@ -517,6 +540,20 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const Dev s2 = reload_dev();
 #else
   const Dev &s2 = s;
+#endif
+#if MRAFT_TICK_LATE
+  if (scan_m) conflict_scans(s2.log, scan_m, late_stash[0][tid], late_stash[1][tid], late_stash[2][tid]);
+  if (late_a1) {
+    const int t = uni(late_t);                                           // :98
+    if (t == T) {
+      commit = top;
+    } else if (t < T) {
+      settled = 1;
+    } else {  // above currentTerm: Go's downward scan (:95-104)
+      const int i = wave_scan_down_eq(s2.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
+      if (i > c0) commit = i;
+    }
+  }
 #endif
   int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
