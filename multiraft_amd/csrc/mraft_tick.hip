@@ -224,6 +224,9 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
                            // the terms_sorted proof a1's top-term probe is only issued before it (no round
                            // trip of either between the header and the pass)
 #endif
+#ifndef MRAFT_TICK_SCAN_NT
+#define MRAFT_TICK_SCAN_NT 0  // ConflictIndex scan words as non-temporal loads (read once, nothing else reads them)
+#endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
 #endif
@@ -410,7 +413,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         const long long sf = (long long)g * P + (q < lp ? q : q + 1);
         const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
                   sh = uni(__shfl(qhead, q, 64));
-        pv[q] = logp[sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L)];  // prev >= dummy + 2: readable
+        const int32_t *pp = logp + sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L);  // prev >= dummy + 2
+        pv[q] = MRAFT_TICK_SCAN_NT ? __builtin_nontemporal_load(pp) : *pp;
       }
     }
 #pragma unroll
@@ -427,7 +431,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         } else if (hi - 64 < lo) {
           ci = sd + 1;
         } else {
-          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
+          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU, MRAFT_TICK_SCAN_NT>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
           ci = r < lo ? sd + 1 : r;
         }
         if (lane == q) {
