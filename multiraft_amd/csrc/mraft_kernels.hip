@@ -1287,6 +1287,15 @@ __global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft
     // lane groups of GW lanes, one segment each (fold_groupw); with
     // MRAFT_FOLD_LONG_SPLIT the 64-lane path is not in this kernel at all
     constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
+    if (MRAFT_FOLD_XCD && (int64_t)gridDim.x * NG >= n_seg) {
+      // each XCD a contiguous range of waves: neighbouring waves' segments
+      // share the lines of the replica arrays in one L2
+      const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
+      const int64_t wb = x * per + min(x, rem) + (b >> 3);
+      fold_groupw<P, GW>(s, items, n_items, seg_begin, NG * wb, n_seg, seg_err, claim, epoch, flags, item_err, pend,
+                         pcount, lcount, llist);
+      return;
+    }
     for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
       fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
                          pcount, lcount, llist);
