@@ -291,6 +291,10 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                      "decisions_per_s": G / (three["device_ms_per_step"] / 1e3),
                      "vs_headline": three["device_ms_per_step"] / headline_ms},
         "one_pipeline_device_ms_per_step": one["device_ms_per_step"],
+        "vs_headline": min(two["device_ms_per_step"], three["device_ms_per_step"]) / headline_ms,
+        "vs_headline_what": "the message path's device time per step with the better of two and three shard "
+                            "pipelines, over the headline's ms_per_step on the same box (the calls one after "
+                            "another on one queue: calls_ms_sum_vs_headline)",
         "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,

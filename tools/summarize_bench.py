@@ -16,6 +16,8 @@ if "message_path_config3" in s:
     m = s["message_path_config3"]
     print("message path ms", m["ms_per_call"], "handle frac", round(m["roofline"]["frac"], 3),
           "fold frac", round(m["fold_roofline"]["frac"], 3))
+    print("message path pipelines: S=2", round(m["shards_2"]["vs_headline"], 3),
+          "S=3", round(m["shards_3"]["vs_headline"], 3) if "shards_3" in m else None, "x the headline")
 if "election_storm_config5" in s:
     e = s["election_storm_config5"]
     print("config5 ms", round(e["kernel_ms_mean"], 4), {k: v for k, v in e.items() if k == "roofline"})
