@@ -1,8 +1,9 @@
 """Per-kernel HBM bytes of the message path (tools/gpu_r4.sh pmcmsg: FETCH_SIZE
 and WRITE_SIZE passes over tools/ab_message_path.py), calibrated with the
 factors of profiles/pmc_traffic_s2.json. Per kernel: dispatches, and the
-average read / written MB per dispatch over all its dispatches of the most
-frequent grid size (the one-pipeline steps' launches are the largest grids).
+average read / written MB per dispatch over its dispatches of the largest
+grid size (the one-pipeline steps' full-batch launches; fixed-grid kernels
+average over every dispatch).
 
 Usage: python tools/pmc_msg.py <fetch_dir> <write_dir> [out.json]"""
 import csv
@@ -31,7 +32,6 @@ def per_kernel(d, counter):
     out = {}
     for k, xs in v.items():
         grids = [g for g, _ in xs]
-        mode = max(set(grids), key=grids.count)
         sel = [x for g, x in xs if g == max(grids)]
         out[k] = {"dispatches": len(xs), "grid_max": max(grids), "avg_at_grid_max": sum(sel) / len(sel)}
     return out
