@@ -753,6 +753,9 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #else
 #define FOLD_STAMP(k, dep) do {} while (0)
 #endif
+#ifndef MRAFT_FOLD_TAIL
+#define MRAFT_FOLD_TAIL 0  // 1: k_fold_long and k_fold_scan as one launch (k_fold_tail)
+#endif
 #ifndef MRAFT_FOLD_XCD
 #define MRAFT_FOLD_XCD 1  // XCD-contiguous segment ranges (r4_v18: fold call -8 %, reads 55 -> 46 MB)
 #endif
@@ -870,7 +873,7 @@ __device__ __forceinline__ void push_pending(int4 *__restrict__ pend, unsigned *
   }
 }
 
-template <int P>
+template <int P, bool PUSH = (MRAFT_FOLD_SPLIT != 0)>
 __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result *__restrict__ items,
                                              const int64_t *__restrict__ seg_begin, int64_t sg,
                                              const int32_t *__restrict__ seg_err,
@@ -978,7 +981,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
     if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
     const unsigned long long rm = __ballot(plo <= phi);  // replies whose evaluation has a range
-    if (MRAFT_FOLD_SPLIT) {
+    if (PUSH) {
       // probes here, scans in k_fold_scan (as fold_group4); with sorted terms
       // a top term below currentTerm settles the range (include/mraft.h)
       bool settled = false;
@@ -990,7 +993,7 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       push_pending(pend, pcount, plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled,
                    make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0),
                    make_int4(dummy, head, (int)(b + base + lane), 0));
-    } else if (MRAFT_FOLD_MERGED_PROBE && rm && !(rm & (rm - 1))) {
+    } else if (MRAFT_FOLD_MERGED_PROBE && !PUSH && rm && !(rm & (rm - 1))) {
       // One range (the usual batch): no separate probe of its top word — the
       // scan's first window starts there (one round trip fewer when the top
       // term is not currentTerm, a 1-KiB window instead of one word when it is).
@@ -1049,13 +1052,13 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
 // replies -> replica state -> probe). A hit sets MRAFT_F_COMMITTED on its reply
 // and raises the replica's commitIndex (atomicMax: several waves may hold
 // ranges of one segment).
-__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend,
-                                                     const unsigned *__restrict__ pcount,
-                                                     int32_t *__restrict__ flags) {
+__device__ __forceinline__ void fold_scan_blocks(const Dev &s, const int4 *__restrict__ pend,
+                                                 const unsigned *__restrict__ pcount, int32_t *__restrict__ flags,
+                                                 int64_t bid, int64_t nblk) {
   const int lane = lane_id();
   const int64_t cnt = (int64_t)*pcount;  // k_fold's compact list: nothing pending, nothing to do
   const int L = s.L;
-  for (int64_t b0 = (int64_t)blockIdx.x * MRAFT_FSCAN_W; b0 < cnt; b0 += (int64_t)gridDim.x * MRAFT_FSCAN_W) {
+  for (int64_t b0 = bid * MRAFT_FSCAN_W; b0 < cnt; b0 += nblk * MRAFT_FSCAN_W) {
     const int64_t i = b0 + lane;
     // the record in one round trip: {lo, hi, slot, currentTerm}, {dummy,
     // head, reply index}
@@ -1078,6 +1081,12 @@ __global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restri
       }
     }
   }
+}
+
+__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend,
+                                                     const unsigned *__restrict__ pcount,
+                                                     int32_t *__restrict__ flags) {
+  fold_scan_blocks(s, pend, pcount, flags, blockIdx.x, gridDim.x);
 }
 
 // Lane groups of GW lanes (the wave as 64 / GW groups).
@@ -1323,6 +1332,31 @@ __global__ __launch_bounds__(64, 8) void k_fold_long(Dev s, const mraft_ae_resul
   const int64_t cnt = (int64_t)*lcount;
   for (int64_t k = blockIdx.x; k < cnt; k += gridDim.x)
     fold_segment<P>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err, pend, pcount);
+}
+
+// k_fold_long and k_fold_scan as one launch (MRAFT_FOLD_TAIL): the first
+// n_long workgroups fold the long segments, scanning their own ranges (so
+// they push nothing), the rest scan the ranges k_fold left open. The two
+// halves touch different replicas (one segment per replica slot, the
+// claim), so they need no order between them: one kernel boundary fewer per
+// fold call.
+template <int P>
+__global__ __launch_bounds__(64, 8) void k_fold_tail(Dev s, const mraft_ae_result *__restrict__ items,
+                                                     const int64_t *__restrict__ seg_begin,
+                                                     const int32_t *__restrict__ seg_err,
+                                                     const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                                     int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                                     const int4 *__restrict__ pend, const unsigned *__restrict__ pcount,
+                                                     const unsigned *__restrict__ lcount,
+                                                     const int64_t *__restrict__ llist, int n_long) {
+  if ((int)blockIdx.x < n_long) {
+    const int64_t cnt = (int64_t)*lcount;
+    for (int64_t k = blockIdx.x; k < cnt; k += n_long)
+      fold_segment<P, false>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err, nullptr,
+                             nullptr);
+  } else {
+    fold_scan_blocks(s, pend, pcount, flags, (int64_t)blockIdx.x - n_long, (int64_t)gridDim.x - n_long);
+  }
 }
 
 // ---------------------------------------------------------------- Start
@@ -1910,6 +1944,13 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   case PP:                                                                                    \
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
                        flags, item_err, pend, pcount, lcount, llist);                         \
+    if (MRAFT_FOLD_TAIL && split && MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1) {            \
+      const int nl = (int)min(n_seg, (int64_t)4096);                                          \
+      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)8192);         \
+      hipLaunchKernelGGL(k_fold_tail<PP>, dim3((unsigned)(nl + ns)), bl, 0, st, s, items, seg_begin, \
+                         seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist, nl); \
+      return;                                                                                 \
+    }                                                                                         \
     if (MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1)                                        \
       hipLaunchKernelGGL(k_fold_long<PP>, dim3((unsigned)min(n_seg, (int64_t)4096)), bl, 0, st, s, items,  \
                          seg_begin, seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist); \
