@@ -754,7 +754,7 @@ __device__ unsigned long long g_fold_trace[65536 * 6];
 #define FOLD_STAMP(k, dep) do {} while (0)
 #endif
 #ifndef MRAFT_FOLD_TAIL
-#define MRAFT_FOLD_TAIL 0  // 1: k_fold_long and k_fold_scan as one launch (k_fold_tail)
+#define MRAFT_FOLD_TAIL 1  // k_fold_long and k_fold_scan as one launch (k_fold_tail; r4_v21: fold call -4 %)
 #endif
 #ifndef MRAFT_FOLD_XCD
 #define MRAFT_FOLD_XCD 1  // XCD-contiguous segment ranges (r4_v18: fold call -8 %, reads 55 -> 46 MB)
