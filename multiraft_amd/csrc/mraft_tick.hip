@@ -239,21 +239,12 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 
 // GetState (raft.go:237-246) of the group's exported replica, fused into the
 // tick (mraft_replicate_tick_export): commit and currentTerm<<1 | isLeader.
-#ifndef MRAFT_TICK_NT_STATE
-#define MRAFT_TICK_NT_STATE 0  // 1: phase C/D's scattered state words and the export as non-temporal stores
-#endif
-// One state word written by phase C/D (or the export).
-__device__ __forceinline__ void stw(int32_t *p, int v) {
-  if (MRAFT_TICK_NT_STATE) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-
 struct Export {
   int32_t *commit, *term_leader;
   __device__ __forceinline__ void put(int g, int c, int t, int role) const {
     if (commit) {
-      stw(commit + g, c);
-      stw(term_leader + g, (int32_t)(((uint32_t)t << 1) | (role == kLeader ? 1u : 0u)));
+      commit[g] = c;
+      term_leader[g] = (int32_t)(((uint32_t)t << 1) | (role == kLeader ? 1u : 0u));
     }
   }
 };
@@ -614,8 +605,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       cR = 1;
     } else {
       if (!COUNT) {
-        if (adopt) { stw(s2.term + f, T); stw(s2.voted + f, -1); }
-        stw(s2.role + f, kFollower);                                      // :120
+        if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
+        s2.role[f] = kFollower;                                           // :120
       }
       cR = 2;                                                            // term, dummy
       cW = (adopt ? 2 : 0) + 1;                                          // role
@@ -629,7 +620,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
           cR += (mk < 0) ? n : (mk < kc ? mk + 1 : mk);                 // compared follower terms
           if (mk >= 0) {
             newlast = prev + n;
-            if (!COUNT) stw(s2.last + f, newlast);
+            if (!COUNT) s2.last[f] = newlast;
             cW += (n - mk) + 1;
             // terms_sorted after appending from Index prev+1+mk: the args'
             // flag (prevLogTerm, entries sorted: the leader's proof, with the
@@ -641,7 +632,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
             const bool at_dummy = MRAFT_TICK_TAIL_HOIST ? ((pd_m >> lane) & 1) != 0 : prev == s2.dummy[f];
             const int sw = !fl ? 0 : (mk == 0 && at_dummy) ? 1 : -1;
             if (sw >= 0) {
-              if (!COUNT) stw(s2.srt + f, sw);
+              if (!COUNT) s2.srt[f] = sw;
               cW += 1;
             }
           }
@@ -650,7 +641,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         if (c0 > fcommit) {
           fcadv = 1;
           cW += 1;
-          if (!COUNT) stw(s2.commit + f, min(c0, newlast));
+          if (!COUNT) s2.commit[f] = min(c0, newlast);
         }
       }
     }
@@ -713,8 +704,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         s2.role[ld] = kFollower;
         mark_persist(s2, ld, MRAFT_PERSIST_STATE);                        // :72, snapshot :64
       }
-      if (commit != c0) stw(s2.commit + ld, commit);
-      if (gflags) stw(gflags + g, flags);
+      if (commit != c0) s2.commit[ld] = commit;
+      if (gflags) gflags[g] = flags;
       ex.put(g, commit, fd.stepped ? fd.term : T, fd.stepped ? kFollower : kLeader);
     }
     TICK_STAMP(3);
@@ -724,8 +715,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (lane < NI && ((fd.gate_m >> lane) & 1)) {
       const bool isr = ((is_m >> lane) & 1) != 0, ok = ((fd.rs_m >> lane) & 1) != 0;
       const int mv = isr ? ldummy : prev + n;
-      stw(s2.next + ld * P + p, ok ? mv + 1 : rci);
-      if (ok) stw(s2.match + ld * P + p, mv);
+      s2.next[ld * P + p] = ok ? mv + 1 : rci;
+      if (ok) s2.match[ld * P + p] = mv;
     }
   } else {
     // Leader-side words, wave-uniform.
