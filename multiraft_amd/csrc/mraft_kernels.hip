@@ -11,6 +11,12 @@ namespace mraft {
 namespace {
 
 constexpr int kBlock = 256;
+#ifndef MRAFT_MSG_BLOCK
+#define MRAFT_MSG_BLOCK 256  // workgroup size of the message path's lane-per-item kernels (gather, claims)
+#endif
+// (a smaller workgroup finds a CU with room sooner while another queue's
+// handler or tick holds most wave slots: shard pipelines)
+constexpr int kMsgBlock = MRAFT_MSG_BLOCK;
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 // A pointer the wave holds in SGPRs where it is used (a per-lane address
@@ -271,7 +277,10 @@ __device__ __forceinline__ void block_append2(bool wa, int64_t va, int64_t *__re
 // One workgroup of kAePlanT threads plans kAeOwn items: every thread
 // classifies one item (its own or a neighbour within kAeHalo on either side)
 // into LDS, then each owned item finds its place in its run from LDS.
-constexpr int kAePlanT = 1024, kAeHalo = 7, kAeOwn = kAePlanT - 2 * kAeHalo;
+#ifndef MRAFT_AE_PLAN_T
+#define MRAFT_AE_PLAN_T 1024  // plan workgroup size (items classified per workgroup, halo included)
+#endif
+constexpr int kAePlanT = MRAFT_AE_PLAN_T, kAeHalo = 7, kAeOwn = kAePlanT - 2 * kAeHalo;
 
 __global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *__restrict__ args, int64_t n,
                                                      int64_t n_log, int L, int ni,
@@ -1851,7 +1860,7 @@ void launch_claim(const void *items, int64_t n, int stride, int slot_off, const 
 void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
                         mraft_ae_args *out, int32_t *err, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_gather_args, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, peers, n,
+  hipLaunchKernelGGL(k_gather_args, dim3(blocks_for(n, kMsgBlock)), dim3(kMsgBlock), 0, st, s, slots, peers, n,
                      out, err);
 }
 
@@ -1859,7 +1868,7 @@ void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
                      unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err,
                      unsigned long long *total, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n)), dim3(kBlock), 0, st, args, n, n_log, L, gp, claim, srcmark,
+  hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n, kMsgBlock)), dim3(kMsgBlock), 0, st, args, n, n_log, L, gp, claim, srcmark,
                      epoch, err, total);
 }
 
@@ -1933,7 +1942,7 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
   unsigned *pcount = split ? (unsigned *)(pend + 2 * n) : nullptr;          // the a1 list's length
   unsigned *lcount = (unsigned *)((int4 *)scan_buf + 2 * n) + 1;            // the long-segment list's length
   int64_t *llist = (int64_t *)((int4 *)scan_buf + 2 * n + 1);
-  hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt)), dim3(kBlock), 0, st, (const char *)items, n_seg,
+  hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt, kMsgBlock)), dim3(kMsgBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
                      epoch, seg_err, n, flags, item_err, pcount, lcount);
   if (n_seg <= 0) return;
