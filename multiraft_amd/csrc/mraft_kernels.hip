@@ -12,7 +12,7 @@ namespace {
 
 constexpr int kBlock = 256;
 #ifndef MRAFT_MSG_BLOCK
-#define MRAFT_MSG_BLOCK 256  // workgroup size of the message path's lane-per-item kernels (gather, claims)
+#define MRAFT_MSG_BLOCK 64  // workgroup size of the message path's lane-per-item kernels (gather, claims; r4_v26: 64 pipelines -3 %)
 #endif
 // (a smaller workgroup finds a CU with room sooner while another queue's
 // handler or tick holds most wave slots: shard pipelines)
