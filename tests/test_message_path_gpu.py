@@ -194,3 +194,31 @@ def test_handle_high_indices_gpu(mode):
         rep, herr = _message_round(e, o, st, slots, peers, G, P, L,
                                    "reference" if mode == "staged" else mode, assert_states_equal)
     assert (rep["success"][herr == 0] == 1).any()
+
+
+@pytest.mark.parametrize("S", [2, 3])
+def test_message_path_shard_pipelines_gpu(S):
+    """The bench's message path as S shard pipelines (bench.message_path: an
+    engine on a dedicated queue per contiguous group range, bound to SoA
+    slices of one state image, one host thread each) leaves the same state as
+    the oracle running gather -> HandleAppendEntries -> the reply fold over
+    the whole batch (the groups share nothing, raft.go:16-40)."""
+    import torch
+
+    import bench
+    from multiraft_amd import synth_seed
+    G, P, L = 768, 5, 256
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + S)
+    dev = torch.device("cuda", 0)
+    master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
+    copies = [{k: v.clone() for k, v in master.items()} for _ in range(2)]
+    bench.message_path(master, copies, lp, G, P, L, dev, S, 1)
+    got = {k: v.cpu().numpy() for k, v in copies[0].items()}
+    o = Oracle(G, P, L, st)
+    slots, peers = all_follower_items(lp, G, P)
+    args, gerr = o.gather_append_args(slots, peers)
+    assert (gerr == 0).all()
+    rep, herr = o.handle_append_entries(args, None)
+    res, seg = results_of(slots, peers, args, rep, herr, G, P)
+    o.process_append_replies(res, seg)
+    assert_states_equal(got, o.state(), G, P, L, f"{S} pipelines")
