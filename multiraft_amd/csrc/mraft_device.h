@@ -60,7 +60,7 @@ __device__ __forceinline__ int first_lane(unsigned long long m) { return __ffsll
 // row whose Index `base` (the dummy) sits at `head` (row length L); returns
 // lo - 1 when every term in the range equals a. Wave-uniform arguments; the
 // term of lo must be readable when lo <= hi (lanes past lo re-read it).
-template <int U = kUnroll, bool NT = false>
+template <int U = kUnroll>
 __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row, int base, int head,
                                                  int L, int lo, int hi, int a) {
   const int lane = lane_id();
@@ -69,8 +69,7 @@ __device__ __forceinline__ int wave_scan_down_ne(const int32_t *__restrict__ row
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = top - lane - kWave * u;
-      const int32_t *wp = row + ring(max(idx, lo) - base + head, L);
-      const int w = NT ? __builtin_nontemporal_load(wp) : *wp;  // unconditional: the loads issue back to back
+      const int w = row[ring(max(idx, lo) - base + head, L)];  // unconditional: the loads issue back to back
       v[u] = idx >= lo ? w : a;
     }
     // Every ballot, no exit per vector (which lets the compiler sink each load

@@ -497,6 +497,13 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   }
   int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
   if (live) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
+  // MRAFT_AE_ENTRIES_SORTED is the sender's claim (it crosses the network):
+  // honoured only where the terms prevLogTerm, entry 0, ... really never
+  // decrease. Here the first step (prevLogTerm <= entry 0, in the round trip
+  // of the follower's log[prev]); the entries themselves are checked on the
+  // pass's loads (DescTrack). Same rule in the oracle (ae_flag_holds).
+  const bool claim = live && nn > 0 && (a.flags & MRAFT_AE_ENTRIES_SORTED) != 0;
+  const bool claim0 = claim && a.prev_log_term <= *src.at(prev + 1);
   mraft_ae_reply r = {0, 0, 0, 0};
   int ftp = 0;
   if (live) {
@@ -532,8 +539,9 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   int newlast = -1, fcommit_new = -1, srt_new = -1;
   const int merge_m = (int)(__ballot(cls == AE_MERGE) & ((1ull << NI) - 1));
   // terms_sorted after an append from Index k (include/mraft.h): the args'
-  // flag when k - 1 is the dummy, cleared without it, else unchanged
-  int shint = (a.flags & MRAFT_AE_ENTRIES_SORTED) ? fdummy + 1 : -1;
+  // flag when k - 1 is the dummy, cleared without it, else unchanged — the
+  // flag as checked (claim0 here, the entries' descents after the pass)
+  int shint = claim0 ? fdummy + 1 : -1;
   if (merge_m) {
     Fol<NI, true> fo;
     fo.log = s.log;
@@ -588,6 +596,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
       vec = vec && (((uintptr_t)ss.at(plo)) & ~(uintptr_t)15) >= (uintptr_t)ss.p &&
             (((uintptr_t)ss.at(phi)) | 15) < (uintptr_t)(ss.p + n_ent);
     int found = -1;
+    DescTrack dt{__ballot(cls == AE_MERGE && claim0) != 0, 0, INT32_MIN};
 #if MRAFT_AE_STASH
     // This lane's reply inputs wait in LDS during the pass (the pass needs
     // the registers: at 8 waves per SIMD they would spill to scratch).
@@ -605,15 +614,15 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     if (vec) {
       int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
       if (MRAFT_AE_PIPE) {
-        if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+        if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
       } else {
-        for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
+        for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
       }
-      copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
+      copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
     } else {
       int c = plo;
-      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi);
-      copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found);
+      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
+      copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
     }
 #if MRAFT_AE_STASH
     asm volatile("" ::: "memory");
@@ -642,6 +651,9 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
         int last_after = flast;
         if (fo.cfrom[q] > 0) {                                         // truncated and appended
           newlast = last_after = phi;
+          // a descent among this message's entries (Index start+1 .. phi)
+          // voids its flag
+          if (dt.last > fo.start[q]) shint = -1;
           srt_new = shint < 0 ? 0 : (fo.cfrom[q] == shint ? 1 : -1);
         }
         if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160

@@ -143,6 +143,63 @@ struct Fol {
   }
 };
 
+// Descent tracking over the entries a pass streams (the message handler's
+// check of an AppendEntries' MRAFT_AE_ENTRIES_SORTED flag, include/mraft.h):
+// the highest Index i in (lo, hi] whose predecessor's term is larger,
+// term(i - 1) > term(i), over the chunks seen. The chunks of one pass are
+// contiguous and ascending and the first starts at or below lo, so `carry`
+// (the last term of the previous chunk) is only read where i - 1 >= lo.
+// NoDesc (the fused tick: the leader's own proof needs no check) compiles to
+// nothing.
+struct NoDesc {
+  template <int EPL>
+  __device__ __forceinline__ void see(const int (&)[EPL], int, int, int) {}
+  __device__ __forceinline__ void see_strided(const int (&)[4], int, int, int) {}
+};
+struct DescTrack {
+  int on;     // wave-uniform: some merging message carries the flag
+  int carry;  // term of the Index just below the current chunk
+  int last;   // highest descent Index seen (INT32_MIN: none)
+  // lane j holds Indexes c + EPL*j .. + EPL - 1
+  template <int EPL>
+  __device__ __forceinline__ void see(const int (&e)[EPL], int c, int lo, int hi) {
+    if (!on) return;
+    const int lane = lane_id();
+    int pl = __shfl_up(e[EPL - 1], 1, 64);
+    if (lane == 0) pl = carry;
+    int d = INT32_MIN;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      const int i = c + EPL * lane + u, b = u ? e[u - 1] : pl;
+      if (i - 1 >= lo && i <= hi && b > e[u]) d = i;
+    }
+    const unsigned long long m = __ballot(d != INT32_MIN);
+    if (m) last = max(last, __builtin_amdgcn_readlane(d, 63 - __clzll((long long)m)));
+    carry = __builtin_amdgcn_readlane(e[EPL - 1], 63);
+  }
+  // lane j holds Indexes c + 64*u + j, u = 0..3
+  __device__ __forceinline__ void see_strided(const int (&e)[4], int c, int lo, int hi) {
+    if (!on) return;
+    const int lane = lane_id();
+    int d = INT32_MIN;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int pl = __shfl_up(e[u], 1, 64);
+      if (lane == 0) pl = u ? __builtin_amdgcn_readlane(e[u - 1], 63) : carry;
+      const int i = c + 64 * u + lane;
+      if (i - 1 >= lo && i <= hi && pl > e[u]) d = max(d, i);
+    }
+    const unsigned long long m = __ballot(d != INT32_MIN);
+    if (m) {
+      int x = d;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, 64));
+      last = max(last, __builtin_amdgcn_readfirstlane(x));
+    }
+    carry = __builtin_amdgcn_readlane(e[3], 63);
+  }
+};
+
 // One chunk of the streaming pass over the leader's log. The pass serves
 // (1) every follower q's entry merge: compare entries [start_q, cend_q) with
 // the follower's log, then (from the first mismatch) copy entries up to `hi`
@@ -151,9 +208,9 @@ struct Fol {
 // VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
 // otherwise lane j owns c+64(4v+u)+j. Entry idx is at src.at(idx), follower
 // q's term of Index idx at fo.at(q, idx).
-template <int V, bool VEC, bool COUNT, class Src, class F>
+template <int V, bool VEC, bool COUNT, class Src, class F, class D = NoDesc>
 __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int slo, int shi, int T,
-                                           int &found, int c, int plo, int phi) {
+                                           int &found, int c, int plo, int phi, D &&dt = D{}) {
   constexpr int NI = F::kNI;
   constexpr int CW = 256 * V;
   const int lane = lane_id();
@@ -174,6 +231,11 @@ __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int 
 #pragma unroll
       for (int u = 0; u < 4; ++u) e[v][u] = (idx[v][u] >= plo && idx[v][u] <= phi) ? ld1(src.at(idx[v][u])) : 0;
     }
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if (VEC) dt.template see<4>(e[v], c + 256 * v, plo, phi);
+    else dt.see_strided(e[v], c + 256 * v, plo, phi);
   }
   int f[NI][V][4];
 #pragma unroll
@@ -293,9 +355,9 @@ __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int 
 // compares; returns the first chunk not processed (the copy-only loop
 // continues there; c stays on the leader row's line grid for EPL >= 2 and
 // the caller's 32-entry chunk origin).
-template <bool COUNT, int EPL = 4, class Src, class F>
+template <bool COUNT, int EPL = 4, class Src, class F, class D = NoDesc>
 __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int slo, int shi, int T, int &found,
-                                         int c, int plo, int phi) {
+                                         int c, int plo, int phi, D &&dt = D{}) {
   constexpr int NI = F::kNI;
   constexpr int CW = 64 * EPL;
   const int lane = lane_id();
@@ -316,6 +378,7 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
   load(c, e, f);
   for (;;) {
     const int i0 = c + EPL * lane;
+    dt.template see<EPL>(e, c, plo, phi);
     // compare: first mismatch of every follower still comparing
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
@@ -396,9 +459,9 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
 // D = 2, 3, 4 are all 3-4 % SLOWER than one chunk ahead (0.350 vs 0.339 ms):
 // more bytes in flight per wave only queue in the memory system. Kept as an
 // A/B alternative.
-template <int D, bool COUNT, class Src, class F>
+template <int D, bool COUNT, class Src, class F, class DT>
 __device__ __forceinline__ void copy_loop_deep(const Src &src, const F &fo, int c, int nend, int plo, int phi,
-                                               int slo, int shi, int T, int &found) {
+                                               int slo, int shi, int T, int &found, DT &dt) {
   constexpr int NI = F::kNI;
   constexpr int CW = 256;
   const int lane = lane_id();
@@ -421,6 +484,10 @@ __device__ __forceinline__ void copy_loop_deep(const Src &src, const F &fo, int 
 #pragma unroll
     for (int d = 0; d + 1 < D; ++d) buf[d] = buf[d + 1];
     buf[D - 1] = load(c + D * CW);  // issued before this chunk's stores
+    {
+      const int ce[4] = {cur.x, cur.y, cur.z, cur.w};
+      dt.template see<4>(ce, c, plo, phi);
+    }
     if (scan && c <= shi && c + CW - 1 >= slo) {
       const int e[4] = {cur.x, cur.y, cur.z, cur.w};
       int lu = -1;
@@ -452,15 +519,15 @@ __device__ __forceinline__ void copy_loop_deep(const Src &src, const F &fo, int 
   }
 }
 
-template <bool VEC, bool COUNT, class Src, class F>
+template <bool VEC, bool COUNT, class Src, class F, class D = NoDesc>
 __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, int nend, int plo, int phi,
-                                          int slo, int shi, int T, int &found) {
+                                          int slo, int shi, int T, int &found, D &&dt = D{}) {
   constexpr int NI = F::kNI;
   constexpr int CW = 256;
   const int lane = lane_id();
   int cmask = fo.copy;
   if constexpr (VEC && MRAFT_COPY_DEPTH > 1) {
-    copy_loop_deep<MRAFT_COPY_DEPTH, COUNT>(src, fo, c, nend, plo, phi, slo, shi, T, found);
+    copy_loop_deep<MRAFT_COPY_DEPTH, COUNT>(src, fo, c, nend, plo, phi, slo, shi, T, found, dt);
     return;
   }
   if constexpr (VEC) {
@@ -474,6 +541,10 @@ __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, in
       const bool more = cn <= phi && (cmask_n || (slo <= shi && cn <= shi));
       int4 nxt = make_int4(0, 0, 0, 0);
       if (more && cn + 4 * lane <= phi) nxt = ld4(src.at(cn + 4 * lane));
+      {
+        const int ce[4] = {cur.x, cur.y, cur.z, cur.w};
+        dt.template see<4>(ce, c, plo, phi);
+      }
       if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
         const int e[4] = {cur.x, cur.y, cur.z, cur.w};
         int lu = -1;
@@ -514,6 +585,7 @@ __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, in
         idx[u] = c + 64 * u + lane;
         e[u] = (idx[u] >= plo && idx[u] <= phi) ? ld1(src.at(idx[u])) : 0;
       }
+      dt.see_strided(e, c, plo, phi);
       if (slo <= shi && c <= shi && c + CW - 1 >= slo) {
         int hit = -1;
 #pragma unroll

@@ -34,8 +34,6 @@
 #include "mraft_internal.h"
 #include "mraft_pass.h"
 
-#include <cstdlib>
-
 namespace mraft {
 
 namespace {
@@ -173,18 +171,11 @@ struct Fold {
 #ifndef MRAFT_TICK_MINW
 #define MRAFT_TICK_MINW 8  // __launch_bounds__ minimum waves per SIMD
 #endif
-#ifndef MRAFT_TICK_EXP
-#define MRAFT_TICK_EXP 0   // traffic experiments only (wrong results): 1 = no pass, 2 = no pass, no scans,
-                           // 3 = as 2 and no log[prev] / log[last] header loads
-#endif
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
 #endif
 #ifndef MRAFT_TICK_RELOAD
 #define MRAFT_TICK_RELOAD 1  // phase C/D re-read the state pointers (not held across the pass)
-#endif
-#ifndef MRAFT_TICK_HDR_EXTRA
-#define MRAFT_TICK_HDR_EXTRA 0  // experiment: extra dependent header round trips (wrong only in timing)
 #endif
 #ifndef MRAFT_TICK_TRACE
 #define MRAFT_TICK_TRACE 0  // diagnostic build: s_memrealtime stamps per group (tools/trace_tick.py)
@@ -209,23 +200,6 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #endif
 #ifndef MRAFT_TICK_SCANU
 #define MRAFT_TICK_SCANU 1  // ConflictIndex scans past the probe: 64 * SCANU terms per round trip
-#endif
-#ifndef MRAFT_TICK_TAIL_HOIST
-#define MRAFT_TICK_TAIL_HOIST 1  // phase C uses the header's terms_sorted / dummy words (no reload after the pass)
-#endif
-#ifndef MRAFT_TICK_PDIRTY
-#define MRAFT_TICK_PDIRTY 0  // follower persist marks: 0 = load-OR-store at the end, 1 = non-returning
-                             // atomic OR, 2 = the word loaded with the header, stored at the end
-                             // (r4_v7: 1 no faster; 2 spills; a byte store with STATE alone in byte 0,
-                             // r4_v8, within noise)
-#endif
-#ifndef MRAFT_TICK_LATE
-#define MRAFT_TICK_LATE 0  // 1: the ConflictIndex scans run after the pass (their inputs parked in LDS), and with
-                           // the terms_sorted proof a1's top-term probe is only issued before it (no round
-                           // trip of either between the header and the pass)
-#endif
-#ifndef MRAFT_TICK_SCAN_NT
-#define MRAFT_TICK_SCAN_NT 0  // ConflictIndex scan words as non-temporal loads (read once, nothing else reads them)
 #endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
@@ -283,18 +257,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     }
     return;
   }
-  long long ld = (long long)g * P + lp;
-#if MRAFT_TICK_HDR_EXTRA
-  // Experiment only (header-latency slope): MRAFT_TICK_HDR_EXTRA
-  // more dependent round trips before the header (a load of an unrelated line
-  // whose value, zeroed behind the compiler's back, feeds the leader index).
-#pragma unroll
-  for (int k = 0; k < MRAFT_TICK_HDR_EXTRA; ++k) {
-    int z = s.votes[(ld * 977 + 131 * k) % ((long long)s.G * P)];
-    asm volatile("v_and_b32 %0, 0, %0" : "+v"(z));
-    ld += uni(z);
-  }
-#endif
+  const long long ld = (long long)g * P + lp;
   const long long lrow = ld * L;
   // Every load that depends only on the leader index, issued together.
   const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
@@ -307,7 +270,6 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const int p = lane < lp ? lane : lane + 1;
   const long long f = (long long)g * P + p;
   int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
-  int fpd = 0;  // MRAFT_TICK_PDIRTY == 2: this lane's follower's persist word
   if (lane < NI) {
     nxt = s.next[ld * P + p];
     fterm = s.term[f];
@@ -315,7 +277,6 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     flast = s.last[f];
     fcommit = s.commit[f];
     fhead = s.head[f];
-    if (MRAFT_TICK_PDIRTY == 2 && !COUNT && s.pdirty) fpd = s.pdirty[f];
   }
   long long hR = 1;  // algorithmic words of the header (wave-uniform)
   if (role != kLeader || c0 < ldummy) {
@@ -346,9 +307,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     return;
   }
   int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = MRAFT_TICK_EXP == 3 ? 0 : uni(s.log[lrow + ring(last + lb, L)]);  // speculative a1 probe
+  const int probe_last = uni(s.log[lrow + ring(last + lb, L)]);  // speculative a1 probe
   int prev_term = 0, ft = 0;
-  if (icls == IC_GO && MRAFT_TICK_EXP != 3) {
+  if (icls == IC_GO) {
     prev_term = s.log[lrow + ring(prev + lb, L)];                        // :49
     if (prev >= fdummy && prev <= flast) ft = s.log[f * L + ring(prev - fdummy + fhead, L)];
   }
@@ -401,9 +362,8 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   // scanning follower in one round trip (most runs end there), then each
   // longer run on its own, 64 * MRAFT_TICK_SCANU terms per round trip (64
   // measured 1.4 % faster than 256: fewer lines fetched past the run's end
-  // outweigh the extra round trips). Nothing before phase D reads their
-  // result (the fold does not use ConflictIndex), so MRAFT_TICK_LATE runs
-  // them after the pass.
+  // outweigh the extra round trips). (Running them after the pass with their
+  // inputs parked in LDS measured no faster and moved no traffic: r4_v13.)
   auto conflict_scans = [&](const int32_t *__restrict__ logp, unsigned long long m, int qdummy, int qhead, int qft) {
     int pv[NI];
 #pragma unroll
@@ -414,7 +374,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
                   sh = uni(__shfl(qhead, q, 64));
         const int32_t *pp = logp + sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L);  // prev >= dummy + 2
-        pv[q] = MRAFT_TICK_SCAN_NT ? __builtin_nontemporal_load(pp) : *pp;
+        pv[q] = *pp;
       }
     }
 #pragma unroll
@@ -431,7 +391,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
         } else if (hi - 64 < lo) {
           ci = sd + 1;
         } else {
-          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU, MRAFT_TICK_SCAN_NT>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
+          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
           ci = r < lo ? sd + 1 : r;
         }
         if (lane == q) {
@@ -441,20 +401,12 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
       }
     }
   };
-  const unsigned long long scan_m = MRAFT_TICK_EXP >= 2 ? 0ull : __ballot(icls == IC_SCAN);
-#if MRAFT_TICK_LATE
-  __shared__ int late_stash[3][64 * MRAFT_TICK_WPB];  // the scans' per-lane inputs, parked across the pass
-  const int tid = (int)threadIdx.x;
-  if (scan_m) {
-    late_stash[0][tid] = fdummy; late_stash[1][tid] = fhead; late_stash[2][tid] = ft;
-  }
-#else
+  const unsigned long long scan_m = __ballot(icls == IC_SCAN);
   if (scan_m) conflict_scans(s.log, scan_m, fdummy, fhead, ft);
-#endif
 
   // prev == the follower's dummy, for phase C's terms_sorted rule (a ballot:
   // no per-lane word kept live across the pass)
-  const unsigned long long pd_m = MRAFT_TICK_TAIL_HOIST ? __ballot(prev == fdummy) : 0ull;
+  const unsigned long long pd_m = __ballot(prev == fdummy);
   // Per-follower pass parameters (wave-uniform).
   const int merge_m = (int)__ballot(icls == IC_MERGE);
   Fol<NI> fo;
@@ -495,29 +447,21 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const int is_m = (int)__ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
   const int have0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
   const int succ0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
-  int late_t = 0, late_a1 = 0;  // MRAFT_TICK_LATE: a1's top term, read after the pass
   if (!maybe_full) {
     fd.run(T, lp, mm, have0, succ0, is_m, ldummy, rterm, prev, n, rci, icls);
     if (fd.any) {
       top = min(fd.mstar, last);
       if (top > c0) {
-        if (MRAFT_TICK_LATE && lsrt && top != last) {
-          // with the proof the top term decides a1 unless it is above
-          // currentTerm: issued now, decided after the pass
-          late_t = s.log[lrow + ring(top + lb, L)];
-          late_a1 = 1;
-        } else {
-          const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
-          if (t == T) commit = top;
-          else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
-          else { slo = c0 + 1; shi = top - 1; }
-        }
+        const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
+        if (t == T) commit = top;
+        else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
+        else { slo = c0 + 1; shi = top - 1; }
       }
     }
   }
   int found = -1;
   TICK_STAMP(1);
-  if (MRAFT_TICK_EXP == 0 && (merge_m || slo <= shi)) {
+  if (merge_m || slo <= shi) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
     // Chunks start on a 128-B line of the leader's row (physical position of
@@ -544,20 +488,6 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   const Dev s2 = reload_dev();
 #else
   const Dev &s2 = s;
-#endif
-#if MRAFT_TICK_LATE
-  if (scan_m) conflict_scans(s2.log, scan_m, late_stash[0][tid], late_stash[1][tid], late_stash[2][tid]);
-  if (late_a1) {
-    const int t = uni(late_t);                                           // :98
-    if (t == T) {
-      commit = top;
-    } else if (t < T) {
-      settled = 1;
-    } else {  // above currentTerm: Go's downward scan (:95-104)
-      const int i = wave_scan_down_eq(s2.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
-      if (i > c0) commit = i;
-    }
-  }
 #endif
   int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
@@ -595,12 +525,9 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
   int fcadv = 0;
   long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
   if (icls >= IC_STALE && icls <= IC_HB) {
-    if (!COUNT) {                                                         // deferred :111
-      if (MRAFT_TICK_PDIRTY == 0) mark_persist(s2, f, MRAFT_PERSIST_STATE);
-      else if (MRAFT_TICK_PDIRTY == 1 && s2.pdirty)
-        (void)__hip_atomic_fetch_or(&s2.pdirty[f], MRAFT_PERSIST_STATE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else if (s2.pdirty) s2.pdirty[f] = fpd | MRAFT_PERSIST_STATE;
-    }
+    // deferred :111 (a load, OR and store: as a non-returning atomic OR it
+    // measured no faster here, r4_v7)
+    if (!COUNT) mark_persist(s2, f, MRAFT_PERSIST_STATE);
     if (icls == IC_STALE) {
       cR = 1;
     } else {
@@ -626,10 +553,10 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
             // flag (prevLogTerm, entries sorted: the leader's proof, with the
             // dummy's term compared explicitly), or the new entries are the
             // whole log when that Index is the dummy's successor
-            bool fl = (MRAFT_TICK_TAIL_HOIST ? lsrt : s2.srt[ld]) != 0;
+            bool fl = lsrt != 0;
             if (fl && prev == ldummy)
               fl = s2.log[lrow + ring(prev + lb, L)] <= s2.log[lrow + ring(prev + 1 + lb, L)];
-            const bool at_dummy = MRAFT_TICK_TAIL_HOIST ? ((pd_m >> lane) & 1) != 0 : prev == s2.dummy[f];
+            const bool at_dummy = ((pd_m >> lane) & 1) != 0;
             const int sw = !fl ? 0 : (mk == 0 && at_dummy) ? 1 : -1;
             if (sw >= 0) {
               if (!COUNT) s2.srt[f] = sw;
@@ -651,8 +578,7 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     if (!COUNT) {
       const int bits = (adopt ? MRAFT_PERSIST_STATE : 0) |                 // raft_snapshot.go:26
                        (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0);  // :47
-      if (MRAFT_TICK_PDIRTY == 2) { if (s2.pdirty && bits) s2.pdirty[f] = fpd | bits; }
-      else mark_persist(s2, f, bits);
+      mark_persist(s2, f, bits);
     }
     if (icls != IC_IS_STALE) {
       if (!COUNT) {
@@ -785,22 +711,11 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
   }
 }
 
-// Experiment knob (not a product setting): MRAFT_TICK_DYN_LDS=<bytes> gives
-// every tick workgroup that much dynamic LDS, capping the waves per CU at
-// 160 KiB / bytes (occupancy experiments, tools/exp_lottery3.py).
-inline size_t tick_dyn_lds() {
-  static const size_t v = [] {
-    const char *e = getenv("MRAFT_TICK_DYN_LDS");
-    return e ? (size_t)atol(e) : (size_t)0;
-  }();
-  return v;
-}
-
 template <int P, bool COUNT>
 void launch_tick_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
                    Export ex, hipStream_t st) {
   const int blocks = (s.G + MRAFT_TICK_WPB - 1) / MRAFT_TICK_WPB;
-  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), tick_dyn_lds(), st, s,
+  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), 0, st, s,
                      lpeer, gflags, counts, ex);
 }
 

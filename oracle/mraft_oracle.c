@@ -213,6 +213,21 @@ int ora_gather_append_args(ora_engine *e, const int32_t *slots,
 /* a4: HandleAppendEntries, raft_append_entry.go:108-162                      */
 /* ------------------------------------------------------------------------ */
 
+/* Whether an AppendEntries' MRAFT_AE_ENTRIES_SORTED claim holds: the terms
+ * prevLogTerm, entry 0, ..., entry n-1 never decrease. The flag crosses the
+ * network, so the engine honours it only where it holds (include/mraft.h
+ * mraft_ae_args); a false claim counts as no flag. Engine bookkeeping for
+ * terms_sorted, not a Go rule: the reference keeps no such proof. */
+static int ae_flag_holds(const mraft_ae_args *a, const int32_t *ent) {
+  if (!(a->flags & MRAFT_AE_ENTRIES_SORTED)) return 0;
+  int32_t prev_t = a->prev_log_term;
+  for (int32_t k = 0; k < a->n_entries; ++k) {
+    if (ent[k] < prev_t) return 0;
+    prev_t = ent[k];
+  }
+  return 1;
+}
+
 /* ent = entries' terms (entry k has Index prev+1+k); cnt_src = the leader
  * replica whose log the entries were copied from (for counting its words), or
  * -1. */
@@ -305,7 +320,7 @@ static int32_t handle_ae_one(ora_engine *e, int32_t f, const mraft_ae_args *a,
       CW(A_LAST, f);
       /* terms_sorted: the args' flag; the new entries are the whole log when
        * the first appended Index is the dummy's successor */
-      if (!(a->flags & MRAFT_AE_ENTRIES_SORTED)) { S.terms_sorted[f] = 0; CW(A_SORTED, f); }
+      if (!ae_flag_holds(a, ent)) { S.terms_sorted[f] = 0; CW(A_SORTED, f); }
       else if (index == dummy + 1) { S.terms_sorted[f] = 1; CW(A_SORTED, f); }
       break;
     }

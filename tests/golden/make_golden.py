@@ -336,6 +336,35 @@ def tick_vectors():
     return out
 
 
+BIN_ARRAYS = ("current_term", "voted_for", "state", "commit_index", "last_applied", "dummy_index",
+              "last_index", "granted_votes", "log_term", "match_index", "next_index", "persist_dirty")
+
+
+def tick_vectors_bin(z) -> bytes:
+    """The tick vectors as the flat little-endian int32 file the plain-C host
+    test reads (tests/c_host/mraft_host_tick.c): "MRTV", version 1, count;
+    per vector G, P, L, leader_peer[G], group flags[G], the GetState words
+    of every group's leader replica (replica 0 when leader_peer is out of
+    range, include/mraft.h mraft_replicate_tick_export) commit[G] and
+    term<<1|isLeader[G], then the BIN_ARRAYS inputs and the expected outputs."""
+    parts = [b"MRTV"]
+    n = 0
+    while f"v{n}_dims" in z:
+        n += 1
+    parts.append(np.array([1, n], dtype="<i4").tobytes())
+    for i in range(n):
+        G, P, L = (int(x) for x in z[f"v{i}_dims"])
+        lp = np.asarray(z[f"v{i}_leader_peer"], dtype=np.int64)
+        rep = np.where((lp >= 0) & (lp < P), lp, 0) + np.arange(G) * P
+        out = {k: np.asarray(z[f"v{i}_out_{k}"], dtype=np.int64) for k in BIN_ARRAYS}
+        commit = out["commit_index"][rep]
+        tl = (out["current_term"][rep] << 1) | (out["state"][rep] == 1)
+        vec = [z[f"v{i}_dims"], z[f"v{i}_leader_peer"], z[f"v{i}_flags"], commit, tl]
+        vec += [z[f"v{i}_in_{k}"] for k in BIN_ARRAYS] + [z[f"v{i}_out_{k}"] for k in BIN_ARRAYS]
+        parts += [np.ascontiguousarray(a, dtype="<i4").tobytes() for a in vec]
+    return b"".join(parts)
+
+
 if __name__ == "__main__":
     kats = build()
     for k in kats:
@@ -343,4 +372,6 @@ if __name__ == "__main__":
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kats, f, indent=1)
     np.savez_compressed(os.path.join(HERE, "tick_vectors.npz"), **tick_vectors())
+    with open(os.path.join(HERE, "tick_vectors.bin"), "wb") as f:
+        f.write(tick_vectors_bin(np.load(os.path.join(HERE, "tick_vectors.npz"))))
     print(f"wrote {len(kats)} KATs and tick vectors")

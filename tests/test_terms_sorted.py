@@ -121,6 +121,70 @@ def test_append_rule(mk):
 
 
 @pytest.mark.parametrize("mk", BACKENDS)
+def test_false_flag_is_not_honoured(mk):
+    """MRAFT_AE_ENTRIES_SORTED crosses the network: a flag on
+    entries that are not sorted — a descent among them, or prevLogTerm above
+    the first — counts as no flag, so the follower's proof never claims an
+    unsorted log (which a later a1 as leader would trust)."""
+    st = _state()
+    _set_log(st, 1, [0, 1, 1, 1])             # sorted
+    _set_log(st, 4, [0, 2, 2, 2])             # sorted
+    _set_log(st, 7, [0, 1, 1, 1])             # sorted
+    _set_log(st, 10, [0, 1, 1, 1])            # sorted
+    e = mk(st)
+    assert list(_store(e)["terms_sorted"][[1, 4, 7, 10]]) == [1, 1, 1, 1]
+    cases = [
+        (_ae(1, 3, 1, 1, 3, 1), [1, 3, 2]),   # a descent after the first appended entry: not honoured -> 0
+        (_ae(4, 3, 1, 2, 2, 1), [1, 1]),      # prevLogTerm 2 > entry 0: not honoured -> 0
+        (_ae(7, 3, 0, 0, 3, 1), [2, 1, 1]),   # appends from dummy + 1, a descent: -> 0
+        (_ae(10, 3, 1, 1, 3, 1), [1, 2, 3]),  # a true flag, append from 3: kept (1)
+    ]
+    buf, args = [], []
+    for a, ent in cases:
+        a["entries_offset"] = len(buf)
+        buf += ent
+        args.append(a)
+    rep, err = e.handle_append_entries(np.array(args, dtype=AE_ARGS), np.array(buf, np.int32))
+    assert not err.any() and rep["success"].all()
+    s = _store(e)
+    assert list(s["last_index"][[1, 4, 7, 10]]) == [4, 3, 3, 4]
+    assert list(s["terms_sorted"][[1, 4, 7, 10]]) == [0, 0, 0, 1]
+    assert_terms_sorted_sound(s, G, P, L, "false flags")
+
+
+@pytest.mark.gpu
+def test_false_flag_by_reference_gpu():
+    """The same check on the by-reference message sets (one streaming pass per
+    set, the flag checked on the pass's loads): args gathered from unsorted
+    leaders with the flag forced on, on random adversarial states, rings
+    rotated; GPU == oracle, proof sound."""
+    from message_cases import all_follower_items, results_of
+    from oracle_lib import rotate_rings
+    from random_states import random_tick_state
+    rng = np.random.default_rng(5)
+    Gh, Ph, Lh = 256, 5, 96
+    st, lp = random_tick_state(rng, Gh, Ph, Lh, monotone=False)
+    st = rotate_rings(st, Gh, Ph, Lh, rng, 0.5)
+    lpv = np.where((lp >= 0) & (lp < Ph), lp, -1).astype(np.int32)
+    slots, peers = all_follower_items(lpv, Gh, Ph)
+    o = Oracle(Gh, Ph, Lh, st)
+    with Engine(Gh, Ph, Lh) as e:
+        e.load_state(st)
+        args, gerr = e.gather_append_args(slots, peers)
+        oargs, ogerr = o.gather_append_args(slots, peers)
+        assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr)
+        ok = gerr == 0
+        forged = args[ok].copy()
+        forged["flags"] = 1
+        rep, herr = e.handle_append_entries(forged, None)
+        orep, oherr = o.handle_append_entries(forged, None)
+        assert np.array_equal(rep, orep) and np.array_equal(herr, oherr)
+        s = e.store_state()
+        assert_states_equal(s, o.state(), Gh, Ph, Lh, "forged flags by reference")
+        assert (s["terms_sorted"] == 0).sum() > 0
+
+
+@pytest.mark.parametrize("mk", BACKENDS)
 def test_start_and_install_rules(mk):
     """Start clears the proof when the last term exceeds currentTerm (not a
     reachable leader, but a valid engine state); an InstallSnapshot that

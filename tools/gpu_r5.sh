@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round 4 GPU pass, parametrised: TAG names the output directory
-# (gpurun_out/$TAG); DO lists what to run (tests bench pmc valu trace smoke).
+# Round 5 GPU pass, parametrised: TAG names the output directory
+# (gpurun_out/$TAG); DO lists what to run (tests bench pmc valu elect cmp trace smoke ...).
 #   TESTS   pytest selection (-k expression) for the tests step ("" = all -m gpu)
 #   BENCH   extra bench.py arguments
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r4_dev}
+TAG=${TAG:-r5_dev}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 for st in ${DO:-tests bench}; do
@@ -76,6 +76,38 @@ for st in ${DO:-tests bench}; do
         > "$OUT/valu_bench.json" 2> "$OUT/valu_bench.err" || { tail -5 "$OUT/valu_bench.err"; exit 1; }
       timeout -k 10 300 python3 bench_election.py --no-cpu-baseline > "$OUT/election_bench.json" 2> "$OUT/election_bench.err" || exit 1
       python3 tools/pmc_valu.py "$TAG" "$OUT/valu" "$OUT/election_bench.json" | tee "$OUT/pmc_valu.log" | grep -E "frac|busy|SQ_INSTS_VALU" ;;
+    elect)
+      # where the election storm's issue slots go: stall and LDS counters of
+      # k_election_rounds<7>, one pass per counter group
+      echo "== elect"
+      i=0
+      for grp in "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VALU" \
+                 "SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/elect$i" -o e -- python3 bench_election.py --no-cpu-baseline --steps 5 \
+          > "$OUT/elect$i.json" 2> "$OUT/elect$i.err" || { tail -5 "$OUT/elect$i.err"; exit 1; }
+      done
+      python3 tools/pmc_kernels.py "$OUT/elect_counters.json" "$OUT"/elect1 "$OUT"/elect2 --kernels "k_election_rounds<7>" | head -40 ;;
+    cmp)
+      # the tick and the handler on the same state copy, counters per kernel
+      echo "== cmp"
+      timeout -k 10 300 python3 tools/cmp_tick_handler.py > "$OUT/cmp_times.json" 2> "$OUT/cmp_times.err" || { tail -5 "$OUT/cmp_times.err"; exit 1; }
+      cat "$OUT/cmp_times.json"
+      i=0
+      for grp in "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES" \
+                 "TCC_HIT TCC_MISS TCC_EA0_RDREQ TCC_EA0_WRREQ TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE" "WRITE_SIZE" \
+                 "TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ_LEVEL TCC_EA0_RDREQ_DRAM_CREDIT_STALL TCC_EA0_WRREQ_STALL" \
+                 "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS"; do
+        i=$((i+1))
+        REPS=3 timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/cmp$i" -o c -- python3 tools/cmp_tick_handler.py \
+          > "$OUT/cmp$i.json" 2> "$OUT/cmp$i.err" || { tail -5 "$OUT/cmp$i.err"; exit 1; }
+      done
+      python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>,k_handle_set<4>,k_ae_set_plan,k_gather_args,k_claim_ae" > /dev/null
+      python3 -c "import json; d=json.load(open('$OUT/cmp_counters.json')); [print(k, {c: round(v, 1) for c, v in sorted(x.items())}) for k, x in d.items()]" ;;
+    ctest)
+      echo "== ctest"
+      make -s -C tests/c_host && timeout -k 10 120 tests/c_host/mraft_host_tick tests/golden/tick_vectors.bin 0 | tee "$OUT/c_host.txt" ;;
     trace)
       # kernel trace + stats of the bench (BENCH) -> $OUT/kt
       echo "== trace ${BENCH:-}"

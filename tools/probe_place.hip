@@ -4,8 +4,9 @@
 // group order (contiguous range per XCD, all eight advancing in lockstep);
 // per group it reads the second half of replica 0's row and the third
 // quarter of replicas 1 and 2, and writes the second half of replicas 3 and 4.
-// Built as a shared library (tools/Makefile) and driven by
-// tools/exp_chunk_sets.py (PROBE=1).
+// Built as a shared library (tools/Makefile) and driven by bench.py after its
+// timed region (roofline.placement_probe); the round-2 experiment drivers that
+// also used it are in git history before commit a48e527's housekeeping.
 #include <hip/hip_runtime.h>
 
 // mode: the group each workgroup takes (blockIdx b, XCD x = b mod 8, j = b / 8,
