@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define MRAFT_ABI_VERSION 4
+#define MRAFT_ABI_VERSION 5
 
 /* Node states, raft_rpc.go:8-12 (values preserved). */
 enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
@@ -314,8 +314,14 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity,
 /* Replaces Kill (utility.go:9-19): waits for the engine's queues, frees device
  * state and every stream / queue the engine created. */
 int mraft_destroy(mraft_engine *h);
-/* Use a caller-provided hipStream_t (NULL = the engine's own stream). */
+/* Use a caller-provided hipStream_t (NULL = the engine's own stream); tick
+ * shard launches still outstanding are ordered before the new stream's work. */
 int mraft_set_stream(mraft_engine *h, void *hip_stream);
+/* The engine stream. With tick shards (mraft_set_tick_shards) a tick's
+ * launches run on the shard queues; this call first orders the engine stream
+ * after every outstanding shard launch (a device-side wait, no host wait), so
+ * work the caller enqueues on the returned stream — a copy of group_flags or
+ * of the export words, an event — sees the tick's outputs. */
 void *mraft_get_stream(mraft_engine *h);
 /* Host wait for all work of the handle (engine stream and tick shards). */
 int mraft_synchronize(mraft_engine *h);
@@ -358,15 +364,14 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * of args.Entries at gather time, raft_append_entry.go:50-54). By reference,
  * consecutive items reading the same entries (one leader's messages to its
  * followers, as the gather lays them out) are served together, reading the
- * entries once; items that read a row this call also writes, and the items
- * writing such rows, run after the others, the former from a staged copy.
- * The call then blocks the host until the batch plan is known: the main
- * launch's first workgroup publishes it when that launch starts (the GPU keeps
- * working meanwhile). If the plan is not published within 120 s (a stream
- * blocked on something that never comes) the call fails with MRAFT_E_HIP and
- * the handle is poisoned: the queued launches may still change state when the
- * stream unblocks, the batch's deferred items never run, and every later call
- * on the handle fails with MRAFT_E_HIP. */
+ * entries once; an item whose own row another item of the call reads runs
+ * after the others (deferred), from a staged copy of its entries when its
+ * source row is written in this call too. Every count this takes stays on the
+ * device: with MRAFT_DEVICE the call enqueues its launches and returns without
+ * waiting (calls may be enqueued back to back with no host synchronisation).
+ * Staged entries use the engine's stage (mraft_set_stage_capacity); a batch
+ * that needs more runs its deferred items in an order that needs no stage (one
+ * wave, slower), with the same results. */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,
@@ -386,6 +391,14 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args,
                                    int64_t n_entry_terms, mraft_ae_reply *replies,
                                    mraft_ae_result *results, int32_t *item_err,
                                    int32_t where);
+
+/* Capacity, in entry words, of the device stage mraft_handle_append_entries
+ * copies the entries of deferred by-reference items into (default 4 Mi words,
+ * 16 MiB; allocated on first use). A batch needing more is still handled
+ * exactly, in the ordered fallback. words in [0, 2^31). Returns MRAFT_OK;
+ * mraft_get_stage_capacity returns the current capacity (-1: null handle). */
+int mraft_set_stage_capacity(mraft_engine *h, int64_t words);
+int64_t mraft_get_stage_capacity(const mraft_engine *h);
 
 /* a2 + a1, processAppendEntriesReply + advanceCommitIndexForLeader
  * (raft_append_entry.go:66-105). Items are folded per segment in array order;

@@ -31,7 +31,7 @@ G_SNAPSHOT_INSTALLED = 256
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
 TERMS_SORTED = 1
 AE_ENTRIES_SORTED = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 FANIN_OVERLAP = 1
 FANIN_ORDERED = 2
 COMM_ID_BYTES = 128
@@ -98,6 +98,7 @@ ABI_SYMBOLS = (
     "mraft_comm_unique_id", "mraft_comm_init", "mraft_comm_destroy", "mraft_allgather_status",
     "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
     "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream", "mraft_handle_append_entries_ex",
+    "mraft_set_stage_capacity", "mraft_get_stage_capacity",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -151,6 +152,8 @@ _SIGS = {
     "mraft_handle_append_entries_ex": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i32]),
     "mraft_get_tick_shards": (_i32, [_vp]),
     "mraft_shard_stream": (_vp, [_vp, _i32]),
+    "mraft_set_stage_capacity": (ctypes.c_int, [_vp, _i64]),
+    "mraft_get_stage_capacity": (_i64, [_vp]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

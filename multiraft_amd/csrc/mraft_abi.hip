@@ -7,7 +7,6 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -19,6 +18,8 @@
 #include "mraft_internal.h"
 
 constexpr int kMaxShards = 8;
+// Default capacity of the AppendEntries stage (mraft_set_stage_capacity): 16 MiB.
+constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
 
 struct mraft_engine {
   int32_t G = 0, P = 0, L = 0, device = 0;
@@ -39,17 +40,11 @@ struct mraft_engine {
   hipEvent_t shard_ev[kMaxShards] = {};
   hipEvent_t fork_ev = nullptr;
   bool shards_pending = false;
-  // a call that failed with work still queued that may change state later
-  // (the handle call's plan-poll timeout): every later call fails
-  bool poisoned = false;
-  std::string poison_msg;
   unsigned long long *claim = nullptr;
-  uint32_t *srcmark = nullptr;             // per slot: epoch of the last call that read its row while writing it
+  uint32_t *srcmark = nullptr;             // per slot: epoch of the last call that read its row
   uint32_t epoch = 0;
-  unsigned long long *plan_host = nullptr;  // pinned, device-written: the AppendEntries plan's totals
-  unsigned long long *plan_host_dev = nullptr;
-  unsigned long long *plan_dev = nullptr;   // the plan's accumulators (0-3) and published totals (4-6)
-  unsigned long long plan_seq = 0;
+  unsigned long long *ae_total = nullptr;  // AppendEntries by reference: staged words, deferred items << 32
+  int64_t stage_cap = kDefaultStageWords;  // words of staged entries the deferred launch may use
   std::vector<void *> scratch_ptr;
   std::vector<size_t> scratch_cap;
 };
@@ -57,11 +52,6 @@ struct mraft_engine {
 namespace {
 
 thread_local std::string g_err;
-
-// mraft_handle_append_entries waits on the host for its plan's totals (a
-// pinned word the plan kernel writes); a stream that never reaches the plan
-// fails the call after this long instead of hanging the caller.
-constexpr int kPlanPollSeconds = 120;
 
 int fail(int code, const char *fmt, ...) {
   char buf[512];
@@ -116,7 +106,6 @@ size_t arr_bytes(const mraft_engine *h, int kind) {
 
 int check(const mraft_engine *h) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
-  if (h->poisoned) return fail(MRAFT_E_HIP, "engine unusable after an earlier failure: %s", h->poison_msg.c_str());
   if (!h->bound) return fail(MRAFT_E_NOSTATE, "engine has no device state bound");
   return MRAFT_OK;
 }
@@ -381,8 +370,7 @@ int mraft_destroy(mraft_engine *h) {
     if (p) (void)hipFree(p);
   if (h->claim) (void)hipFree(h->claim);
   if (h->srcmark) (void)hipFree(h->srcmark);
-  if (h->plan_host) (void)hipHostFree(h->plan_host);
-  if (h->plan_dev) (void)hipFree(h->plan_dev);
+  if (h->ae_total) (void)hipFree(h->ae_total);
   if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
   if (h->fanin_masked) (void)hipStreamSynchronize(h->fanin_masked);
   destroy_shard_queues(h);
@@ -401,7 +389,17 @@ int mraft_set_stream(mraft_engine *h, void *stream) {
   return join_shards(h);
 }
 
-void *mraft_get_stream(mraft_engine *h) { return h ? (void *)h->stream : nullptr; }
+// With tick shards, the engine stream is first ordered after the outstanding
+// shard launches (a device-side wait), so work the caller puts on the returned
+// stream sees the tick's outputs.
+void *mraft_get_stream(mraft_engine *h) {
+  if (!h) return nullptr;
+  if (h->shards_pending) {
+    (void)hipSetDevice(h->device);
+    (void)join_shards(h);
+  }
+  return (void *)h->stream;
+}
 
 int mraft_synchronize(mraft_engine *h) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
@@ -564,84 +562,49 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   TRY(sg.map(replies, sizeof(mraft_ae_reply) * n, false, true, &r));
   TRY(sg.map(results, sizeof(mraft_ae_result) * n, false, true, &rs));
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
-  const int32_t *src = en ? (const int32_t *)en : h->dev.log_term;
-  const int64_t src_n = en ? n_entry_terms : gp_of(h) * h->L;
-  const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
-  if (en) {  // entries in a host-supplied buffer: one message per wave
+  if (en) {  // entries in a caller buffer: one message per wave, nothing is read while written
     mraft::launch_claim(a, n, sizeof(mraft_ae_args), offsetof(mraft_ae_args, slot), nullptr, gp_of(h), h->P,
                         h->claim, h->epoch, (int32_t *)e, h->stream);
-    mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, nullptr, nullptr, 0,
-                            nullptr, 1, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, (mraft_ae_result *)rs, h->stream);
+    mraft::launch_handle_ae_host(dev_of(h), (const mraft_ae_args *)a, n, (const int32_t *)en, n_entry_terms,
+                                 (mraft_ae_reply *)r, (int32_t *)e, (mraft_ae_result *)rs, h->stream);
     return sg.finish();
   }
-  // Entries by reference into the engine's log: messages reading the same
-  // entries form sets served by one wave each (the main launch); items that
-  // read or write a row another item of this batch writes or reads are
-  // deferred to a second launch, the readers' entries staged first (the
-  // reference's copy at gather time, raft_append_entry.go:50-54). The plan's
-  // totals reach the host (pinned words the main launch's first workgroup
-  // writes) while the main launch runs.
-  if (!h->plan_host) {
-    HIP_TRY(hipHostMalloc((void **)&h->plan_host, 4 * sizeof(unsigned long long),
-                          hipHostMallocMapped | hipHostMallocCoherent));
-    HIP_TRY(hipHostGetDevicePointer((void **)&h->plan_host_dev, h->plan_host, 0));
-    h->plan_host[3] = 0;
-    if (hipMalloc(&h->plan_dev, 8 * sizeof(unsigned long long)) != hipSuccess)
-      return fail(MRAFT_E_NOMEM, "plan counters alloc failed");
-    HIP_TRY(hipMemsetAsync(h->plan_dev, 0, 8 * sizeof(unsigned long long), h->stream));
+  // Entries by reference into the engine's log: the claims with the set
+  // heads, the main launch, the deferred launch — three launches, every count
+  // they need stays on the device, nothing waits on the host (mraft_kernels.hip
+  // "a4" for the rules).
+  if (!h->ae_total) {
+    if (hipMalloc(&h->ae_total, 2 * sizeof(unsigned long long)) != hipSuccess)
+      return fail(MRAFT_E_NOMEM, "AppendEntries counters alloc failed");
+    HIP_TRY(hipMemsetAsync(h->ae_total, 0, 2 * sizeof(unsigned long long), h->stream));
   }
-  void *soff, *sets, *defer, *stage = nullptr;
+  void *sethd, *soff, *defer, *order, *stage = nullptr;
   TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
-  TRY(scratch(h, 17, sizeof(int64_t) * (size_t)n, &sets));
+  TRY(scratch(h, 15, (size_t)n, &sethd));
   TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
-  mraft::launch_claim_ae((const mraft_ae_args *)a, n, src_n, h->L, gp_of(h), h->claim, h->srcmark, h->epoch,
-                         (int32_t *)e, h->plan_dev, h->stream);
-  mraft::launch_ae_set_plan((const mraft_ae_args *)a, n, src_n, h->L, ni, h->claim, h->srcmark, h->epoch,
-                            (int32_t *)e, (int64_t *)soff, (int64_t *)sets, (int64_t *)defer, h->plan_dev, h->stream);
-  // main launch: grid sized by the upper bound n, the set count read on the
-  // device (the plan's packed counter plan_dev[1]); its first workgroup writes
-  // the totals to the host's pinned words, then the sequence word
-  mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, nullptr, 0, (const int64_t *)soff,
-                          (const int64_t *)sets, n, h->plan_dev + 1, ni, (mraft_ae_reply *)r, (int32_t *)e,
-                          h->plan_host_dev, ++h->plan_seq, (mraft_ae_result *)rs, h->stream);
-  volatile unsigned long long *ph = h->plan_host;
-  const auto t_poll = std::chrono::steady_clock::now();
-  for (unsigned spin = 1; ph[3] != h->plan_seq; ++spin) {
-    if ((spin & 4095) == 0) {  // the stream drained (or failed) without the word: stop polling
-      const hipError_t q = hipStreamQuery(h->stream);
-      if (q == hipErrorNotReady) {
-        // work queued ahead of the plan may take a while, but not forever (e.g.
-        // a stream waiting on a host-side dependency that never comes)
-        if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(kPlanPollSeconds)) {
-          // the claim, plan and main launch stay queued and will still change
-          // follower state when the stream unblocks, while the deferred items
-          // never run: the batch would be half-applied, so the engine refuses
-          // every later call
-          h->poisoned = true;
-          h->poison_msg = "an AppendEntries batch was left half-applied (plan-poll timeout)";
-          return fail(MRAFT_E_HIP, "append plan not published after %d s (stream blocked?); engine poisoned",
-                      kPlanPollSeconds);
-        }
-        continue;
-      }
-      HIP_TRY(q);
-      if (ph[3] != h->plan_seq) return fail(MRAFT_E_HIP, "append plan did not publish its totals");
-    }
-  }
-  const unsigned long long staged = ph[0], n_defer = ph[2];
-  if (n_defer > 0) {
-    if (staged > 0) {
-      TRY(scratch(h, 16, sizeof(int32_t) * (size_t)staged, &stage));
-      mraft::launch_ae_stage_copy(h->dev.log_term, h->dev.log_head, h->L, (const mraft_ae_args *)a, n,
-                                  (const int64_t *)soff, (int32_t *)stage, h->stream);
-    }
-    mraft::launch_handle_ae(dev_of(h), (const mraft_ae_args *)a, n, src, src_n, (const int32_t *)stage,
-                            (int64_t)staged, (const int64_t *)soff, (const int64_t *)defer, (int64_t)n_defer,
-                            nullptr, ni, (mraft_ae_reply *)r, (int32_t *)e, nullptr, 0, (mraft_ae_result *)rs,
-                            h->stream);
-  }
+  // the ordered fallback's in-degrees and queue (n each) and cycle buffer (L)
+  TRY(scratch(h, 19, sizeof(int32_t) * (2 * (size_t)n + (size_t)h->L), &order));
+  if (h->stage_cap > 0) TRY(scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage));
+  const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
+  const int64_t n_log = gp_of(h) * h->L;
+  int32_t *kin = (int32_t *)order, *kq = kin + n, *cyc = kq + n;
+  mraft::launch_claim_ae((const mraft_ae_args *)a, n, n_log, h->L, gp_of(h), ni, h->claim, h->srcmark, h->epoch,
+                         (int32_t *)e, (uint8_t *)sethd, h->ae_total, h->stream);
+  mraft::launch_handle_ae_ref(dev_of(h), (const mraft_ae_args *)a, n, ni, h->claim, h->srcmark, h->epoch,
+                              (int32_t *)e, (const uint8_t *)sethd, (int64_t *)soff, (int64_t *)defer, h->ae_total,
+                              (int32_t *)stage, stage ? h->stage_cap : 0, kin, kq, cyc, (mraft_ae_reply *)r,
+                              (mraft_ae_result *)rs, h->stream);
   return sg.finish();
 }
+
+int mraft_set_stage_capacity(mraft_engine *h, int64_t words) {
+  TRY(enter(h));
+  if (words < 0 || words > INT32_MAX) return fail(MRAFT_E_INVAL, "stage capacity %lld out of [0, 2^31)", (long long)words);
+  h->stage_cap = words;
+  return MRAFT_OK;
+}
+
+int64_t mraft_get_stage_capacity(const mraft_engine *h) { return h ? h->stage_cap : -1; }
 
 int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, int64_t n,
                                  const int64_t *seg_begin, int64_t n_seg, int32_t *out_flags,

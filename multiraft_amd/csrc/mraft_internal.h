@@ -26,20 +26,19 @@ void launch_claim(const void *items, int64_t n, int stride, int slot_off, const 
 
 void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers, int64_t n,
                         mraft_ae_args *out, int32_t *err, hipStream_t st);
-void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp,
-                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err,
+// AppendEntries by reference (mraft_handle_append_entries, entry_terms NULL):
+// the claims and the set heads (sethd, one byte per item), then the main and
+// the deferred launch, every count on the device (kernels: mraft_kernels.hip).
+void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp, int ni,
+                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, uint8_t *sethd,
                      unsigned long long *total, hipStream_t st);
-void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
-                        const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
-                        int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
-                        unsigned long long *total, hipStream_t st);
-void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
-                          const int64_t *soff, int32_t *stage, hipStream_t st);
-void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
-                      const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
-                      int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
-                      int32_t *err, unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
-                      hipStream_t st);
+void launch_handle_ae_ref(const Dev &s, const mraft_ae_args *args, int64_t n, int ni, const unsigned long long *claim,
+                          const uint32_t *srcmark, uint32_t epoch, int32_t *err, const uint8_t *sethd, int64_t *soff,
+                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap, int32_t *kin,
+                          int32_t *kq, int32_t *cyc, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st);
+// AppendEntries with the entries in a caller buffer (claims by launch_claim).
+void launch_handle_ae_host(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
+                           mraft_ae_reply *rep, int32_t *err, mraft_ae_result *res, hipStream_t st);
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
                  int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st);

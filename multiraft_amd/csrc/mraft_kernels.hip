@@ -155,211 +155,145 @@ __global__ void k_gather_args(Dev s, const int32_t *__restrict__ slots,
 }
 
 // ---------------------------------------------------------------- a4
-// One wave per item: uniform prologue, wave-cooperative conflict scan / merge.
-#ifndef MRAFT_AE_WPB
-#define MRAFT_AE_WPB 1  // messages (waves) per workgroup of the AppendEntries handler (1: 6 % faster than 4)
-#endif
-#ifndef MRAFT_AE_XCD
-#define MRAFT_AE_XCD 1  // each XCD takes a contiguous range of workgroups: a group's consecutive
-                        // messages share one L2 for the leader entries (another 8 %)
-#endif
-
+// HandleAppendEntries (raft_append_entry.go:108-162, matchLog
+// raft_log.go:92-96), message-level, fully on the device: the host enqueues
+// three launches and returns (round 5; rounds 2-4 polled a pinned word for
+// the batch plan before enqueuing the second half).
+//
 // Entries by reference into the engine's own log (entry_terms NULL):
 // entries_offset = source slot * L + (Index - dummy) of the first entry, a
 // logical position in that replica's ring. The reference copies args.Entries
 // when it builds the message (appendOneRound, raft_append_entry.go:50-54),
-// before any handler runs; here they are read in place from the source ring
-// (see below for rows this batch also writes: a stale second leader).
+// before any handler runs, so every item must see its source row as it was
+// before the call, even when another item of the batch writes that row (two
+// leaders of one group). Per item, from the claims of k_claim_ae (the lowest
+// item addressed to a slot owns it; srcmark marks every row some item reads):
+//   read   its source row is written by an item of this batch (claimed);
+//   written  its own slot is some item's source row (srcmark).
+// An item that is not `written` runs in the MAIN launch, reading its source in
+// place (a row some item reads and another writes belongs to a `written`
+// item, which is deferred: the row is pristine throughout the main launch).
+// A `written` item is DEFERRED to a second launch,
+// after every main item has read what it needs; if it is also `read`, its
+// entries are staged (copied by the main launch, whose items never write the
+// rows deferred items read) and the deferred launch reads the copy. Deferred
+// items are independent given the copies and run in parallel. When the
+// staged words exceed the stage capacity (mraft_set_stage_capacity), the
+// deferred launch instead orders them itself on one wave: an item that reads a
+// row runs before that row's writer (each item has at most one writer ahead of
+// it, so the order is a forest of chains feeding cycles), and a cycle is
+// broken by copying one member's entries to an L-word buffer first.
 //
 // Messages that read the same entries (same source row, same ring position of
 // Index 0, same last Index: the P-1 messages one leader's gather makes for
 // its followers, consecutive in the batch) form a *set*, up to NI messages,
 // served by one wave with one streaming pass over the shared entries, as the
-// fused tick serves a group (mraft_pass.h). A message whose run of same-entry
-// predecessors is NI or longer is a set of its own, so membership is decided
-// from at most NI neighbours on each side.
-//
-// Entries whose source row this batch also writes must be read as they were
-// before the call. k_ae_src_mark marks every source row that is also a
-// receiving slot (claim epoch set by k_claim); the items reading such a row
-// (staged: their entries are copied out first) and the items writing one are
-// *deferred*: handled by a second launch after the main one, which touches
-// neither kind of row. The host learns whether a deferred launch is needed
-// from a readback that overlaps the main launch.
-//
-// k_ae_set_plan decides per item:
-//   soff = -1      malformed reference (MRAFT_ITEM_BAD_SLOT);
-//   soff = -2      read in place through the source ring;
-//   soff >= 0      staged at stage[soff];
-// and appends every main set's first item to `sets` (first * 8 + size - 1)
-// and every deferred item to `defer` (item * 8); total = {staged words,
-// main sets, deferred items}.
+// fused tick serves a group (mraft_pass.h). k_claim_ae cuts the sets from the
+// keys alone (a message whose run of same-entry predecessors is NI or longer is
+// a set of its own) and writes each head's size; the main launch's wave v
+// serves the sets whose heads lie in items [v*NI, (v+1)*NI) — one set per
+// wave for a gathered batch — masking members that turn out to be
+// duplicates, malformed or deferred.
 struct AeKey {
-  int64_t row;  // source slot
+  int64_t row;  // source slot (-1: no key, a set of its own)
   int base;     // ring position of the entries, relative: (offset mod L) - (prev + 1)
   int end;      // Index of the last entry
 };
-
-enum : int { AK_DUP = -3, AK_ERR = -2, AK_BAD = -1, AK_RING = 0, AK_STAGED = 1, AK_WRITER = 2 };
 
 __device__ __forceinline__ bool ae_ref_ok(const mraft_ae_args &a, int64_t n_log, int L) {
   return !(a.n_entries < 0 || a.entries_offset < 0 || a.entries_offset + a.n_entries > n_log ||
            a.entries_offset % L + a.n_entries > L);
 }
 
-// Item i's kind. `dup`: check item i's claim (the plan's own duplicate-slot
-// verdict: the lowest item addressed to a slot wins, k_claim_ae's atomicMax).
-__device__ __forceinline__ int ae_kind(const mraft_ae_args &a, int e, int64_t i, bool dup, int64_t n_log, int L,
-                                       const unsigned long long *__restrict__ claim,
-                                       const uint32_t *__restrict__ srcmark, uint32_t epoch, AeKey &key) {
-  if (e) return AK_ERR;
-  if (dup && claim[a.slot] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i))) return AK_DUP;
-  if (!ae_ref_ok(a, n_log, L)) return AK_BAD;
-  key.row = a.entries_offset / L;
-  key.base = (int)(a.entries_offset % L) - (a.prev_log_index + 1);
-  key.end = a.prev_log_index + a.n_entries;
-  if (a.n_entries > 0 && (uint32_t)(claim[key.row] >> 32) == epoch) return AK_STAGED;
-  if (srcmark && srcmark[a.slot] == epoch) return AK_WRITER;
-  return AK_RING;
+__device__ __forceinline__ unsigned long long claim_tag(uint32_t epoch, int64_t i) {
+  return ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i);
 }
 
-// The claims of AppendEntries by reference (k_claim's slot check and
-// atomicMax), and in the same pass the source rows: srcmark[row] = epoch for
-// every row some item reads entries from. The plan then finds the items
-// whose receiving row is read by another (srcmark of their slot) and the
-// duplicate slots (claim word) itself: one launch fewer than a separate
-// check. (An item that turns out to be a duplicate still marked its source;
-// that can only stage or defer some other item needlessly, never change a
-// result: staged entries are the pre-call entries.)
-__global__ void k_claim_ae(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log, int L, int64_t gp,
-                           unsigned long long *__restrict__ claim, uint32_t *__restrict__ srcmark, uint32_t epoch,
-                           int32_t *__restrict__ err, unsigned long long *__restrict__ total) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i == 0) {  // arm the plan's accumulators (the previous call's handler has read them)
+__device__ __forceinline__ AeKey ae_key(const mraft_ae_args &a, int64_t gp, int64_t n_log, int L) {
+  if (a.slot < 0 || a.slot >= gp || !ae_ref_ok(a, n_log, L)) return AeKey{-1, 0, 0};
+  return AeKey{a.entries_offset / L, (int)(a.entries_offset % L) - (a.prev_log_index + 1),
+               a.prev_log_index + a.n_entries};
+}
+
+__device__ __forceinline__ bool same_key(const AeKey &x, const AeKey &y) {
+  return x.row >= 0 && x.row == y.row && x.base == y.base && x.end == y.end;
+}
+
+// The claims of AppendEntries by reference and the set heads, one launch
+// (rounds 2-4: a claim kernel, then a plan kernel that classified every item
+// and compacted set and deferral lists through contended atomics). Per item:
+// the slot check and the claim (atomicMax: the lowest item wins), srcmark of
+// the row it reads, and sethd[i] = the size of the set item i heads, else 0
+// (keys of the neighbours within kAeHalo from LDS, the halo loaded by the
+// wave's edge lanes). Its first thread also arms the counters the main launch
+// adds into (total[0]: staged words, total[1]: deferred items << 32); the
+// previous call's deferred launch has read them (stream order).
+constexpr int kAeHalo = 7;
+
+__global__ __launch_bounds__(64) void k_claim_ae(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log,
+                                                 int L, int64_t gp, int ni, unsigned long long *__restrict__ claim,
+                                                 uint32_t *__restrict__ srcmark, uint32_t epoch,
+                                                 int32_t *__restrict__ err, uint8_t *__restrict__ sethd,
+                                                 unsigned long long *__restrict__ total) {
+  __shared__ long long kr[64 + 2 * kAeHalo];
+  __shared__ int kb[64 + 2 * kAeHalo], ke[64 + 2 * kAeHalo];
+  const int t = (int)threadIdx.x;
+  const int64_t i = blockIdx.x * (int64_t)64 + t;
+  if (i == 0) {
     total[0] = 0;
     total[1] = 0;
   }
-  if (i >= n) return;
-  const mraft_ae_args a = args[i];
-  if (a.slot < 0 || a.slot >= gp) { err[i] = MRAFT_ITEM_BAD_SLOT; return; }
-  err[i] = 0;
-  atomicMax(&claim[a.slot], ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i));
-  if (a.n_entries > 0 && ae_ref_ok(a, n_log, L)) srcmark[a.entries_offset / L] = epoch;
-}
-
-// Appends `va` (when `wa`) to la and `vb` (when `wb`) to lb, with one
-// 64-bit atomic per workgroup on `count` (la's count in the low word).
-template <int NW>
-__device__ __forceinline__ void block_append2(bool wa, int64_t va, int64_t *__restrict__ la, bool wb, int64_t vb,
-                                              int64_t *__restrict__ lb, unsigned long long *__restrict__ count,
-                                              int *lds) {
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const unsigned long long ma = __ballot(wa), mb = __ballot(wb);
-  if (lane == 0) { lds[w] = __popcll(ma); lds[NW + 1 + w] = __popcll(mb); }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int ta = 0, tb = 0;
-    for (int j = 0; j < NW; ++j) {
-      const int ca = lds[j], cb = lds[NW + 1 + j];
-      lds[j] = ta; lds[NW + 1 + j] = tb;
-      ta += ca; tb += cb;
-    }
-    const unsigned long long inc = ((unsigned long long)tb << 32) | (unsigned)ta;
-    const unsigned long long base = inc ? atomicAdd(count, inc) : 0;
-    lds[NW] = (int)(base & 0xFFFFFFFFu);
-    lds[2 * NW + 1] = (int)(base >> 32);
-  }
-  __syncthreads();
-  if (wa) la[(int64_t)lds[NW] + lds[w] + __popcll(ma & ((1ull << lane) - 1))] = va;
-  if (wb) lb[(int64_t)lds[2 * NW + 1] + lds[NW + 1 + w] + __popcll(mb & ((1ull << lane) - 1))] = vb;
-}
-
-// One workgroup of kAePlanT threads plans kAeOwn items: every thread
-// classifies one item (its own or a neighbour within kAeHalo on either side)
-// into LDS, then each owned item finds its place in its run from LDS.
-#ifndef MRAFT_AE_PLAN_T
-#define MRAFT_AE_PLAN_T 1024  // plan workgroup size (items classified per workgroup, halo included)
-#endif
-constexpr int kAePlanT = MRAFT_AE_PLAN_T, kAeHalo = 7, kAeOwn = kAePlanT - 2 * kAeHalo;
-
-__global__ __launch_bounds__(kAePlanT) void k_ae_set_plan(const mraft_ae_args *__restrict__ args, int64_t n,
-                                                     int64_t n_log, int L, int ni,
-                                                     const unsigned long long *__restrict__ claim,
-                                                     const uint32_t *__restrict__ srcmark, uint32_t epoch,
-                                                     int32_t *__restrict__ err, int64_t *__restrict__ soff,
-                                                     int64_t *__restrict__ sets, int64_t *__restrict__ defer,
-                                                     unsigned long long *__restrict__ total) {
-  constexpr int NW = kAePlanT / 64;
-  __shared__ int lds[2 * NW + 2];
-  __shared__ int kd[kAePlanT], kb[kAePlanT], ke[kAePlanT];
-  __shared__ long long kr[kAePlanT];
-  const int t = threadIdx.x;
-  const int64_t i = blockIdx.x * (int64_t)kAeOwn - kAeHalo + t;
   AeKey k{-1, 0, 0};
-  // err[i] holds k_claim_ae's slot verdict; the duplicate verdict is taken
-  // here from the claim word (and written by the item's owner below)
-  const int kind = (i >= 0 && i < n) ? ae_kind(args[i], err[i], i, true, n_log, L, claim, srcmark, epoch, k) : -9;
-  kd[t] = kind; kr[t] = k.row; kb[t] = k.base; ke[t] = k.end;
-  __syncthreads();
-  const bool own = t >= kAeHalo && t < kAeHalo + kAeOwn && i < n;
-  if (own) {
-    if (kind == AK_DUP) err[i] = MRAFT_ITEM_DUP_SLOT;
-    int64_t o = -1;
-    if (kind == AK_STAGED) o = (int64_t)atomicAdd(&total[0], (unsigned long long)args[i].n_entries);
-    else if (kind >= AK_RING) o = -2;
-    soff[i] = o;
-  }
-  int64_t head = -1;  // first * 8 + (size - 1) when item i starts a main set
-  if (own && kind < AK_STAGED) {
-    int pos = 0;  // this item's place in its run of same-entry messages (up to ni back)
-    if (kind == AK_RING)
-      for (int d = 1; d <= ni && kd[t - d] == AK_RING && kr[t - d] == k.row && kb[t - d] == k.base &&
-                      ke[t - d] == k.end; ++d)
-        ++pos;
-    if (kind != AK_RING || pos >= ni) {
-      head = i * 8;
-    } else if (pos == 0) {
-      int cnt = 1;  // the set's size (up to ni forward)
-      for (int d = 1; d < ni && kd[t + d] == AK_RING && kr[t + d] == k.row && kb[t + d] == k.base &&
-                      ke[t + d] == k.end; ++d)
-        ++cnt;
-      head = i * 8 + (cnt - 1);
+  if (i < n) {
+    const mraft_ae_args a = args[i];
+    if (a.slot < 0 || a.slot >= gp) {
+      err[i] = MRAFT_ITEM_BAD_SLOT;
+    } else {
+      err[i] = 0;
+      atomicMax(&claim[a.slot], claim_tag(epoch, i));
+      k = ae_key(a, gp, n_log, L);
+      if (a.n_entries > 0 && k.row >= 0) srcmark[k.row] = epoch;
     }
   }
-  block_append2<NW>(head >= 0, head, sets, own && kind >= AK_STAGED, i * 8, defer, &total[1], lds);
-  // The totals stay in the device accumulators (total[0]: staged words,
-  // total[1]: main sets | deferred items << 32); the main handler launch reads
-  // its set count there and its first workgroup publishes them to the host.
-  // (Round 2 had the plan's last workgroup publish them: one more contended
-  // atomic per workgroup and a serial tail, ~5 us.)
-}
-
-__global__ void k_ae_stage_copy(const int32_t *__restrict__ log, const int32_t *__restrict__ head, int L,
-                                const mraft_ae_args *__restrict__ args, int64_t n,
-                                const int64_t *__restrict__ soff, int32_t *__restrict__ stage) {
-  const int64_t i = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  kr[kAeHalo + t] = k.row; kb[kAeHalo + t] = k.base; ke[kAeHalo + t] = k.end;
+  if (t < kAeHalo || t >= 64 - kAeHalo) {  // the halo: kAeHalo neighbours on either side of the wave
+    const int64_t j = t < kAeHalo ? i - kAeHalo : i + kAeHalo;
+    AeKey h{-1, 0, 0};
+    if (j >= 0 && j < n) h = ae_key(args[j], gp, n_log, L);
+    const int slot = t < kAeHalo ? t : t + 2 * kAeHalo;
+    kr[slot] = h.row; kb[slot] = h.base; ke[slot] = h.end;
+  }
+  __syncthreads();
   if (i >= n) return;
-  const int64_t o = soff[i];
-  if (o < 0) return;
-  const mraft_ae_args a = args[i];
-  const int64_t r = a.entries_offset / L;
-  wave_copy_from_ring(log + r * L, 0, head[r], L, (int)(a.entries_offset % L), stage + o, a.n_entries);
+  int hd = 0;
+  const int c = kAeHalo + t;
+  int pos = 0;  // this item's place in its run of same-entry messages (up to ni back)
+  if (k.row >= 0)
+    for (int d = 1; d <= ni && same_key(k, AeKey{kr[c - d], kb[c - d], ke[c - d]}); ++d) ++pos;
+  if (k.row < 0 || pos >= ni) {
+    hd = 1;
+  } else if (pos == 0) {
+    hd = 1;  // the set's size (up to ni forward)
+    for (int d = 1; d < ni && same_key(k, AeKey{kr[c + d], kb[c + d], ke[c + d]}); ++d) ++hd;
+  }
+  sethd[i] = (uint8_t)hd;
 }
 
-// a4, HandleAppendEntries (raft_append_entry.go:108-162, matchLog
-// raft_log.go:92-96) for one set of messages per wave: lane q < size takes
-// message first+q's prologue (its args, the receiving follower's scalars,
+// a4 for one set of messages per wave: lane q < size takes message first+q's
+// prologue (its args, the claims, the receiving follower's scalars,
 // log[prev]); conflict scans run wave-wide one message at a time; every
 // merging message joins one streaming pass over the shared entries
-// (mraft_pass.h). `sets` NULL: message i = workgroup i, a set of one (entries
-// from a host buffer).
-enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE };
+// (mraft_pass.h).
+enum : int { AE_DEFER = -1, AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE };
+// The three ways handle_one is entered.
+enum : int {
+  HM_MAIN = 0,   // by reference, the main launch: classify, defer `written` items
+  HM_DEFER = 1,  // by reference, a deferred item: entries staged (soff >= 0) or in place (-2)
+  HM_HOST = 2    // entries in a host-supplied buffer: one message per wave, nothing deferred
+};
 
 #ifndef MRAFT_AE_MINW
 #define MRAFT_AE_MINW 8  // __launch_bounds__ minimum waves per SIMD of the handler
-#endif
-#ifndef MRAFT_AE_SPB
-#define MRAFT_AE_SPB 4  // main launch: grid = the item count / this (sets per workgroup at most)
 #endif
 #ifndef MRAFT_AE_STASH
 #define MRAFT_AE_STASH 1  // park the per-lane reply inputs in LDS across the pass
@@ -368,47 +302,43 @@ enum : int { AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE_MISS, AE_MERGE
 #define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
 #endif
 
-#ifndef MRAFT_AE_PDIRTY_ATOMIC
-#define MRAFT_AE_PDIRTY_ATOMIC 1  // the handler's persist marks as non-returning atomic ORs (0: load, OR, store)
-#endif
-// The handler's mark at the end of a set's wave as a non-returning atomic OR:
-// the wave does not wait for a load of the bits (a dependent round trip at
-// its very end). Same-box A/B: handle call -8 us on average over three passes
-// (profiles/r3_v8/message_path_ab.txt, r3w); the same change in the fused
-// tick measured +0.7 % there and is not used.
+// The handler's persist mark at the end of a set's wave as a non-returning
+// atomic OR: the wave does not wait for a load of the bits (a dependent round
+// trip at its very end). Same-box A/B: handle call -8 us on average over three
+// passes (profiles/r3_v8/message_path_ab.txt, r3w); the same change in the
+// fused tick measured +0.7 % there and is not used.
 __device__ __forceinline__ void mark_persist_ae(const Dev &s, int64_t slot, int bits) {
-  if (MRAFT_AE_PDIRTY_ATOMIC) {
-    if (s.pdirty && bits) (void)__hip_atomic_fetch_or(&s.pdirty[slot], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    mark_persist(s, slot, bits);
-  }
+  if (s.pdirty && bits) (void)__hip_atomic_fetch_or(&s.pdirty[slot], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 #ifndef MRAFT_AE_RELOAD
 #define MRAFT_AE_RELOAD 1  // after the pass, kernel arguments re-read from the kernarg segment (not held across it)
 #endif
 
-// Every argument of k_handle_set, as its one kernel argument: the handler
-// re-reads them from the kernel-argument segment after the streaming pass
-// (reload_hs) instead of holding ~16 pointers live across it (at 8 waves per
-// SIMD they spilled through VGPR lanes to scratch: 28 B per lane, ~100 MB of
-// scratch write-back per config-#3 call).
+// Every argument of the handler kernels, as their one kernel argument: the
+// handler re-reads them from the kernel-argument segment after the streaming
+// pass (reload_hs) instead of holding ~16 pointers live across it (at 8 waves
+// per SIMD they spilled through VGPR lanes to scratch: 28 B per lane, ~100 MB
+// of scratch write-back per config-#3 call).
 struct HsArgs {
   Dev s;
   const mraft_ae_args *args;
   int64_t n;
-  const int32_t *ent0;
+  const int32_t *ent0;  // HM_HOST: the entries buffer
   int64_t n_ent0;
-  const int32_t *stage;
-  int64_t n_stage;
-  const int64_t *soff, *sets;
-  int64_t n_sets;
-  const unsigned long long *set_count;  // the plan's packed counter (main sets in the low word, deferred items
-                                        // in the high word); set_count[-1] is its staged-word count
+  int32_t *stage;       // staged entries of deferred `read` items (the cycle buffer in the fallback)
+  int64_t stage_cap;    // its capacity in words
+  int64_t *soff;        // per deferred item: its staged offset, or -2 (in place)
+  const uint8_t *sethd; // per item: the size of the set it heads, else 0
+  int64_t *defer;       // the deferred items
+  unsigned long long *total;  // [0] staged words, [1] deferred items << 32
+  const unsigned long long *claim;
+  const uint32_t *srcmark;
+  uint32_t epoch;
+  int32_t *kin, *kq;    // fallback order: in-degree per item, queue
+  int32_t *cyc;         // fallback cycle buffer (L words)
   mraft_ae_reply *rep;
   int32_t *err;
-  volatile unsigned long long *host_total;  // main launch: workgroup 0 publishes the plan's totals here
-  unsigned long long seq;
   mraft_ae_result *res;  // optional: each item's reply as its co-resident leader folds it
 };
 
@@ -422,9 +352,9 @@ __device__ __forceinline__ HsArgs reload_hs() {
   k.s.log = kp->s.log; k.s.match = kp->s.match; k.s.next = kp->s.next; k.s.pdirty = kp->s.pdirty;
   k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.srt = kp->s.srt; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
   k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
-  k.n_stage = kp->n_stage; k.soff = kp->soff; k.sets = kp->sets; k.n_sets = kp->n_sets;
-  k.set_count = kp->set_count; k.rep = kp->rep; k.err = kp->err; k.host_total = kp->host_total; k.seq = kp->seq;
-  k.res = kp->res;
+  k.stage_cap = kp->stage_cap; k.soff = kp->soff; k.sethd = kp->sethd; k.defer = kp->defer; k.total = kp->total;
+  k.claim = kp->claim; k.srcmark = kp->srcmark; k.epoch = kp->epoch; k.kin = kp->kin; k.kq = kp->kq; k.cyc = kp->cyc;
+  k.rep = kp->rep; k.err = kp->err; k.res = kp->res;
   return k;
 }
 
@@ -438,72 +368,143 @@ __device__ __forceinline__ int4 no_record() {
   return make_int4(m, m, z, z);
 }
 
-template <int NI>
-__device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int size) {
+// The number of set bits of m below this lane (v_mbcnt: no per-lane mask
+// register, which the compiler would hoist and hold across the pass).
+__device__ __forceinline__ int lanes_below(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The main launch's bookkeeping for the `written` lanes of a wave (rare: a
+// stale leader both sending and receiving in one batch): their place in the
+// deferred list, and for those that also `read`, a staged offset and the copy
+// of their entries (the source row is pristine: its writer is deferred too).
+__device__ __forceinline__ void defer_lanes(const HsArgs &k0, bool dfr, bool stg, int64_t i, int n, const int32_t *row,
+                                            int head, int from, int L) {
+  const unsigned long long m = __ballot(dfr);
+  const int lane = lane_id(), q0 = first_lane(m);
+  unsigned long long b = 0;
+  if (lane == q0) b = atomicAdd(&k0.total[1], (unsigned long long)__popcll(m) << 32) >> 32;
+  b = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), q0) << 32) |
+      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, q0);
+  if (dfr) {
+    k0.defer[b + lanes_below(m)] = i;
+    int64_t in_place = -2;  // made here (as a hoisted constant pair it was spilled across the pass)
+    asm volatile("" : "+v"(in_place));
+    if (!stg) k0.soff[i] = in_place;
+  }
+  for (unsigned long long sm = __ballot(stg); sm; sm &= sm - 1) {
+    const int q = first_lane(sm);
+    const int nq = __builtin_amdgcn_readlane(n, q);
+    unsigned long long o = 0;
+    if (lane == q) {
+      o = atomicAdd(&k0.total[0], (unsigned long long)nq);
+      k0.soff[i] = (int64_t)o;
+    }
+    o = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(o >> 32), q) << 32) |
+        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o, q);
+    if ((long long)o + nq <= k0.stage_cap) {  // past the capacity the deferred launch takes the ordered fallback
+      const uint64_t ra = (uint64_t)(uintptr_t)row;
+      const int32_t *rq = (const int32_t *)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(ra >> 32), q) << 32) |
+                                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ra, q));
+      wave_copy_from_ring(rq, 0, __builtin_amdgcn_readlane(head, q), L, __builtin_amdgcn_readlane(from, q),
+                          k0.stage + o, nq);
+    }
+  }
+}
+
+template <int NI, int MODE>
+__device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int size, int64_t so_force = -2) {
   const Dev &s = k0.s;
   const mraft_ae_args *__restrict__ args = k0.args;
-  const int32_t *__restrict__ ent0 = k0.ent0;
-  const int64_t n_ent0 = k0.n_ent0;
-  const int32_t *__restrict__ stage = k0.stage;
-  const int64_t n_stage = k0.n_stage;
-  const int64_t *__restrict__ soff = k0.soff;
   const int lane = lane_id();
   const bool mine = lane < size;
   int64_t i = first + (mine ? lane : 0);
-  // Three round trips before the pass: the item (error word, args, plan),
-  // the follower's scalars, log[prev].
+  // Three round trips before the pass: the item (error word, args[, staged
+  // offset]), the claims with the follower's scalars and the source's ring
+  // head, then log[prev] (and the first entry, for a sorted-terms claim).
   const int e = mine ? k0.err[i] : 1;
   mraft_ae_args a = args[i];
-  const int64_t so = soff ? soff[i] : -1;
+  const int64_t so0 = MODE == HM_DEFER ? k0.soff[i] : so_force;
   asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
-               "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so));
-  const int L = s.L;
-  // Where the entries are: Index x of this lane's message at src.at(x).
-  RingRow src{ent0, 0, 0, INT32_MAX};
-  int64_t n_ent = n_ent0;
-  bool ok = true;
-  if (e) {
-  } else if (!soff) {   // host buffer
-    src.row = a.entries_offset - (a.prev_log_index + 1);
-  } else if (so >= 0) { // staged copy
-    src.p = stage;
-    n_ent = n_stage;
-    src.row = so - (a.prev_log_index + 1);
-    a.entries_offset = so;
-  } else if (so == -2) { // in place through the source ring
-    const int64_t r = a.entries_offset / L;
-    src.p = s.log;
-    src.row = r * L;
-    src.L = L;
-    src.base = s.head[r] + (int)(a.entries_offset % L) - (a.prev_log_index + 1);
-    n_ent = INT64_MAX;
-  } else {
-    ok = false;          // malformed reference
-  }
-  int cls = e ? AE_NONE : AE_DONE;
-  if (!e && (!ok || a.n_entries < 0 || a.entries_offset < 0 ||
-             (a.n_entries > 0 && so != -2 && a.entries_offset + a.n_entries > n_ent)))
-    cls = AE_BAD;
+               "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so0));
+  // L re-read per set: the division by it (a reciprocal) is then computed here,
+  // not hoisted out of the wave's loop over sets and held across the pass
+  int L = s.L;
+  asm volatile("" : "+s"(L));
+  const int64_t gp = (int64_t)s.G * s.P;
   int f = a.slot;
   const int prev = a.prev_log_index, nn = a.n_entries;
+  // every word that depends only on the args, in one round trip (e == 0: the
+  // slot is in range; the follower's words are read before the claims decide
+  // whether the item runs here: no extra dependent round trip)
+  int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
+  if (!e) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
+  // Where the entries are: Index x of this lane's message at src.at(x).
+  RingRow src{k0.ent0, 0, 0, INT32_MAX};
+  int64_t n_ent = k0.n_ent0;
+  bool ok = true, dup = false, dfr = false, stg = false;
+  int64_t srow = 0;  // by reference: the source row
+  int rhead = 0;
+  if (MODE == HM_HOST) {
+    if (!e) src.row = a.entries_offset - (prev + 1);
+  } else if (!e) {
+    ok = ae_ref_ok(a, gp * L, L);
+    srow = ok ? a.entries_offset / L : 0;
+    unsigned long long cs = 0, cr = 0;
+    uint32_t sm = 0;
+    if (MODE == HM_MAIN) {
+      cs = k0.claim[f];
+      sm = k0.srcmark[f];
+      if (ok && nn > 0) cr = k0.claim[srow];
+    }
+    if (ok) rhead = s.head[srow];
+    if (MODE == HM_MAIN) {
+      dup = cs != claim_tag(k0.epoch, i);
+      dfr = !dup && ok && sm == k0.epoch;                              // `written`: deferred
+      stg = dfr && nn > 0 && (uint32_t)(cr >> 32) == k0.epoch;        // and `read`: staged
+    }
+    const int64_t so = MODE == HM_MAIN ? -2 : so0;
+    if (so >= 0) {  // staged copy (or the fallback's cycle buffer)
+      src.p = k0.stage;
+      n_ent = MODE == HM_DEFER ? k0.stage_cap : L;
+      src.row = so - (prev + 1);
+      a.entries_offset = so;
+    } else {        // in place through the source ring
+      src.p = s.log;
+      src.row = srow * L;
+      src.L = L;
+      src.base = rhead + (int)(a.entries_offset % L) - (prev + 1);
+      n_ent = INT64_MAX;
+    }
+  }
+  int cls = e ? AE_NONE : AE_DONE;
+  if (dup) cls = AE_NONE;
+  else if (dfr) cls = AE_DEFER;
+  else if (!e && (!ok || nn < 0 || a.entries_offset < 0 ||
+                  (nn > 0 && src.L == INT32_MAX && a.entries_offset + nn > n_ent)))
+    cls = AE_BAD;
   const bool live = cls == AE_DONE;
-  if (k0.res && mine) {
+  if (dup && mine) k0.err[i] = MRAFT_ITEM_DUP_SLOT;
+  if (MODE == HM_MAIN && __ballot(dfr))
+    defer_lanes(k0, dfr, stg, i, nn, s.log + srow * L, rhead, (int)(a.entries_offset % L), L);
+  if (k0.res && mine && cls != AE_DEFER) {
     // the args half of the item's reply record for its co-resident leader's
     // fold, stored now (no reload of the args at the wave's end); the reply
     // half follows with the reply. Failed items: slot = peer = -1.
-    const int PP = s.P;
+    int PP = s.P;
+    asm volatile("" : "+s"(PP));  // (the division's reciprocal made here, not hoisted and spilled)
     int4 *rr = reinterpret_cast<int4 *>(k0.res + i);
     rr[0] = live ? make_int4((f / PP) * PP + a.leader_id, f % PP, a.term, prev) : no_record();
   }
-  int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
-  if (live) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
   // MRAFT_AE_ENTRIES_SORTED is the sender's claim (it crosses the network):
   // honoured only where the terms prevLogTerm, entry 0, ... really never
   // decrease. Here the first step (prevLogTerm <= entry 0, in the round trip
-  // of the follower's log[prev]); the entries themselves are checked on the
-  // pass's loads (DescTrack). Same rule in the oracle (ae_flag_holds).
+  // of the follower's log[prev]; a flat source addressed in 64 bits, whatever
+  // the Index); the entries themselves are checked on the pass's loads
+  // (DescTrack). Same rule in the oracle (ae_flag_holds).
   const bool claim = live && nn > 0 && (a.flags & MRAFT_AE_ENTRIES_SORTED) != 0;
-  const bool claim0 = claim && a.prev_log_term <= *src.at(prev + 1);
+  const bool claim0 =
+      claim && a.prev_log_term <= (src.L == INT32_MAX ? src.p[src.row + prev + 1] : *src.at(prev + 1));
   mraft_ae_reply r = {0, 0, 0, 0};
   int ftp = 0;
   if (live) {
@@ -693,7 +694,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
 #else
   mraft_ae_result *__restrict__ res = k0.res;
 #endif
-  if (res && mine) {
+  if (res && mine && cls != AE_DEFER) {
     // the reply half of the record (nEntries, reply term, success,
     // ConflictIndex); an item rejected after the prologue (capacity: cls
     // AE_DONE) gets slot = peer = -1 as well
@@ -703,39 +704,153 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   }
 }
 
-// The grid may be sized by an upper bound: set_count holds the number of
-// sets on the device, and a workgroup serves sets blockIdx, blockIdx + grid,
-// ... (grid a multiple of 8: each XCD keeps its contiguous range of sets,
-// neighbouring sets share one L2).
-template <int NI>
+// The main launch: wave v serves the sets whose heads lie in items
+// [v*NI, (v+1)*NI) (one set for a gathered batch), each XCD a contiguous
+// range of waves (neighbouring sets share one L2 for the leaders' entries).
+// HM_HOST: wave v serves message v.
+template <int NI, int MODE>
 __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(HsArgs ka) {
-  const int64_t *__restrict__ sets = ka.sets;
-  const unsigned long long sc = ka.set_count ? *ka.set_count : 0ull;
-  const int64_t nb = sets ? (ka.set_count ? (int64_t)(sc & 0xFFFFFFFFull) : ka.n_sets) : ka.n;
-  if (ka.host_total && blockIdx.x == 0 && threadIdx.x == 0) {
-    // the plan's totals to the host's pinned words (staged, sets, deferred),
-    // then the sequence word with a system-scope release (the host polls it)
-    const unsigned long long staged = ka.set_count[-1];
-    ka.host_total[0] = staged;
-    ka.host_total[1] = sc & 0xFFFFFFFFull;
-    ka.host_total[2] = sc >> 32;
-    __hip_atomic_store(&ka.host_total[3], ka.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int64_t nb = MODE == HM_HOST ? ka.n : (ka.n + NI - 1) / NI;
+  int64_t v = blockIdx.x;
+  {
+    const int64_t x = v & 7, per = nb >> 3, rem = nb & 7, j = v >> 3;
+    if (j >= per + (x < rem ? 1 : 0)) return;
+    v = x * per + min(x, rem) + j;
   }
-  for (int64_t v = blockIdx.x;; v += gridDim.x) {
-    int64_t gb = v;
-    if (MRAFT_AE_XCD) {
-      const int64_t x = v & 7, per = nb >> 3, rem = nb & 7, j = v >> 3;
-      if (j >= per + (x < rem ? 1 : 0)) return;
-      gb = x * per + min(x, rem) + j;
-    } else if (v >= nb) {
-      return;
+  if (MODE == HM_HOST) {
+    handle_one<NI, HM_HOST>(ka, v, 1);
+    return;
+  }
+  const int lane = lane_id();
+  const int64_t c0 = v * NI;
+  const int hd = (lane < NI && c0 + lane < ka.n) ? (int)ka.sethd[c0 + lane] : 0;
+  for (unsigned long long m = __ballot(hd > 0); m; m &= m - 1) {
+    const int q = first_lane(m);
+    handle_one<NI, HM_MAIN>(ka, c0 + q, __builtin_amdgcn_readlane(hd, q));
+  }
+}
+
+// The source row's writer of a deferred item: the item that owns the row it
+// reads (claim winner) when that row is claimed in this call and the owner is
+// itself a deferred item (a well-formed reference; its slot is read, so it
+// was deferred); else -1.
+__device__ __forceinline__ int64_t ae_writer(const HsArgs &k, int64_t x) {
+  const mraft_ae_args a = k.args[x];
+  const int L = k.s.L;
+  const int64_t gp = (int64_t)k.s.G * k.s.P;
+  if (a.n_entries <= 0 || !ae_ref_ok(a, gp * L, L)) return -1;
+  const unsigned long long c = __hip_atomic_load(&k.claim[a.entries_offset / L], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+  if ((uint32_t)(c >> 32) != k.epoch) return -1;
+  const int64_t w = (int64_t)(0xFFFFFFFFull - (c & 0xFFFFFFFFull));
+  return ae_ref_ok(k.args[w], gp * L, L) ? w : -1;
+}
+
+__device__ __forceinline__ int at_load(int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void at_store(int32_t *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void phase_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+// The ordered fallback (the staged words exceed the stage capacity), on one
+// wave: Kahn's order over the deferred items with the edge x -> writer(x)
+// (x reads the row its writer rewrites, so x runs first); every item reads its
+// source in place, except that when no item is free the remaining ones are
+// all on cycles (each item has one writer at most), and one of them has its
+// entries copied to the cycle buffer first, which frees its writer. Shared
+// words through L2 (agent-scope atomics); wave-uniform control.
+template <int NI>
+__device__ void handle_ordered(const HsArgs &k, int64_t nd) {
+  const int lane = lane_id();
+  for (int64_t j = lane; j < nd; j += 64) at_store(&k.kin[k.defer[j]], 0);
+  phase_fence();
+  for (int64_t j = lane; j < nd; j += 64) {
+    const int64_t w = ae_writer(k, k.defer[j]);
+    if (w >= 0) (void)atomicAdd(&k.kin[w], 1);
+  }
+  phase_fence();
+  int64_t qt = 0;  // queue tail (wave-uniform)
+  for (int64_t j0 = 0; j0 < nd; j0 += 64) {
+    const int64_t j = j0 + lane;
+    const int64_t x = j < nd ? k.defer[j] : -1;
+    const bool free0 = x >= 0 && at_load(&k.kin[x]) == 0;
+    const unsigned long long m = __ballot(free0);
+    if (free0) at_store(&k.kq[qt + lanes_below(m)], (int)x);
+    qt += __popcll(m);
+  }
+  phase_fence();
+  int64_t qh = 0, brk = -1;
+  const int L = k.s.L;
+  for (int64_t done = 0; done < nd;) {
+    if (qh == qt) {
+      // every item left is on a cycle: copy one member's entries aside and
+      // free its writer
+      int64_t x = -1;
+      for (int64_t j0 = 0; j0 < nd && x < 0; j0 += 64) {
+        const int64_t j = j0 + lane;
+        const int64_t y = j < nd ? k.defer[j] : -1;
+        const unsigned long long m = __ballot(y >= 0 && at_load(&k.kin[y]) > 0);
+        if (m) {
+          const int q = first_lane(m);
+          x = ((int64_t)__builtin_amdgcn_readlane((int)(y >> 32), q) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)y, q);
+        }
+      }
+      if (x < 0) return;  // unreachable: the counts say an item is left
+      const mraft_ae_args a = k.args[x];
+      const int64_t row = a.entries_offset / L;
+      wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L), k.cyc,
+                          a.n_entries);
+      brk = x;
+      const int64_t w = ae_writer(k, x);
+      if (w < 0) return;  // unreachable: an item on a cycle has a writer
+      phase_fence();
+      int fr = 0;
+      if (lane == 0) fr = atomicSub(&k.kin[w], 1) == 1;
+      if (__builtin_amdgcn_readfirstlane(fr)) {
+        if (lane == 0) at_store(&k.kq[qt], (int)w);
+        ++qt;
+      }
+      phase_fence();
+      continue;
     }
-    if (sets) {
-      const int64_t h = sets[gb];
-      handle_one<NI>(ka, h >> 3, (int)(h & 7) + 1);
-    } else {
-      handle_one<NI>(ka, gb, 1);
+    const int64_t x = __builtin_amdgcn_readfirstlane(at_load(&k.kq[qh]));
+    ++qh;
+    HsArgs kx = k;
+    kx.stage = k.cyc;
+    kx.stage_cap = L;
+    handle_one<NI, HM_DEFER>(kx, x, 1, x == brk ? 0 : -2);
+    ++done;
+    phase_fence();
+    const int64_t w = ae_writer(k, x);
+    if (lane == 0) at_store(&k.kin[x], -1);
+    int fr = 0;
+    if (w >= 0 && lane == 0) fr = atomicSub(&k.kin[w], 1) == 1;
+    if (__builtin_amdgcn_readfirstlane(fr)) {
+      if (lane == 0) at_store(&k.kq[qt], (int)w);
+      ++qt;
     }
+    phase_fence();
+  }
+}
+
+// The deferred launch: every deferred item (a set of one), grid-stride; the
+// counts are read on the device (the host enqueues this launch blind: with no
+// deferred item, every workgroup exits at once).
+// (Each deferred item is a set of one: the one-lane form of the pass.)
+__global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_deferred(HsArgs ka) {
+  const unsigned long long staged = ka.total[0];
+  const int64_t nd = (int64_t)(ka.total[1] >> 32);
+  if (nd == 0) return;
+  if ((long long)staged <= ka.stage_cap) {
+    for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) handle_one<1, HM_DEFER>(ka, ka.defer[j], 1);
+  } else if (blockIdx.x == 0) {
+    handle_ordered<1>(ka, nd);
   }
 }
 
@@ -1876,59 +1991,53 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
                      out, err);
 }
 
-void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp,
-                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err,
+void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp, int ni,
+                     unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, uint8_t *sethd,
                      unsigned long long *total, hipStream_t st) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n, kMsgBlock)), dim3(kMsgBlock), 0, st, args, n, n_log, L, gp, claim, srcmark,
-                     epoch, err, total);
+  hipLaunchKernelGGL(k_claim_ae, dim3(blocks_for(n, 64)), dim3(64), 0, st, args, n, n_log, L, gp,
+                     ni < 1 ? 1 : ni > kAeHalo ? kAeHalo : ni, claim, srcmark, epoch, err, sethd, total);
 }
 
-void launch_ae_set_plan(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int ni,
-                        const unsigned long long *claim, const uint32_t *srcmark, uint32_t epoch,
-                        int32_t *err, int64_t *soff, int64_t *sets, int64_t *defer,
-                        unsigned long long *total, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_ae_set_plan, dim3(blocks_for(n, kAeOwn)), dim3(kAePlanT), 0, st, args, n, n_log, L,
-                     ni < 1 ? 1 : ni > kAeHalo ? kAeHalo : ni, claim, srcmark, epoch, err, soff, sets, defer, total);
-}
-
-void launch_ae_stage_copy(const int32_t *log, const int32_t *head, int L, const mraft_ae_args *args, int64_t n,
-                          const int64_t *soff, int32_t *stage, hipStream_t st) {
-  hipLaunchKernelGGL(k_ae_stage_copy, dim3(blocks_for(n, 4)), dim3(256), 0, st, log, head, L, args, n, soff,
-                     stage);
+// grid for k_handle_set: nb waves, each XCD a contiguous range (k_handle_set)
+template <int NI, int MODE>
+static void launch_set(const HsArgs &ka, int64_t nb, hipStream_t st) {
+  hipLaunchKernelGGL((k_handle_set<NI, MODE>), dim3((unsigned)nb), dim3(64), 0, st, ka);
 }
 
 template <int NI>
-static void launch_set(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
-                       const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
-                       int64_t n_sets, const unsigned long long *set_count, mraft_ae_reply *rep, int32_t *err,
-                       unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
-                       hipStream_t st) {
-  // with the count on the device, n_sets is an upper bound: a workgroup per
-  // MRAFT_AE_SPB sets of the bound (grid a multiple of 8, see k_handle_set)
-  int64_t nb = sets ? n_sets : n;
-  if (set_count) nb = ((nb + MRAFT_AE_SPB - 1) / MRAFT_AE_SPB + 7) / 8 * 8;
-  const HsArgs ka{s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, seq,
-                  res};
-  hipLaunchKernelGGL(k_handle_set<NI>, dim3((unsigned)nb), dim3(64), 0, st, ka);
+static void launch_ref(const HsArgs &ka, hipStream_t st) {
+  launch_set<NI, HM_MAIN>(ka, (ka.n + NI - 1) / NI, st);
+  // the deferred launch, enqueued blind (its counts are on the device): a
+  // fixed grid that grid-strides over the deferred items
+  const int64_t g = min(ka.n, (int64_t)2048);
+  hipLaunchKernelGGL(k_handle_deferred, dim3((unsigned)g), dim3(64), 0, st, ka);
 }
 
-void launch_handle_ae(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
-                      const int32_t *stage, int64_t n_stage, const int64_t *soff, const int64_t *sets,
-                      int64_t n_sets, const unsigned long long *set_count, int ni, mraft_ae_reply *rep,
-                      int32_t *err, unsigned long long *host_total, unsigned long long seq, mraft_ae_result *res,
-                      hipStream_t st) {
-  if (n <= 0 || (sets && n_sets <= 0)) return;
-#define MRAFT_SET_CASE(k) \
-  case k: launch_set<k>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total, \
-                        seq, res, st); break;
-  switch (sets ? ni : 1) {
-    MRAFT_SET_CASE(1) MRAFT_SET_CASE(2) MRAFT_SET_CASE(3) MRAFT_SET_CASE(4) MRAFT_SET_CASE(5) MRAFT_SET_CASE(6)
-    default: launch_set<7>(s, args, n, ent, n_ent, stage, n_stage, soff, sets, n_sets, set_count, rep, err, host_total,
-                           seq, res, st);
+void launch_handle_ae_ref(const Dev &s, const mraft_ae_args *args, int64_t n, int ni, const unsigned long long *claim,
+                          const uint32_t *srcmark, uint32_t epoch, int32_t *err, const uint8_t *sethd, int64_t *soff,
+                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap, int32_t *kin,
+                          int32_t *kq, int32_t *cyc, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st) {
+  if (n <= 0) return;
+  const HsArgs ka{s,     args,  n,     nullptr, 0,   stage, stage_cap, soff, sethd, defer, total,
+                  claim, srcmark, epoch, kin,   kq,  cyc,   rep,       err,  res};
+  switch (ni) {
+    case 1: launch_ref<1>(ka, st); break;
+    case 2: launch_ref<2>(ka, st); break;
+    case 3: launch_ref<3>(ka, st); break;
+    case 4: launch_ref<4>(ka, st); break;
+    case 5: launch_ref<5>(ka, st); break;
+    case 6: launch_ref<6>(ka, st); break;
+    default: launch_ref<7>(ka, st);
   }
-#undef MRAFT_SET_CASE
+}
+
+void launch_handle_ae_host(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
+                           mraft_ae_reply *rep, int32_t *err, mraft_ae_result *res, hipStream_t st) {
+  if (n <= 0) return;
+  const HsArgs ka{s,       args,    n, ent,     n_ent,   nullptr, 0,   nullptr, nullptr, nullptr, nullptr,
+                  nullptr, nullptr, 0, nullptr, nullptr, nullptr, rep, err,     res};
+  launch_set<1, HM_HOST>(ka, n, st);
 }
 
 #if MRAFT_FOLD_TRACE

@@ -153,6 +153,14 @@ class Engine:
     def tick_shards(self) -> int:
         return int(self._lib.mraft_get_tick_shards(self._h))
 
+    def set_stage_capacity(self, words: int):
+        """Words of staged entries mraft_handle_append_entries may use for its
+        deferred items (mraft_set_stage_capacity; 0 forces the ordered fallback)."""
+        _ck(self._lib.mraft_set_stage_capacity(self._h, words), "mraft_set_stage_capacity")
+
+    def stage_capacity(self) -> int:
+        return int(self._lib.mraft_get_stage_capacity(self._h))
+
     def shard_stream(self, shard: int) -> int:
         return self._lib.mraft_shard_stream(self._h, shard) or 0
 

@@ -92,3 +92,42 @@ def stale_second_leader_state(st, lp, G, P, L, rng, groups):
     slots = np.array([s for s, _ in pairs], np.int32)
     peers = np.array([p for _, p in pairs], np.int32)
     return st, slots, peers
+
+
+def stale_cycle_state(st, lp, G, P, L, rng, groups, k):
+    """Stale leaders sending to each other in a ring: in each of `groups`,
+    replicas r_0 = lp[g], r_1, ..., r_{k-1} (k <= P) are all Leaders, r_j one
+    term below r_{j-1} with a log that diverges from r_{j-1}'s, and the batch
+    holds r_j -> r_{j+1 mod k}. Every item then reads a row another item
+    writes and writes a row another item reads: a cycle of k deferred items
+    whose entries the engine must take as they were before the call (staged,
+    or, past the stage capacity, one of them copied to break the cycle).
+    2 <= k <= P."""
+    st = {kk: v.copy() for kk, v in st.items()}
+    pairs = []
+    for g in groups:
+        l = int(lp[g])
+        rs = [(l + j) % P for j in range(k)]
+        slots = [g * P + r for r in rs]
+        T = int(st["current_term"][slots[0]])
+        prev_row = st["log_term"][slots[0] * L:(slots[0] + 1) * L]
+        prev_last = int(st["last_index"][slots[0]])
+        for j in range(1, k):
+            s = slots[j]
+            st["state"][s] = LEADER
+            st["current_term"][s] = max(1, T - j)
+            st["dummy_index"][s] = 0
+            last = min(L - 1, max(4, prev_last))
+            row = st["log_term"][s * L:(s + 1) * L]
+            d = int(rng.integers(1, max(2, min(last, prev_last) - 1)))
+            row[:d + 1] = prev_row[:d + 1]
+            row[d + 1:last + 1] = max(1, T - j)
+            st["last_index"][s] = last
+            st["commit_index"][s] = min(int(st["commit_index"][s]), d)
+            st["last_applied"][s] = min(int(st["last_applied"][s]), int(st["commit_index"][s]))
+            prev_row, prev_last = row, last
+        for j in range(k):
+            a, b = slots[j], slots[(j + 1) % k]
+            st["next_index"][a * P + (b % P)] = int(rng.integers(1, int(st["last_index"][a]) + 2))
+            pairs.append((a, b % P))
+    return st, np.array([a for a, _ in pairs], np.int32), np.array([b for _, b in pairs], np.int32)

@@ -1,0 +1,131 @@
+"""The message-level AppendEntries handler with no host round trip (VERDICT r4
+item 1): mraft_handle_append_entries[_ex] by reference enqueues its three
+launches and returns, whatever the batch; items that must run after others
+are ordered on the device (include/mraft.h, mraft_kernels.hip "a4").
+
+* K message steps (gather -> HandleAppendEntries -> reply fold,
+  src/raft/raft_append_entry.go:20-162) enqueued back to back on one engine
+  behind a device spin, with no host synchronisation: the calls return while
+  the stream is still busy, and every step's outputs equal K oracle steps.
+* Batches whose items read rows other items write, in rings of 2 and 3 stale
+  leaders and with crafted self-references (cycles of deferred items), with
+  the default stage, a stage too small for the batch and no stage at all (the
+  ordered fallback): GPU == oracle (which copies every item's entries at the
+  start of the call, as the reference's gather does, raft_append_entry.go:50-54)."""
+import numpy as np
+import pytest
+
+from message_cases import all_follower_items, results_of, stale_cycle_state, stale_second_leader_state
+from oracle_lib import Oracle, assert_states_equal
+
+from multiraft_amd import DEVICE, Engine, _abi, synth_seed, synth_tick_state
+from multiraft_amd._abi import AE_ARGS, AE_REPLY, AE_RESULT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_back_to_back_steps_without_host_sync_gpu():
+    import torch
+    G, P, L, K = 512, 5, 256, 4
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + 9)
+    slots, peers = all_follower_items(lp, G, P)
+    n = len(slots)
+    dev = torch.device("cuda", 0)
+    lib = _abi.lib()
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+    args = [z(n, 10) for _ in range(K)]
+    gerr, herr, ferr, flags = ([z(n) for _ in range(K)] for _ in range(4))
+    rep, res = [z(n, 4) for _ in range(K)], [z(n, 8) for _ in range(K)]
+    sl_d, pe_d = torch.from_numpy(slots).to(dev), torch.from_numpy(peers).to(dev)
+    seg = np.concatenate([[0], np.cumsum(np.bincount(slots // P, minlength=G)[lp >= 0])]).astype(np.int64)
+    seg_d = torch.from_numpy(seg).to(dev)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        stream = torch.cuda.ExternalStream(e.stream(), device=dev)
+        e.synchronize()
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(2e8))  # ~0.1 s of device spin ahead of the calls
+        for k in range(K):
+            assert lib.mraft_gather_append_args(e._h, sl_d.data_ptr(), pe_d.data_ptr(), n, args[k].data_ptr(),
+                                                gerr[k].data_ptr(), DEVICE) == 0, _abi.last_error()
+            assert lib.mraft_handle_append_entries_ex(e._h, args[k].data_ptr(), n, None, 0, rep[k].data_ptr(),
+                                                      res[k].data_ptr(), herr[k].data_ptr(), DEVICE) == 0, \
+                _abi.last_error()
+            assert lib.mraft_process_append_replies(e._h, res[k].data_ptr(), n, seg_d.data_ptr(), len(seg) - 1,
+                                                    flags[k].data_ptr(), ferr[k].data_ptr(), DEVICE) == 0, \
+                _abi.last_error()
+        # every call returned with the device still behind the spin: nothing waited on it
+        assert not stream.query(), "a message call waited on the device"
+        e.synchronize()
+        got = e.store_state()
+    o = Oracle(G, P, L, st)
+    for k in range(K):
+        oargs, ogerr = o.gather_append_args(slots, peers)
+        assert np.array_equal(args[k].cpu().numpy().view(AE_ARGS).reshape(-1), oargs), k
+        assert np.array_equal(gerr[k].cpu().numpy(), ogerr), k
+        orep, oherr = o.handle_append_entries(oargs, None)
+        assert np.array_equal(rep[k].cpu().numpy().view(AE_REPLY).reshape(-1), orep), k
+        assert np.array_equal(herr[k].cpu().numpy(), oherr), k
+        ores, oseg = results_of(slots, peers, oargs, orep, oherr, G, P)
+        assert np.array_equal(res[k].cpu().numpy().view(AE_RESULT).reshape(-1), ores), k
+        of, oferr = o.process_append_replies(ores, oseg)
+        assert np.array_equal(flags[k].cpu().numpy(), of) and np.array_equal(ferr[k].cpu().numpy(), oferr), k
+    assert_states_equal(got, o.state(), G, P, L, f"{K} steps, no host sync")
+
+
+def _self_reference(st, lp, G, P, L, rng):
+    """A gathered batch in which some leaders' first message is addressed to
+    the leader's own slot: the item reads the row it writes."""
+    slots, peers = all_follower_items(lp, G, P)
+    return slots, peers, rng.choice(G // 4, size=G // 8, replace=False)
+
+
+CASES = ["stale_leader", "ring2", "ring3", "self"]
+
+
+@pytest.mark.parametrize("cap", ["default", "small", "zero"])
+@pytest.mark.parametrize("case", CASES)
+def test_deferred_items_gpu(case, cap):
+    G, P, L = 256, 5, 128
+    rng = np.random.default_rng(11 * CASES.index(case) + len(cap))
+    st, lp, _ = synth_tick_state(G, P, L, seed=77 + CASES.index(case))
+    self_groups = None
+    if case == "stale_leader":
+        st, slots, peers = stale_second_leader_state(st, lp, G, P, L, rng, range(0, G, 2))
+    elif case.startswith("ring"):
+        st, slots, peers = stale_cycle_state(st, lp, G, P, L, rng, range(0, G, 3), int(case[-1]))
+    else:
+        slots, peers, self_groups = _self_reference(st, lp, G, P, L, rng)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        if cap == "small":
+            e.set_stage_capacity(64)
+        elif cap == "zero":
+            e.set_stage_capacity(0)
+        assert e.stage_capacity() == {"default": 1 << 22, "small": 64, "zero": 0}[cap]
+        args, gerr = e.gather_append_args(slots, peers)
+        oargs, ogerr = o.gather_append_args(slots, peers)
+        assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr)
+        batch = args[gerr == 0].copy()
+        if self_groups is not None:
+            first = {}
+            for j, a in enumerate(batch):
+                g = int(a["slot"]) // P
+                if g in set(self_groups.tolist()) and g not in first:
+                    first[g] = j
+            for g, j in first.items():
+                batch[j]["slot"] = int(batch[j]["entries_offset"]) // L   # the leader's own slot
+        rep, herr, gres = e.handle_append_entries(batch, None, results=True)
+        orep, oherr = o.handle_append_entries(batch, None)
+        assert np.array_equal(herr, oherr), case
+        assert np.array_equal(rep, orep), case
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"{case}, stage {cap}")
+        # a second call on the same engine after the fallback: the counters re-arm
+        args2, gerr2 = e.gather_append_args(slots, peers)
+        oargs2, ogerr2 = o.gather_append_args(slots, peers)
+        assert np.array_equal(args2, oargs2)
+        rep2, herr2 = e.handle_append_entries(args2[gerr2 == 0], None)
+        orep2, oherr2 = o.handle_append_entries(oargs2[ogerr2 == 0], None)
+        assert np.array_equal(herr2, oherr2) and np.array_equal(rep2, orep2)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"{case}, stage {cap}, second call")
