@@ -95,14 +95,14 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
     slices, no copies), its own engine on a hardware queue of its own
     (MRAFT_CREATE_DEDICATED_QUEUE) driven by its own host thread — the Go
     host's goroutine per shard: ctypes releases the GIL in
-    the engine calls, so one shard's host-side waits (the handle call waits
-    for its plan) do not hold the other back. Step i runs on copy i restored
+    the engine calls, so one shard's host-side work does not hold the other
+    back (no call waits on the device: round 5). Step i runs on copy i restored
     from `master`; the warm-up on copy `steps`.
     S = 1: one event between consecutive calls (the per-call split);
     S > 1: one event per step on each queue (the device span per step);
     shard s > 0 starts `offset_ms` * s / (S - 1) after shard 0 (a device
     spin on its queue), so the shards' short latency-bound calls (gather,
-    claim, plan, fold) can run beside another shard's streaming handler
+    claims, fold) can run beside another shard's streaming handler
     instead of in lock-step with it.
     words=True: the algorithmic words of one batch (tools/msg_words.py) from
     the warm-up's inputs (S = 1 only)."""
@@ -295,7 +295,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
         "vs_headline_what": "the message path's device time per step with the better of two and three shard "
                             "pipelines, over the headline's ms_per_step on the same box (the calls one after "
                             "another on one queue: calls_ms_sum_vs_headline)",
-        "roofline": {"kernel": "mraft_handle_append_entries (whole call: plan + k_handle_set)", "bound": "hbm",
+        "roofline": {"kernel": "mraft_handle_append_entries (whole call: claims + set heads, main and deferred launches)", "bound": "hbm",
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
                      "sets": hw["sets"], "merges": hw["merges"]},

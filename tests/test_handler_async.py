@@ -66,11 +66,65 @@ def test_back_to_back_steps_without_host_sync_gpu():
         orep, oherr = o.handle_append_entries(oargs, None)
         assert np.array_equal(rep[k].cpu().numpy().view(AE_REPLY).reshape(-1), orep), k
         assert np.array_equal(herr[k].cpu().numpy(), oherr), k
-        ores, oseg = results_of(slots, peers, oargs, orep, oherr, G, P)
-        assert np.array_equal(res[k].cpu().numpy().view(AE_RESULT).reshape(-1), ores), k
-        of, oferr = o.process_append_replies(ores, oseg)
+        # the handler's reply records: the host-assembled records of the items it handled,
+        # slot = peer = -1 for the others (a gather that failed forwards
+        # zeroed args; with no host in between the batch carries them on)
+        gres = res[k].cpu().numpy().view(AE_RESULT).reshape(-1)
+        okh = oherr == 0
+        hand = gres[okh][np.argsort(gres["slot"][okh], kind="stable")]
+        assert np.array_equal(hand, results_of(slots, peers, oargs, orep, oherr, G, P)[0]), k
+        assert (gres["slot"][~okh] == -1).all(), k
+        # the fold over exactly what the device folded
+        of, oferr = o.process_append_replies(gres, seg)
         assert np.array_equal(flags[k].cpu().numpy(), of) and np.array_equal(ferr[k].cpu().numpy(), oferr), k
     assert_states_equal(got, o.state(), G, P, L, f"{K} steps, no host sync")
+
+
+def test_back_to_back_copies_without_host_sync_gpu():
+    """The bench's pattern: K steps, each on its own pristine state copy
+    (mraft_bind_state), enqueued back to back with no synchronisation: every
+    call's scratch is reused by the next while the device is still behind;
+    every copy must end as one oracle step on the original state."""
+    import torch
+    G, P, L, K = 1024, 5, 512, 5
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + 10)
+    slots, peers = all_follower_items(lp, G, P)
+    n = len(slots)
+    dev = torch.device("cuda", 0)
+    lib = _abi.lib()
+    copies = [{k: torch.from_numpy(v.copy()).to(dev) for k, v in st.items()} for _ in range(K)]
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+    args, gerr, herr, ferr, flags, rep, res = z(n, 10), z(n), z(n), z(n), z(n), z(n, 4), z(n, 8)
+    fl_all = z(K, n)
+    sl_d, pe_d = torch.from_numpy(slots).to(dev), torch.from_numpy(peers).to(dev)
+    seg = np.concatenate([[0], np.cumsum(np.bincount(slots // P, minlength=G)[lp >= 0])]).astype(np.int64)
+    seg_d = torch.from_numpy(seg).to(dev)
+    torch.cuda.synchronize()
+    with Engine(G, P, L, alloc=False) as e:
+        e.bind(copies[0])
+        stream = torch.cuda.ExternalStream(e.stream(), device=dev)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(2e8))
+        for k in range(K):
+            e.bind(copies[k])
+            assert lib.mraft_gather_append_args(e._h, sl_d.data_ptr(), pe_d.data_ptr(), n, args.data_ptr(),
+                                                gerr.data_ptr(), DEVICE) == 0
+            assert lib.mraft_handle_append_entries_ex(e._h, args.data_ptr(), n, None, 0, rep.data_ptr(),
+                                                      res.data_ptr(), herr.data_ptr(), DEVICE) == 0
+            assert lib.mraft_process_append_replies(e._h, res.data_ptr(), n, seg_d.data_ptr(), len(seg) - 1,
+                                                    fl_all[k].data_ptr(), ferr.data_ptr(), DEVICE) == 0
+        assert not stream.query(), "a message call waited on the device"
+        e.synchronize()
+    o = Oracle(G, P, L, st)
+    oargs, ogerr = o.gather_append_args(slots, peers)
+    assert (ogerr == 0).all()
+    orep, oherr = o.handle_append_entries(oargs, None)
+    ores, oseg = results_of(slots, peers, oargs, orep, oherr, G, P)
+    of, _ = o.process_append_replies(ores, oseg)
+    want = o.state()
+    for k in range(K):
+        assert np.array_equal(fl_all[k].cpu().numpy(), of), k
+        assert_states_equal({kk: v.cpu().numpy() for kk, v in copies[k].items()}, want, G, P, L, f"copy {k}")
 
 
 def _self_reference(st, lp, G, P, L, rng):
