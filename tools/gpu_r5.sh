@@ -103,8 +103,8 @@ for st in ${DO:-tests bench}; do
         REPS=3 timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/cmp$i" -o c -- python3 tools/cmp_tick_handler.py \
           > "$OUT/cmp$i.json" 2> "$OUT/cmp$i.err" || { tail -5 "$OUT/cmp$i.err"; exit 1; }
       done
-      python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>,k_handle_set<4>,k_ae_set_plan,k_gather_args,k_claim_ae" > /dev/null
-      python3 -c "import json; d=json.load(open('$OUT/cmp_counters.json')); [print(k, {c: round(v, 1) for c, v in sorted(x.items())}) for k, x in d.items()]" ;;
+      python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>,k_handle_set<4, 0>,k_handle_deferred,k_gather_args,k_claim_ae" > /dev/null
+      python3 tools/cmp_summary.py "$OUT" "$OUT/cmp_summary.json" | head -60 ;;
     ctest)
       echo "== ctest"
       make -s -C tests/c_host && timeout -k 10 120 tests/c_host/mraft_host_tick tests/golden/tick_vectors.bin 0 | tee "$OUT/c_host.txt" ;;
