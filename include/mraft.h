@@ -404,7 +404,14 @@ int64_t mraft_get_stage_capacity(const mraft_engine *h);
  * (raft_append_entry.go:66-105). Items are folded per segment in array order;
  * segment s = items [seg_begin[s], seg_begin[s+1]) all with the same leader
  * slot (distinct across segments). seg_begin == NULL means one item per
- * segment. out_flags[i] gets MRAFT_F_* bits for item i. */
+ * segment. out_flags[i] gets MRAFT_F_* bits for item i. A segment is rejected,
+ * every item_err of it set, in this order: its first record's slot out of
+ * range (MRAFT_ITEM_BAD_SLOT); an earlier non-empty segment names the same
+ * slot (MRAFT_ITEM_DUP_SLOT, whatever that segment's own outcome); a record
+ * of another slot or a bad peer (MRAFT_ITEM_BAD_SLOT); commitIndex below
+ * dummyIndex (MRAFT_ITEM_BAD_STATE). The same rule holds for
+ * mraft_process_install_snapshot_replies and mraft_process_vote_replies
+ * (without the last). */
 int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items,
                                  int64_t n, const int64_t *seg_begin,
                                  int64_t n_seg, int32_t *out_flags,

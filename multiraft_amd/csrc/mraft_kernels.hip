@@ -1057,7 +1057,9 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     const int64_t i = base + lane;
     int sl = it.slot, pr = it.peer;
     if (base > 0 && i < cnt) { sl = items[b + i].slot; pr = items[b + i].peer; }
-    if (__ballot(i < cnt && (sl != slot || pr < 0 || pr >= P || pr == me))) bad = MRAFT_ITEM_BAD_SLOT;
+    // (a segment that does not own its slot stays MRAFT_ITEM_DUP_SLOT: the
+    // claim decides first, include/mraft.h)
+    if (__ballot(i < cnt && (sl != slot || pr < 0 || pr >= P || pr == me)) && !bad) bad = MRAFT_ITEM_BAD_SLOT;
   }
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {
@@ -1312,7 +1314,9 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   int term = gw_bcast<GW>(vb, 0), role = gw_bcast<GW>(vb, 1), commit = gw_bcast<GW>(vb, 2);
   const int last = gw_bcast<GW>(vb, 3), dummy = gw_bcast<GW>(vb, 4), head = gw_bcast<GW>(vb, 5);
   const int srt = gw_bcast<GW>(vb, 6);
-  if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)))
+  // (a segment that does not own its slot stays MRAFT_ITEM_DUP_SLOT: the
+  // claim decides first, include/mraft.h)
+  if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)) && !bad)
     bad = MRAFT_ITEM_BAD_SLOT;
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {

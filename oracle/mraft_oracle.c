@@ -169,6 +169,26 @@ static int32_t *claim_slots(ora_engine *e, const int32_t *slot_of, int64_t n,
   return first;
 }
 
+/* The owner of every replica slot among a batch of reply segments: the lowest
+ * non-empty segment whose first record names that slot (in range). Segments
+ * are meant to name distinct slots (one per leader / candidate replica); a
+ * later segment naming an owned slot is rejected with MRAFT_ITEM_DUP_SLOT
+ * whatever the owner's own outcome (the engine claims slots before it checks
+ * records). `slot_of` = the slot field of record 0, records `stride` bytes. */
+static int64_t *segment_owners(ora_engine *e, const void *slot_of, size_t stride, int64_t n,
+                               const int64_t *seg_begin, int64_t ns) {
+  int64_t gp = (int64_t)e->G * e->P;
+  int64_t *owner = (int64_t *)malloc(sizeof(int64_t) * (size_t)(gp ? gp : 1));
+  for (int64_t i = 0; i < gp; ++i) owner[i] = -1;
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t b = seg_begin ? seg_begin[s] : s, en = seg_begin ? seg_begin[s + 1] : s + 1;
+    if (b >= en || b < 0 || b >= n) continue;
+    int32_t slot = *(const int32_t *)((const char *)slot_of + b * stride);
+    if (slot >= 0 && slot < gp && owner[slot] < 0) owner[slot] = s;
+  }
+  return owner;
+}
+
 /* ------------------------------------------------------------------------ */
 /* a3: appendOneRound args gather, raft_append_entry.go:20-54                 */
 /* ------------------------------------------------------------------------ */
@@ -482,7 +502,7 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
   const int32_t P = e->P;
   int64_t gp = (int64_t)e->G * P;
   int64_t ns = seg_begin ? n_seg : n;
-  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  int64_t *owner = segment_owners(e, &items[0].slot, sizeof(mraft_ae_result), n, seg_begin, ns);
   for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
   for (int64_t s = 0; s < ns; ++s) {
     int64_t b = seg_begin ? seg_begin[s] : s, en = seg_begin ? seg_begin[s + 1] : s + 1;
@@ -490,7 +510,7 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
     int32_t slot = items[b].slot;
     int32_t bad = 0;
     if (slot < 0 || slot >= gp) bad = MRAFT_ITEM_BAD_SLOT;
-    else if (seen[slot]) bad = MRAFT_ITEM_DUP_SLOT;
+    else if (owner[slot] != s) bad = MRAFT_ITEM_DUP_SLOT;
     else {
       for (int64_t i = b; i < en; ++i)
         if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
@@ -501,7 +521,6 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
       for (int64_t i = b; i < en; ++i) item_err[i] = bad;
       continue;
     }
-    seen[slot] = 1;
     for (int64_t i = b; i < en; ++i) {
       const mraft_ae_result *it = &items[i];
       out_flags[i] = process_reply_one(e, slot, it->peer, it->args_term,
@@ -510,7 +529,7 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
                                        it->reply_conflict_index, NULL);
     }
   }
-  free(seen);
+  free(owner);
   return MRAFT_OK;
 }
 
@@ -665,25 +684,24 @@ int ora_process_install_snapshot_replies(ora_engine *e, const mraft_is_result *i
   const int32_t P = e->P;
   int64_t gp = (int64_t)e->G * P;
   int64_t ns = seg_begin ? n_seg : n;
-  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  int64_t *owner = segment_owners(e, &items[0].slot, sizeof(mraft_is_result), n, seg_begin, ns);
   for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
   for (int64_t sg = 0; sg < ns; ++sg) {
     int64_t b = seg_begin ? seg_begin[sg] : sg, en = seg_begin ? seg_begin[sg + 1] : sg + 1;
     if (b >= en) continue;
     int32_t slot = items[b].slot, bad = 0;
     if (slot < 0 || slot >= gp) bad = MRAFT_ITEM_BAD_SLOT;
-    else if (seen[slot]) bad = MRAFT_ITEM_DUP_SLOT;
+    else if (owner[slot] != sg) bad = MRAFT_ITEM_DUP_SLOT;
     else
       for (int64_t i = b; i < en; ++i)
         if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
             items[i].peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
     if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
-    seen[slot] = 1;
     for (int64_t i = b; i < en; ++i)
       out_flags[i] = process_is_reply_one(e, slot, items[i].peer, items[i].args_term,
                                           items[i].args_last_included_index, items[i].reply_term);
   }
-  free(seen);
+  free(owner);
   return MRAFT_OK;
 }
 
@@ -993,7 +1011,7 @@ int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
   const int32_t P = e->P;
   int64_t gp = (int64_t)e->G * P;
   int64_t ns = seg_begin ? n_seg : n;
-  int32_t *seen = (int32_t *)calloc((size_t)(gp ? gp : 1), sizeof(int32_t));
+  int64_t *owner = segment_owners(e, &items[0].slot, sizeof(mraft_rv_result), n, seg_begin, ns);
   for (int64_t i = 0; i < n; ++i) { out_flags[i] = 0; item_err[i] = 0; }
   for (int64_t s = 0; s < ns; ++s) {
     int64_t b = seg_begin ? seg_begin[s] : s, en = seg_begin ? seg_begin[s + 1] : s + 1;
@@ -1001,18 +1019,17 @@ int ora_process_vote_replies(ora_engine *e, const mraft_rv_result *items,
     int32_t c = items[b].slot;
     int32_t bad = 0;
     if (c < 0 || c >= gp) bad = MRAFT_ITEM_BAD_SLOT;
-    else if (seen[c]) bad = MRAFT_ITEM_DUP_SLOT;
+    else if (owner[c] != s) bad = MRAFT_ITEM_DUP_SLOT;
     else {
       for (int64_t i = b; i < en; ++i)
         if (items[i].slot != c || items[i].peer < 0 || items[i].peer >= P ||
             items[i].peer == c % P) bad = MRAFT_ITEM_BAD_SLOT;
     }
     if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
-    seen[c] = 1;
     for (int64_t i = b; i < en; ++i)
       out_flags[i] = tally_one(e, c, items[i].args_term, items[i].reply_term, items[i].vote_granted);
   }
-  free(seen);
+  free(owner);
   return MRAFT_OK;
 }
 

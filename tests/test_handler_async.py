@@ -187,3 +187,58 @@ def test_deferred_items_gpu(case, cap):
         orep2, oherr2 = o.handle_append_entries(oargs2[ogerr2 == 0], None)
         assert np.array_equal(herr2, oherr2) and np.array_equal(rep2, orep2)
         assert_states_equal(e.store_state(), o.state(), G, P, L, f"{case}, stage {cap}, second call")
+
+
+@pytest.mark.parametrize("fold", ["append", "vote", "install"])
+def test_segment_owner_rule_gpu(fold):
+    """Reply segments that name the same replica slot (the chain above makes
+    them: a failed gather forwards zeroed args): the lowest non-empty segment
+    naming a slot owns it even when its own records are bad, and a later one
+    is MRAFT_ITEM_DUP_SLOT (include/mraft.h) — GPU == oracle for each fold."""
+    from multiraft_amd._abi import IS_RESULT, RV_RESULT
+    G, P, L = 64, 5, 64
+    st, lp, _ = synth_tick_state(G, P, L, seed=5150)
+    rng = np.random.default_rng(3)
+    dt = {"append": AE_RESULT, "vote": RV_RESULT, "install": IS_RESULT}[fold]
+    recs, seg = [], [0]
+    for g in range(G):
+        slot = g * P + int(max(lp[g], 0))
+        for k in range(int(rng.integers(1, 4))):
+            r = np.zeros(1, dtype=dt)[0]
+            r["slot"], r["peer"] = slot, (slot % P + 1 + k) % P
+            r["args_term"] = int(st["current_term"][slot])
+            if fold == "append":
+                r["args_prev_log_index"] = int(st["next_index"][slot * P + r["peer"]]) - 1
+                r["reply_term"], r["reply_success"], r["args_n_entries"] = r["args_term"], 1, 1
+            elif fold == "vote":
+                r["reply_term"], r["vote_granted"] = r["args_term"], 1
+            else:
+                r["args_last_included_index"], r["reply_term"] = int(st["dummy_index"][slot]), r["args_term"]
+            recs.append(r)
+        seg.append(len(recs))
+    recs = np.array(recs, dtype=dt)
+    seg = np.array(seg, np.int64)
+    # corrupt: segment 3's second-to-first record names another slot (BAD_SLOT),
+    # segment 9 repeats segment 3's slot (DUP: 3 owns it), segment 12 repeats
+    # segment 5's slot (DUP), segment 20 is empty, segment 21 names an
+    # out-of-range slot
+    b3, b9, b12, b5 = seg[3], seg[9], seg[12], seg[5]
+    if seg[4] - b3 > 1:
+        recs["slot"][b3 + 1] = recs["slot"][b3] + 1
+    recs["slot"][b9:seg[10]] = recs["slot"][b3]
+    recs["slot"][b12:seg[13]] = recs["slot"][b5]
+    recs["slot"][seg[21]:seg[22]] = G * P + 7
+    seg = np.concatenate([seg[:21], [seg[20]], seg[21:]])   # an empty segment before 21
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        if fold == "append":
+            got, want = e.process_append_replies(recs, seg), o.process_append_replies(recs, seg)
+        elif fold == "vote":
+            got, want = e.process_vote_replies(recs, seg), o.process_vote_replies(recs, seg)
+        else:
+            got, want = e.process_install_snapshot_replies(recs, seg), o.process_install_snapshot_replies(recs, seg)
+        assert np.array_equal(got[1], want[1]), fold
+        assert np.array_equal(got[0], want[0]), fold
+        assert (want[1] == _abi.ITEM_DUP_SLOT).sum() > 0 and (want[1] == _abi.ITEM_BAD_SLOT).sum() > 0
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"{fold} owner rule")

@@ -2,8 +2,8 @@
 (k_handle_set), from the state before the call and the
 replies: what the handler must read and write, whatever kernel runs it.
 
-Per message: its args record (10 words) and plan word pair (soff, 2) read,
-its reply (4) written; the receiving follower's term, dummy, last, commit and
+Per message: its args record (10 words) and its set-head byte (1/4 word,
+round 5; rounds 2-4 read a plan word pair, 2) read, its reply (4) written; the receiving follower's term, dummy, last, commit and
 ring head (5) read; log[prev] (1) when prev lies inside the follower's log;
 the ConflictIndex scan's words; for a merge, the follower's terms compared up
 to the first mismatch and the entries written from there; the state words a
@@ -11,8 +11,9 @@ follower's reply changes (role; term and votedFor on adoption; last on
 truncation; terms_sorted when an append changes it (include/mraft.h); commit
 when it moves; the persist-flag read-modify-write).
 Per set (messages reading the same entries): the shared entries once, from
-the lowest compared Index to the highest one any message of the set needs,
-plus the set record (2). raft_append_entry.go:108-162, raft_log.go:92-96."""
+the lowest compared Index to the highest one any message of the set needs
+(round 5: no set record; rounds 2-4 read one, 2 words).
+raft_append_entry.go:108-162, raft_log.go:92-96."""
 import numpy as np
 
 
@@ -34,7 +35,7 @@ def handle_words(st, args, rep, herr, G, P, L, chunk=2048):
     stale = ok & (args["term"] < ft)
     below = ok & ~stale & (prev < fd)
     inside = ok & ~stale & ~below & (prev <= fl)
-    words = len(args) * (10 + 2 + 4) + int(ok.sum()) * 5 + int(inside.sum())
+    words = len(args) * (10 + 4) + len(args) / 4 + int(ok.sum()) * 5 + int(inside.sum())
     miss = ok & ~stale & ~below & (rep["success"] == 0)
     merge = ok & ~stale & ~below & (rep["success"] == 1)
     # ConflictIndex scan (:136-142): Indexes prev-1 down to the first other term
@@ -74,7 +75,6 @@ def handle_words(st, args, rep, herr, G, P, L, chunk=2048):
         hi_set = np.maximum.reduceat(hi_s, cut)
         words += int(np.maximum(0, hi_set - lo_set + 1).sum())
     n_sets = len(np.unique(src[ok] * (1 << 20) + (prev[ok] + n[ok]))) if ok.any() else 0
-    words += 2 * n_sets
     # state written by the replies (:111-161)
     wr = ok & ~stale
     adopt = wr & (args["term"] > ft)
