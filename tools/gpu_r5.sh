@@ -88,6 +88,18 @@ for st in ${DO:-tests bench}; do
           > "$OUT/elect$i.json" 2> "$OUT/elect$i.err" || { tail -5 "$OUT/elect$i.err"; exit 1; }
       done
       python3 tools/pmc_kernels.py "$OUT/elect_counters.json" "$OUT"/elect1 "$OUT"/elect2 --kernels "k_election_rounds<7>" | head -40 ;;
+    abelect)
+      # election storm A/B of library variants (tools/variants/libmraft_hip_<tag>.so, ABELECT_LIBS tags)
+      echo "== abelect ${ABELECT_LIBS:-}"
+      for pass in 1 2 3; do
+        for t in ${ABELECT_LIBS:-} in-tree; do
+          if [ "$t" = in-tree ]; then unset MRAFT_LIB; else export MRAFT_LIB=$PWD/tools/variants/libmraft_hip_$t.so; fi
+          timeout -k 10 200 python3 bench_election.py --no-cpu-baseline > "$OUT/abelect_${t}_$pass.json" 2> "$OUT/abelect_${t}_$pass.err" \
+            || { tail -3 "$OUT/abelect_${t}_$pass.err"; exit 1; }
+          python3 -c "import json; d=json.loads(open('$OUT/abelect_${t}_$pass.json').read().strip().splitlines()[-1]); print('$t', $pass, round(d['kernel_ms_mean'], 4))"
+        done
+      done
+      unset MRAFT_LIB ;;
     cmp)
       # the tick and the handler on the same state copy, counters per kernel
       echo "== cmp"
