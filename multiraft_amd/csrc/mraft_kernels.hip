@@ -289,7 +289,8 @@ enum : int { AE_DEFER = -1, AE_NONE = 0, AE_DONE, AE_BAD, AE_STALE, AE_BELOW, AE
 enum : int {
   HM_MAIN = 0,   // by reference, the main launch: classify, defer `written` items
   HM_DEFER = 1,  // by reference, a deferred item: entries staged (soff >= 0) or in place (-2)
-  HM_HOST = 2    // entries in a host-supplied buffer: one message per wave, nothing deferred
+  HM_HOST = 2,   // entries in a host-supplied buffer: one message per wave, nothing deferred
+  HM_ORDER = 3   // by reference, the ordered fallback: entries in place (-2) or the cycle buffer (0)
 };
 
 #ifndef MRAFT_AE_MINW
@@ -424,7 +425,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   // head, then log[prev] (and the first entry, for a sorted-terms claim).
   const int e = mine ? k0.err[i] : 1;
   mraft_ae_args a = args[i];
-  const int64_t so0 = MODE == HM_DEFER ? k0.soff[i] : so_force;
+  const int64_t so0 = MODE == HM_DEFER ? k0.soff[i] : so_force;  // HM_ORDER: the caller's choice
   asm volatile("" ::"v"(a.slot), "v"(a.term), "v"(a.prev_log_index), "v"(a.prev_log_term),
                "v"(a.n_entries), "v"(a.leader_commit), "v"(a.entries_offset), "v"(so0));
   // L re-read per set: the division by it (a reciprocal) is then computed here,
@@ -466,7 +467,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     const int64_t so = MODE == HM_MAIN ? -2 : so0;
     if (so >= 0) {  // staged copy (or the fallback's cycle buffer)
       src.p = k0.stage;
-      n_ent = MODE == HM_DEFER ? k0.stage_cap : L;
+      n_ent = k0.stage_cap;  // (HM_ORDER: the cycle buffer, capacity L)
       src.row = so - (prev + 1);
       a.entries_offset = so;
     } else {        // in place through the source ring
@@ -824,7 +825,7 @@ __device__ void handle_ordered(const HsArgs &k, int64_t nd) {
     HsArgs kx = k;
     kx.stage = k.cyc;
     kx.stage_cap = L;
-    handle_one<NI, HM_DEFER>(kx, x, 1, x == brk ? 0 : -2);
+    handle_one<NI, HM_ORDER>(kx, x, 1, x == brk ? 0 : -2);
     ++done;
     phase_fence();
     const int64_t w = ae_writer(k, x);
