@@ -299,6 +299,9 @@ enum : int {
 #ifndef MRAFT_AE_STASH
 #define MRAFT_AE_STASH 1  // park the per-lane reply inputs in LDS across the pass
 #endif
+#ifndef MRAFT_AE_DESC
+#define MRAFT_AE_DESC 1  // check a sorted-terms claim on the pass's loads (0: diagnostic only, wrong proofs)
+#endif
 #ifndef MRAFT_AE_PIPE
 #define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
 #endif
@@ -594,11 +597,20 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
         vec = vec && ((((uintptr_t)ss.at(sp + 1) ^ (uintptr_t)fo.at(q, sp + 1)) & 15) == 0);
       }
     }
-    if (ss.L == INT32_MAX)  // a flat buffer: every dwordx4 read must stay inside it
+    if (ss.L == INT32_MAX) {  // a flat buffer: every dwordx4 read must stay inside it
+      // its size as the first merging message sees it: n_ent is per lane (a
+      // lane with no item keeps the host-buffer size, 0 by reference), and a
+      // per-lane `vec` would split the wave between the two passes
+      const uint64_t nb = (uint64_t)n_ent;
+      const uint32_t nlo = (uint32_t)__shfl((int)(uint32_t)nb, q0, 64), nhi = (uint32_t)__shfl((int)(nb >> 32), q0, 64);
+      const int64_t sn = (int64_t)(((uint64_t)uni((int)nhi) << 32) | (uint32_t)uni((int)nlo));
       vec = vec && (((uintptr_t)ss.at(plo)) & ~(uintptr_t)15) >= (uintptr_t)ss.p &&
-            (((uintptr_t)ss.at(phi)) | 15) < (uintptr_t)(ss.p + n_ent);
+            (((uintptr_t)ss.at(phi)) | 15) < (uintptr_t)(ss.p + sn);
+    }
+    // the pass is wave-wide (ballots, shuffles): one choice for every lane
+    vec = __ballot(!vec) == 0;
     int found = -1;
-    DescTrack dt{__ballot(cls == AE_MERGE && claim0) != 0, 0, INT32_MIN};
+    DescTrack dt{MRAFT_AE_DESC && __ballot(cls == AE_MERGE && claim0) != 0, 0, INT32_MIN};
 #if MRAFT_AE_STASH
     // This lane's reply inputs wait in LDS during the pass (the pass needs
     // the registers: at 8 waves per SIMD they would spill to scratch).
@@ -2215,3 +2227,4 @@ void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t 
 }
 
 }  // namespace mraft
+
