@@ -96,7 +96,7 @@ for st in ${DO:-tests bench}; do
           if [ "$t" = in-tree ]; then unset MRAFT_LIB; else export MRAFT_LIB=$PWD/tools/variants/libmraft_hip_$t.so; fi
           timeout -k 10 200 python3 bench_election.py --no-cpu-baseline > "$OUT/abelect_${t}_$pass.json" 2> "$OUT/abelect_${t}_$pass.err" \
             || { tail -3 "$OUT/abelect_${t}_$pass.err"; exit 1; }
-          python3 -c "import json; d=json.loads(open('$OUT/abelect_${t}_$pass.json').read().strip().splitlines()[-1]); print('$t', $pass, round(d['kernel_ms_mean'], 4))"
+          python3 -c "import json; d=json.loads(open('$OUT/abelect_${t}_$pass.json').read().strip().splitlines()[-1]); print('$t', $pass, round(d['ms_per_step'], 4), d['roofline'].get('frac'))"
         done
       done
       unset MRAFT_LIB ;;
@@ -115,7 +115,7 @@ for st in ${DO:-tests bench}; do
         REPS=3 timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/cmp$i" -o c -- python3 tools/cmp_tick_handler.py \
           > "$OUT/cmp$i.json" 2> "$OUT/cmp$i.err" || { tail -5 "$OUT/cmp$i.err"; exit 1; }
       done
-      python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>,k_handle_set<4, 0>,k_handle_deferred,k_gather_args,k_claim_ae" > /dev/null
+      python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>;k_handle_set<4, 0>;k_handle_deferred;k_gather_args;k_claim_ae" > /dev/null
       python3 tools/cmp_summary.py "$OUT" "$OUT/cmp_summary.json" | head -60 ;;
     ctest)
       echo "== ctest"

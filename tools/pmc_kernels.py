@@ -2,7 +2,7 @@
 directories (each pass its own directory): counters_per_dispatch[kernel]
 [counter] = mean over that kernel's dispatches of the largest grid.
 
-Usage: python tools/pmc_kernels.py out.json dir1 [dir2 ...] [--kernels a,b]"""
+Usage: python tools/pmc_kernels.py out.json dir1 [dir2 ...] [--kernels "a;b"]"""
 import csv
 import glob
 import json
@@ -42,7 +42,7 @@ if __name__ == "__main__":
     only = None
     if "--kernels" in args:
         i = args.index("--kernels")
-        only = set(args[i + 1].split(","))
+        only = set(args[i + 1].split(";"))
         args = args[:i] + args[i + 2:]
     res = collect(args[1:], only)
     json.dump(res, open(args[0], "w"), indent=1)
