@@ -88,7 +88,7 @@ def sleep_cycles_per_ms(stream) -> float:
     return 1e6 / max(a.elapsed_time(b), 1e-3)
 
 
-def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset_ms=0.0):
+def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset_ms=0.0, split=False):
     """The config #3 message-level path (gather -> HandleAppendEntries by
     reference -> processAppendEntriesReply + a1) as S shard
     pipelines: shard s = groups [G*s/S, G*(s+1)/S) of every state copy (SoA
@@ -98,8 +98,10 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
     the engine calls, so one shard's host-side work does not hold the other
     back (no call waits on the device: round 5). Step i runs on copy i restored
     from `master`; the warm-up on copy `steps`.
-    S = 1: one event between consecutive calls (the per-call split);
-    S > 1: one event per step on each queue (the device span per step);
+    split (S = 1): one event between consecutive calls (the per-call split;
+    each event is a marker packet, a bubble of ~6 us on the queue: profiles/r5_c1);
+    otherwise one event per step on each queue, as the headline records one
+    per tick (the device span per step);
     shard s > 0 starts `offset_ms` * s / (S - 1) after shard 0 (a device
     spin on its queue), so the shards' short latency-bound calls (gather,
     claims, fold) can run beside another shard's streaming handler
@@ -192,7 +194,7 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
         assert np.array_equal(fw["commit"][ld_sl], copies[steps]["commit_index"].cpu().numpy()[ld_sl]), \
             "fold word count: replayed commits differ from the device's"
         out["hw"], out["fw"] = hw, fw
-    nm = 4 if S == 1 else 1
+    nm = 4 if S == 1 and split else 1
     marks = [[[torch.cuda.Event(enable_timing=True) for _ in range(nm)] for _ in range(steps)] for _ in range(S)]
     # A gate: every queue waits for an event recorded behind a ~5 ms device
     # spin on torch's stream, so all threads have enqueued their first step
@@ -229,7 +231,7 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
     torch.cuda.synchronize()
     out["device_ms_per_step"] = max(t_begin.elapsed_time(marks[si][-1][-1]) for si in range(S)) / steps
     out["steps"] = steps
-    if S == 1:
+    if S == 1 and split:
         m = marks[0]
         out["ms_per_call"] = {"gather": float(np.mean([x[0].elapsed_time(x[1]) for x in m])),
                               "handle": float(np.mean([x[1].elapsed_time(x[2]) for x in m])),
@@ -264,7 +266,8 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
         return torch.cuda.Event(enable_timing=True)
 
     # -- message-level path, config #3
-    one = message_path(master, copies, lp, G, P, L, dev, 1, steps, words=True)
+    one = message_path(master, copies, lp, G, P, L, dev, 1, steps, words=True, split=True)
+    flat = message_path(master, copies, lp, G, P, L, dev, 1, len(copies) - 1)
     two = message_path(master, copies, lp, G, P, L, dev, 2, len(copies) - 1)
     three = message_path(master, copies, lp, G, P, L, dev, 3, len(copies) - 1)
     hw, fw, ms = one["hw"], one["fw"], one["ms_per_call"]
@@ -290,7 +293,11 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                      "steps": three["steps"], "device_ms_per_step": three["device_ms_per_step"],
                      "decisions_per_s": G / (three["device_ms_per_step"] / 1e3),
                      "vs_headline": three["device_ms_per_step"] / headline_ms},
-        "one_pipeline_device_ms_per_step": one["device_ms_per_step"],
+        "one_pipeline_device_ms_per_step": flat["device_ms_per_step"],
+        "one_pipeline_vs_headline": flat["device_ms_per_step"] / headline_ms,
+        "one_pipeline_what": "the three calls one after another on one queue, one event per step (as the "
+                             "headline's per-tick event); the per-call split (ms_per_call) is a separate run "
+                             "with an event between calls",
         "vs_headline": min(two["device_ms_per_step"], three["device_ms_per_step"]) / headline_ms,
         "vs_headline_what": "the message path's device time per step with the better of two and three shard "
                             "pipelines, over the headline's ms_per_step on the same box (the calls one after "

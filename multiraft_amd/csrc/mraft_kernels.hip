@@ -2027,7 +2027,9 @@ static void launch_ref(const HsArgs &ka, hipStream_t st) {
   launch_set<NI, HM_MAIN>(ka, (ka.n + NI - 1) / NI, st);
   // the deferred launch, enqueued blind (its counts are on the device): a
   // fixed grid that grid-strides over the deferred items
-  const int64_t g = min(ka.n, (int64_t)2048);
+  // (512 workgroups: an empty launch costs its dispatch — 4.1 us at 2,048,
+  // profiles/r5_c1 — and deferred items are few; they grid-stride)
+  const int64_t g = min(ka.n, (int64_t)512);
   hipLaunchKernelGGL(k_handle_deferred, dim3((unsigned)g), dim3(64), 0, st, ka);
 }
 
@@ -2092,8 +2094,10 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
                        flags, item_err, pend, pcount, lcount, llist);                         \
     if (MRAFT_FOLD_TAIL && split && MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1) {            \
-      const int nl = (int)min(n_seg, (int64_t)4096);                                          \
-      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)8192);         \
+      /* grid-stride over both lists, sized for their usual lengths (long segments are */     \
+      /* rare, most a1 ranges settle in k_fold): 12,288 workgroups took 4.2 us to launch */   \
+      const int nl = (int)min(n_seg, (int64_t)256);                                           \
+      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)2048);         \
       hipLaunchKernelGGL(k_fold_tail<PP>, dim3((unsigned)(nl + ns)), bl, 0, st, s, items, seg_begin, \
                          seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist, nl); \
       return;                                                                                 \

@@ -26,9 +26,10 @@ def main():
     copies = [{k: v.clone() for k, v in master.items()} for _ in range(copies_n)]
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    one = bench.message_path(master, copies, lp, G, P, L, dev, 1, 8)
+    one = bench.message_path(master, copies, lp, G, P, L, dev, 1, 8, split=True)
+    flat = bench.message_path(master, copies, lp, G, P, L, dev, 1, copies_n - 1)
     out = {"lib": os.environ.get("MRAFT_LIB", "in-tree"), "ms_per_call": one["ms_per_call"],
-           "one_pipeline_ms": one["device_ms_per_step"]}
+           "one_pipeline_split_ms": one["device_ms_per_step"], "one_pipeline_ms": flat["device_ms_per_step"]}
     for S in [int(x) for x in os.environ.get("SHARDS", "2").split(",")]:
         r = bench.message_path(master, copies, lp, G, P, L, dev, S, copies_n - 1)
         out["two_pipelines_ms" if S == 2 else f"pipelines_{S}_ms"] = r["device_ms_per_step"]
