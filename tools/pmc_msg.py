@@ -1,4 +1,4 @@
-"""Per-kernel HBM bytes of the message path (tools/gpu_r4.sh pmcmsg: FETCH_SIZE
+"""Per-kernel HBM bytes of the message path (tools/gpu_r5.sh pmcmsg: FETCH_SIZE
 and WRITE_SIZE passes over tools/ab_message_path.py), calibrated with the
 factors of profiles/pmc_traffic_s2.json. Per kernel: dispatches, and the
 average read / written MB per dispatch over its dispatches of the largest

@@ -1,5 +1,5 @@
 """VALU issue of the config #5 election storm (k_election_rounds<7>) from a
-rocprofv3 --pmc pass of bench_election.py (tools/gpu_r4.sh step `valu`) into
+rocprofv3 --pmc pass of bench_election.py (tools/gpu_r5.sh step `valu`) into
 profiles/pmc_valu_config5.json, read by bench.py / bench_election.py as the
 storm's roofline (bound: VALU issue).
 
