@@ -25,16 +25,6 @@ namespace {
 #ifndef MRAFT_EL_GM_LDS
 #define MRAFT_EL_GM_LDS 1  // grant-mask transpose: 1 LDS bytes, 2 ballots, 0 __shfl
 #endif
-#ifndef MRAFT_EL_MASK_LDS
-#define MRAFT_EL_MASK_LDS 1  // round masks staged in LDS, kEmBlock rounds per cooperative load (0: one
-                             // global load per round, one round ahead)
-#endif
-// Rounds of candidate masks one cooperative load stages (the workgroup's 32
-// groups x kEmBlock bytes): every load of a block is in flight at once, and a
-// round then reads its mask from LDS instead of waiting on a global load
-// issued one round earlier (an L2 / Infinity Cache round trip is longer than a
-// round's work).
-constexpr int kEmBlock = 64;
 
 // A broadcast term word: with the sparse voter loop the candidate bit is not
 // needed (the loop walks the candidate mask), so the word is the bare term.
@@ -71,39 +61,14 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
   __shared__ int lds_cx[256];
   __shared__ __attribute__((aligned(8))) uint8_t lds_gm[256];
-  // staged masks: [local group][round in block], 4-B aligned rows
-  __shared__ __attribute__((aligned(16))) uint8_t lds_m[32][kEmBlock + 4];
   const int seg = (int)(threadIdx.x & 63) & ~7;
-  const int lg = (int)(threadIdx.x >> 3);  // this lane's group within the workgroup
-  const long long g0 = (long long)blockIdx.x * 32;
   int fl = 0, became = 0, pd = 0;  // pd: persist() ran (StartElection :15, HandleRequestVote :57, :45)
-  int mnext = (!MRAFT_EL_MASK_LDS && grp && R > 0) ? (int)cand[g] : 0;  // (no staging) one round ahead
-  uint32_t mw = 0;  // (staging) four rounds' masks, read from LDS as one word
+  // The round's timeout mask, loaded one round ahead. (Staging 64 rounds of
+  // masks through LDS per cooperative load measured 1 % slower, r5_c1 / r5_e3.)
+  int mnext = (grp && R > 0) ? (int)cand[g] : 0;
   for (int r = 0; r < R; ++r) {
-    int m;
-    if (MRAFT_EL_MASK_LDS) {
-      const int rr = r % kEmBlock;
-      if (rr == 0) {
-        // the next block: thread t loads round t / 4's bytes of groups
-        // (t % 4) * 8 .. + 7 of this workgroup
-        __syncthreads();  // every wave is done with the previous block
-        const int t = (int)threadIdx.x, br = t >> 2, gb = (t & 3) * 8;
-        if (r + br < R) {
-          const uint8_t *src = cand + (long long)(r + br) * s.G + g0 + gb;
-          uint8_t v[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = (g0 + gb + k < s.G) ? src[k] : 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) lds_m[gb + k][br] = v[k];
-        }
-        __syncthreads();
-      }
-      if ((rr & 3) == 0) mw = *reinterpret_cast<const uint32_t *>(&lds_m[lg][rr]);
-      m = grp ? (int)((mw >> (8 * (rr & 3))) & 0xffu) : 0;
-    } else {
-      m = mnext;
-      if (grp && r + 1 < R) mnext = (int)cand[(long long)(r + 1) * s.G + g];
-    }
+    const int m = mnext;
+    if (grp && r + 1 < R) mnext = (int)cand[(long long)(r + 1) * s.G + g];
     const int isc = act && ((m >> p) & 1) && role != kLeader;
     if (isc) {                                                         // StartElection :6-17
       role = kCandidate;
