@@ -6,29 +6,19 @@
 // order, every RequestVote delivered voter by voter in candidate order
 // (HandleRequestVote :54-77 with isLogUpToDate, raft_log.go:99-104), every
 // candidate's tally in voter order (closure :22-47).
+//
+// Round 5 (profiles/r5_e1 README): one lane per group, two lanes per group,
+// a dense voter loop, a branch-free vote-key loop and LDS-staged round masks
+// were all measured (parity green) and all slower; this layout hides its
+// dependent chains with 8 waves per SIMD, and its branchy sparse loop skips
+// the grant evaluation where `a >= term` fails. The alternatives' compile-time
+// knobs are gone (the ISA of this kernel is unchanged by their removal).
 #include "mraft_device.h"
 #include "mraft_internal.h"
 
 namespace mraft {
 
 namespace {
-
-#ifndef MRAFT_EL_CX_LDS
-#define MRAFT_EL_CX_LDS 1  // candidate broadcast through LDS (else __shfl)
-#endif
-#ifndef MRAFT_EL_SPARSE
-#define MRAFT_EL_SPARSE 1  // voter loop over the round's candidates only (else all P peers)
-#endif
-#ifndef MRAFT_EL_TALLY_CF
-#define MRAFT_EL_TALLY_CF 1  // closed-form vote tally (else the per-reply fold)
-#endif
-#ifndef MRAFT_EL_GM_LDS
-#define MRAFT_EL_GM_LDS 1  // grant-mask transpose: 1 LDS bytes, 2 ballots, 0 __shfl
-#endif
-
-// A broadcast term word: with the sparse voter loop the candidate bit is not
-// needed (the loop walks the candidate mask), so the word is the bare term.
-#define EL_T(x) (MRAFT_EL_SPARSE ? (x) : ((x) & 0x7fffffff))
 
 template <int P>
 __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *__restrict__ cand,
@@ -81,17 +71,14 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // One broadcast per replica per round, through this wave's LDS words: its
     // term with the candidate bit on top.
     int cx[8];
-    const int mycx = MRAFT_EL_SPARSE ? at : (int)((unsigned)at | ((unsigned)isc << 31));
-    if (MRAFT_EL_CX_LDS) {
-      lds_cx[threadIdx.x] = mycx;
-      __builtin_amdgcn_wave_barrier();
+    const int mycx = at;
+    lds_cx[threadIdx.x] = mycx;
+    __builtin_amdgcn_wave_barrier();
+    {
       const int4 a = *reinterpret_cast<const int4 *>(&lds_cx[threadIdx.x & ~7u]);
       const int4 b = *reinterpret_cast<const int4 *>(&lds_cx[(threadIdx.x & ~7u) + 4]);
       cx[0] = a.x; cx[1] = a.y; cx[2] = a.z; cx[3] = a.w;
       cx[4] = b.x; cx[5] = b.y; cx[6] = b.z; cx[7] = b.w;
-    } else {
-#pragma unroll
-      for (int c = 0; c < 8; ++c) cx[c] = c < P ? __shfl(mycx, c, 8) : 0;
     }
     // RequestVote deliveries: voter p handles the candidates in peer order
     // (HandleRequestVote :54-77). pmx = max args.Term over candidates c <= p,
@@ -99,7 +86,6 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // tally below needs (a voter's term after handling c is the max of the
     // two, the stale branch included).
     int gm = 0, pmx = INT32_MIN;
-#if MRAFT_EL_SPARSE
     // Only the candidates: the k-th set bit of the group's candidate mask, for
     // k below the wave's largest candidate count (ascending peer order kept).
     const unsigned long long cb = __ballot(isc);
@@ -113,7 +99,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       cm &= cm - 1;
       const int cxc = __shfl(mycx, c, 8);
       const bool cisc = any;
-      const int cat = EL_T(cxc);
+      const int cat = (cxc);
       pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
       const bool h = act && cisc && c != p;                            // this voter handles c's RV
       const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
@@ -125,58 +111,27 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       voted = grant ? c : voted;
       gm |= (int)grant << c;
     }
-#else
-#pragma unroll
-    for (int c = 0; c < P; ++c) {  // branch-free: every step is a select
-      const bool cisc = cx[c] < 0;
-      const int cat = cx[c] & 0x7fffffff;
-      pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
-      const bool h = act && cisc && c != p;                            // this voter handles c's RV
-      pd |= (int)h;
-      const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
-      const bool gt = h && cat > term;                                 // :63-66
-      term = gt ? cat : term;
-      role = gt ? kFollower : role;
-      voted = gt ? -1 : voted;
-      const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
-      voted = grant ? c : voted;
-      gm |= (int)grant << c;
-    }
-#endif
     // Grants transposed through LDS: byte v of the segment's word = voter v's
     // grant mask; bit v of mine = voter v granted this lane.
     int mine = 0;
-    if (MRAFT_EL_GM_LDS == 1) {
+    {
       lds_gm[threadIdx.x] = (uint8_t)gm;
       __builtin_amdgcn_wave_barrier();
       const unsigned long long gw = *reinterpret_cast<const unsigned long long *>(&lds_gm[threadIdx.x & ~7u]);
       mine = (int)((((gw >> p) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
       __builtin_amdgcn_wave_barrier();
-    } else if (MRAFT_EL_GM_LDS == 2) {
-      // One ballot per candidate bit: bit seg+v of b_c = voter v granted c.
-      unsigned long long bs = 0;
-#pragma unroll
-      for (int c = 0; c < P; ++c) {
-        const unsigned long long b = __ballot((gm >> c) & 1);
-        bs = p == c ? b : bs;
-      }
-      mine = (int)((bs >> seg) & 0xffull);
-    } else {
-#pragma unroll
-      for (int v = 0; v < P; ++v) mine |= ((__shfl(gm, v, 8) >> p) & 1) << v;
     }
     // Tally (closure :22-47): candidate p folds its replies in voter order.
     // The guard (:29) can only flip at the first event, becoming leader at the
     // grant that makes a majority (:32-38) or stepping down at the first
     // refusal whose reply.Term exceeds args.Term (:42-45), so the fold is
     // closed-form: whichever of the two positions comes first in voter order.
-#if MRAFT_EL_TALLY_CF
     {
       const bool ok0 = isc && term == at && role == kCandidate;
       const int om = ((1 << P) - 1) & ~(1 << p);
       int gt = 0, tv = 0;
 #pragma unroll
-      for (int v = 0; v < P; ++v) gt |= (int)(EL_T(cx[v]) > at) << v;
+      for (int v = 0; v < P; ++v) gt |= (int)((cx[v]) > at) << v;
       // reply.Term = max(voter's own term, pmx) > at: every refusal when pmx > at.
       const int smask = om & ~mine & (pmx > at ? om : gt);
       int mm = mine & om;
@@ -184,12 +139,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       for (int k = 1; k < (P / 2 > 1 ? P / 2 : 1); ++k) mm &= mm - 1;  // the (P/2)-th grant
       const int lpos = mm ? __builtin_ctz(mm) : 32;
       const int spos = smask ? __builtin_ctz(smask) : 32;
-      if (MRAFT_EL_CX_LDS) {
-        tv = EL_T(lds_cx[(threadIdx.x & ~7u) + min(spos, 7)]);  // used only when spos < P
-      } else {
-#pragma unroll
-        for (int v = 0; v < P; ++v) tv = spos == v ? EL_T(cx[v]) : tv;
-      }
+      tv = lds_cx[(threadIdx.x & ~7u) + min(spos, 7)];  // used only when spos < P
       const bool lead = ok0 && lpos < spos;
       const bool sd = ok0 && spos < lpos;
       const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
@@ -201,24 +151,6 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       voted = sd ? -1 : voted;
       fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
     }
-#else
-#pragma unroll
-    for (int v = 0; v < P; ++v) {
-      const bool ok = isc && v != p && term == at && role == kCandidate;  // :29
-      const bool gr = ok && ((mine >> v) & 1);                         // :30
-      votes += (int)gr;                                                // :31
-      const bool lead = gr && votes > P / 2;                           // :32-38
-      role = lead ? kLeader : role;
-      became |= (int)lead;
-      fl |= lead ? MRAFT_G_ELECTED : 0;
-      const int rt = max(cx[v] & 0x7fffffff, pmx);                     // voter v's reply.Term
-      const bool sd = ok && !gr && rt > term;                          // :42-45
-      role = sd ? kFollower : role;
-      term = sd ? rt : term;
-      voted = sd ? -1 : voted;
-      fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
-    }
-#endif
   }
   const unsigned long long el = __ballot(fl & MRAFT_G_ELECTED), sd = __ballot(fl & MRAFT_G_STEPPED_DOWN);
   if (grp && p == 0 && gflags) {
