@@ -315,6 +315,22 @@ __device__ __forceinline__ void mark_persist_ae(const Dev &s, int64_t slot, int 
   if (s.pdirty && bits) (void)__hip_atomic_fetch_or(&s.pdirty[slot], bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Grids of the launches enqueued blind (their work is counted on the device
+// and is usually small: deferred items need two leaders of one group in a
+// batch, long segments more replies than a lane group, a1 scans a range the
+// top-term probe did not settle). Small grids: a launch that must find free
+// wave slots beside another pipeline's handler finds them at once — two
+// pipelines 0.366-0.369 -> 0.358 ms per step, three 0.363-0.365 -> 0.354
+// (profiles/r5_g1; 512 / 256 / 2,048 workgroups before).
+#ifndef MRAFT_AE_DGRID
+#define MRAFT_AE_DGRID 8       // workgroups of the deferred launch (grid-stride over the deferred items)
+#endif
+#ifndef MRAFT_FOLD_TAIL_NL
+#define MRAFT_FOLD_TAIL_NL 16  // k_fold_tail workgroups for the long segments (grid-stride)
+#endif
+#ifndef MRAFT_FOLD_TAIL_NS
+#define MRAFT_FOLD_TAIL_NS 256 // k_fold_tail workgroups for the pending a1 scans (grid-stride)
+#endif
 #ifndef MRAFT_AE_RELOAD
 #define MRAFT_AE_RELOAD 1  // after the pass, kernel arguments re-read from the kernarg segment (not held across it)
 #endif
@@ -2027,9 +2043,7 @@ static void launch_ref(const HsArgs &ka, hipStream_t st) {
   launch_set<NI, HM_MAIN>(ka, (ka.n + NI - 1) / NI, st);
   // the deferred launch, enqueued blind (its counts are on the device): a
   // fixed grid that grid-strides over the deferred items
-  // (512 workgroups: an empty launch costs its dispatch — 4.1 us at 2,048,
-  // profiles/r5_c1 — and deferred items are few; they grid-stride)
-  const int64_t g = min(ka.n, (int64_t)512);
+  const int64_t g = min(ka.n, (int64_t)MRAFT_AE_DGRID);
   hipLaunchKernelGGL(k_handle_deferred, dim3((unsigned)g), dim3(64), 0, st, ka);
 }
 
@@ -2094,10 +2108,8 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
     hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
                        flags, item_err, pend, pcount, lcount, llist);                         \
     if (MRAFT_FOLD_TAIL && split && MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1) {            \
-      /* grid-stride over both lists, sized for their usual lengths (long segments are */     \
-      /* rare, most a1 ranges settle in k_fold): 12,288 workgroups took 4.2 us to launch */   \
-      const int nl = (int)min(n_seg, (int64_t)256);                                           \
-      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)2048);         \
+      const int nl = (int)min(n_seg, (int64_t)MRAFT_FOLD_TAIL_NL);                            \
+      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)MRAFT_FOLD_TAIL_NS); \
       hipLaunchKernelGGL(k_fold_tail<PP>, dim3((unsigned)(nl + ns)), bl, 0, st, s, items, seg_begin, \
                          seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist, nl); \
       return;                                                                                 \
