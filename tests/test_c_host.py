@@ -1,11 +1,15 @@
 """The boundary from a plain C host: tests/c_host/
 mraft_host_tick.c includes only include/mraft.h (C11, -Wall -Wextra -Werror
 -pedantic, no C++, no HIP header) and links libmraft_hip.so as a cgo binding
-does. It runs create -> load_state -> set_tick_shards(2) ->
-replicate_tick_export -> store_state -> destroy on each seeded tick vector and
-compares flags, GetState words and state with tests/golden/tick_vectors.bin —
-the committed tick_vectors.npz (expected outputs from the pure-Python
-restatement of src/raft/raft_append_entry.go:20-162) as a flat int32 file."""
+does. On each seeded tick vector it runs one replication
+round three ways, each on a fresh engine: the fused tick
+(set_tick_shards(2) -> replicate_tick_export), the per-message sequence a Go
+host drives (gather_append_args -> handle_append_entries_ex by reference ->
+process_append_replies -> export_group_status), and the same with the entries
+passed by value; every path's flags, GetState words and state are compared
+with tests/golden/tick_vectors.bin — the committed tick_vectors.npz (expected
+outputs from the pure-Python restatement of src/raft/raft_append_entry.go:
+20-162) as a flat int32 file."""
 import os
 import subprocess
 
@@ -49,4 +53,4 @@ def test_c_host_tick_vectors_gpu():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok: 3 vectors" in r.stdout
-    assert r.stdout.count("bit-exact") == 3
+    assert r.stdout.count("tick (2 shards), messages and by value") == 3 and r.stdout.count("bit-exact") == 3
