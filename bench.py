@@ -306,7 +306,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                      "algorithmic_bytes": hb, "achieved": hb / ms["handle"] / 1e6, "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": hb / (ms["handle"] / 1e3) / HBM_PEAK,
                      "sets": hw["sets"], "merges": hw["merges"]},
-        "fold_roofline": {"kernel": "mraft_process_append_replies (whole call: claim + k_fold + k_fold_scan)", "bound": "hbm",
+        "fold_roofline": {"kernel": "mraft_process_append_replies (whole call: claim + k_fold + k_fold_tail)", "bound": "hbm",
                           "algorithmic_bytes": 4 * fw["words"], "a1_log_bytes": 4 * fw["a1_log_words"],
                           "achieved": 4 * fw["words"] / ms["fold"] / 1e6, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                           "frac": 4 * fw["words"] / (ms["fold"] / 1e3) / HBM_PEAK,
@@ -314,7 +314,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                           "note": "tools/msg_words.py fold_words: a1 reads each range's top term and, unless it "
                                   "settles the range (currentTerm, or below it on a replica whose terms_sorted "
                                   "proof holds: include/mraft.h), Go's downward scan; k_fold folds the replies and "
-                                  "probes each range's top word, k_fold_scan scans the ranges the probes left open"}}
+                                  "probes each range's top word, k_fold_tail scans the ranges the probes left open"}}
 
     # -- config #5 election storm
     Ge, Pe, R = 65536, 7, 64

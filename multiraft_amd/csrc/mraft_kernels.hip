@@ -81,8 +81,8 @@ __global__ void k_claim_zero(const char *__restrict__ items, int64_t n, int stri
     z0[i] = 0;
     z1[i] = 0;
   }
-  if (i == 0 && zc) *zc = 0;  // no a1 range pending for k_fold_scan yet
-  if (i == 0 && zl) *zl = 0;  // no long segment for k_fold_long yet
+  if (i == 0 && zc) *zc = 0;  // no a1 range pending for k_fold_tail's scans yet
+  if (i == 0 && zl) *zl = 0;  // no long segment for k_fold_tail yet
   if (i >= n) return;
   int64_t rec = i;
   if (seg_begin) {
@@ -296,15 +296,6 @@ enum : int {
 #ifndef MRAFT_AE_MINW
 #define MRAFT_AE_MINW 8  // __launch_bounds__ minimum waves per SIMD of the handler
 #endif
-#ifndef MRAFT_AE_STASH
-#define MRAFT_AE_STASH 1  // park the per-lane reply inputs in LDS across the pass
-#endif
-#ifndef MRAFT_AE_DESC
-#define MRAFT_AE_DESC 1  // check a sorted-terms claim on the pass's loads (0: diagnostic only, wrong proofs)
-#endif
-#ifndef MRAFT_AE_PIPE
-#define MRAFT_AE_PIPE 1  // dwordx4 compare chunks software-pipelined (pass_pipe, mraft_pass.h)
-#endif
 
 // The handler's persist mark at the end of a set's wave as a non-returning
 // atomic OR: the wave does not wait for a load of the bits (a dependent round
@@ -330,9 +321,6 @@ __device__ __forceinline__ void mark_persist_ae(const Dev &s, int64_t slot, int 
 #endif
 #ifndef MRAFT_FOLD_TAIL_NS
 #define MRAFT_FOLD_TAIL_NS 256 // k_fold_tail workgroups for the pending a1 scans (grid-stride)
-#endif
-#ifndef MRAFT_AE_RELOAD
-#define MRAFT_AE_RELOAD 1  // after the pass, kernel arguments re-read from the kernarg segment (not held across it)
 #endif
 
 // Every argument of the handler kernels, as their one kernel argument: the
@@ -626,8 +614,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     // the pass is wave-wide (ballots, shuffles): one choice for every lane
     vec = __ballot(!vec) == 0;
     int found = -1;
-    DescTrack dt{MRAFT_AE_DESC && __ballot(cls == AE_MERGE && claim0) != 0, 0, INT32_MIN};
-#if MRAFT_AE_STASH
+    DescTrack dt{__ballot(cls == AE_MERGE && claim0) != 0, 0, INT32_MIN};
     // This lane's reply inputs wait in LDS during the pass (the pass needs
     // the registers: at 8 waves per SIMD they would spill to scratch).
     // (plain LDS stores and loads across a compiler memory barrier: a
@@ -640,36 +627,25 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     stash[9][lane] = (int)(uint32_t)(uint64_t)i; stash[10][lane] = (int)((uint64_t)i >> 32);
     stash[11][lane] = shint;
     asm volatile("" ::: "memory");
-#endif
     if (vec) {
       int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
-      if (MRAFT_AE_PIPE) {
-        if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
-      } else {
-        for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, true, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
-      }
+      if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
       copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
     } else {
       int c = plo;
       for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
       copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
     }
-#if MRAFT_AE_STASH
     asm volatile("" ::: "memory");
     cls = stash[0][lane]; f = stash[1][lane]; fterm = stash[2][lane]; flast = stash[3][lane];
     fc = stash[4][lane]; a.term = stash[5][lane]; a.leader_commit = stash[6][lane];
     r.conflict_index = stash[7][lane]; r.term = stash[8][lane];
     i = (int64_t)(((uint64_t)(uint32_t)stash[10][lane] << 32) | (uint32_t)stash[9][lane]);
     shint = stash[11][lane];
-#endif
-#if MRAFT_AE_RELOAD
+    // kernel arguments re-read from the kernarg segment, not held across the pass
     const HsArgs kr = reload_hs();
     int32_t *__restrict__ err = kr.err;
     mraft_ae_reply *__restrict__ rep = kr.rep;
-#else
-    int32_t *__restrict__ err = k0.err;
-    mraft_ae_reply *__restrict__ rep = k0.rep;
-#endif
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       if (lane != q || cls != AE_MERGE) continue;
@@ -691,16 +667,10 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
       }
     }
   }
-#if MRAFT_AE_RELOAD
   const HsArgs kt = reload_hs();
   const Dev &s2 = kt.s;
   int32_t *__restrict__ err2 = kt.err;
   mraft_ae_reply *__restrict__ rep2 = kt.rep;
-#else
-  const Dev &s2 = k0.s;
-  int32_t *__restrict__ err2 = k0.err;
-  mraft_ae_reply *__restrict__ rep2 = k0.rep;
-#endif
   if (cls == AE_NONE) {
     if (mine) rep2[i] = r;
   } else if (cls == AE_BAD) {
@@ -718,11 +688,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     mark_persist_ae(s2, f, MRAFT_PERSIST_STATE);                       // deferred :111
     rep2[i] = r;
   }
-#if MRAFT_AE_RELOAD
   mraft_ae_result *__restrict__ res = kt.res;
-#else
-  mraft_ae_result *__restrict__ res = k0.res;
-#endif
   if (res && mine && cls != AE_DEFER) {
     // the reply half of the record (nEntries, reply term, success,
     // ConflictIndex); an item rejected after the prologue (capacity: cls
@@ -903,73 +869,18 @@ __device__ __forceinline__ int quorum_rt(const int (&m)[8], int me) {
 #ifndef MRAFT_FOLD_GRID
 #define MRAFT_FOLD_GRID (1 << 30)  // workgroups of the reply fold (segments beyond: grid-stride)
 #endif
-#ifndef MRAFT_FOLD_TRACE
-#define MRAFT_FOLD_TRACE 0  // diagnostic build: s_memrealtime stamps per segment (tools/trace_fold.py)
-#endif
-#if MRAFT_FOLD_TRACE
-__device__ unsigned long long g_fold_trace[65536 * 6];
-#define FOLD_STAMP(k, dep)                                                                         \
-  do {                                                                                             \
-    if (sg < 65536 && lane == 0) {                                                                 \
-      asm volatile("" ::"v"(dep));                                                                 \
-      g_fold_trace[sg * 6 + (k)] = __builtin_amdgcn_s_memrealtime();                               \
-    }                                                                                              \
-  } while (0)
-#else
-#define FOLD_STAMP(k, dep) do {} while (0)
-#endif
-#ifndef MRAFT_FOLD_TAIL
-#define MRAFT_FOLD_TAIL 1  // k_fold_long and k_fold_scan as one launch (k_fold_tail; r4_v21: fold call -4 %)
-#endif
-#ifndef MRAFT_FOLD_XCD
-#define MRAFT_FOLD_XCD 1  // XCD-contiguous segment ranges (r4_v18: fold call -8 %, reads 55 -> 46 MB)
-#endif
-#ifndef MRAFT_FOLD_GROUP
-#define MRAFT_FOLD_GROUP 8  // reply segments per wave (64 / this lanes each: 8 or 4, 4 measured 10 % slower); 1: one per wave
-#endif
-#ifndef MRAFT_FOLD_MINW
-// __launch_bounds__ minimum waves per SIMD of the reply fold: one segment per
-// wave, 8 (SGPRs spill to VGPR lanes; 13 % faster than 7); four per wave, 6
-// (80 VGPRs, no scratch; at 8 the per-lane fold state spills 72 B/lane)
-#define MRAFT_FOLD_MINW (MRAFT_FOLD_GROUP > 1 && !MRAFT_FOLD_LONG_SPLIT ? 6 : 8)
-#endif
-
-#ifndef MRAFT_FOLD_EXP
-#define MRAFT_FOLD_EXP 0  // timing experiments only (wrong results): 1 = no a1 log reads, 2 = probes only
-#endif
-#ifndef MRAFT_FOLD_SCANU
-#define MRAFT_FOLD_SCANU 4    // a1 scan, first iteration: dword loads per lane in flight (64·U terms)
-#endif
-// Measured alternatives of the a1 scan (config #3 message path, both
-// populations of state copies, profiles/r3_experiments/fold_variants.txt):
-// a one-range batch scanning from its top without a separate probe, and 512 /
-// 768 / 1,024 / 1,280 terms per round trip after the first window (at 8, 8, 7
-// and 6 waves per SIMD) all fold in the same 0.125-0.144 ms or slower; the
-// wider windows lose (more load instructions, no fewer waits that matter).
-#ifndef MRAFT_FOLD_MERGED_PROBE
-#define MRAFT_FOLD_MERGED_PROBE 0  // 1: a batch with one a1 range scans from its top without a separate probe
-#endif
-#ifndef MRAFT_FOLD_SCANU2
-#define MRAFT_FOLD_SCANU2 4   // a1 scan, later iterations: dword loads per lane in flight (64·U2 terms)
-#endif
-#ifndef MRAFT_FOLD_SPLIT
-#define MRAFT_FOLD_SPLIT 1  // the four-segment fold's a1 scans in a second launch (k_fold_scan)
-#endif
-#ifndef MRAFT_FOLD_PROBE
-#define MRAFT_FOLD_PROBE 1  // split fold: k_fold probes each range's top word (0: k_fold_scan's first window does)
-#endif
-#ifndef MRAFT_FSCAN_U1
-#define MRAFT_FSCAN_U1 MRAFT_FSCAN_U  // k_fold_scan: dword loads per lane in the first window
-#endif
-#ifndef MRAFT_FSCAN_W
-#define MRAFT_FSCAN_W 4     // replies per k_fold_scan wave
-#endif
-#ifndef MRAFT_FOLD_LONG_SPLIT
-#define MRAFT_FOLD_LONG_SPLIT 1  // segments longer than a lane group go to k_fold_long (k_fold without the 64-lane path)
-#endif
-#ifndef MRAFT_FSCAN_U
-#define MRAFT_FSCAN_U 8     // k_fold_scan: dword loads per lane in flight (64·U terms per round trip; 4: +7 %)
-#endif
+// The fold's shape (r3-r5 A/B runs, profiles/INDEX.md): eight reply segments
+// per wave, 8 lanes each (four per wave measured 10 % slower; one per wave
+// slower still), waves of one XCD on a contiguous segment range (r4_v18: fold
+// call -8 %, reads 55 -> 46 MB); each segment's a1 ranges probed by their top
+// word in k_fold and the open ones scanned in a second launch, k_fold_tail,
+// which also folds the segments longer than a lane group on all 64 lanes
+// (r4_v21: -4 % against separate launches; the scans back inside k_fold,
+// r5_f1: no difference). Earlier variants live in git history.
+constexpr int kFoldGroups = 8;              // reply segments per k_fold wave
+constexpr int kFoldScanU = 4;               // long-segment a1 scan: dword loads per lane in flight (64·U terms)
+constexpr int kFscanU = 8;                  // k_fold_tail scans: dword loads per lane in flight (4: +7 %)
+constexpr int kFscanW = 4;                  // pending a1 ranges per k_fold_tail scan wave
 
 // One iteration of the a1 scan: the highest idx in [max(lo, top - 64·U + 1),
 // top] with row[idx] == a, or lo - 1 (wave-uniform arguments).
@@ -996,31 +907,18 @@ __device__ __forceinline__ int fold_scan_iter(const int32_t *__restrict__ row, i
 }
 
 // Highest idx in [lo, hi] with row[idx - base] == a, or lo - 1: the a1 scan
-// of the reply fold, 64·U terms in the first round trip, 64·U2 after.
-template <int U, int U2>
+// of the reply fold, 64·U terms per round trip.
+template <int U>
 __device__ __forceinline__ int fold_scan_down_eq(const int32_t *__restrict__ row, int base, int head, int L,
                                                  int lo, int hi, int a) {
   if (hi < lo) return lo - 1;
   int r = fold_scan_iter<U>(row, base, head, L, lo, hi, a);
-  for (int top = hi - kWave * U; r < lo && top >= lo; top -= kWave * U2)
-    r = fold_scan_iter<U2>(row, base, head, L, lo, top, a);
+  for (int top = hi - kWave * U; r < lo && top >= lo; top -= kWave * U)
+    r = fold_scan_iter<U>(row, base, head, L, lo, top, a);
   return r;
 }
 
-// Wave per segment (one 64-thread workgroup each). Lane k loads reply k of a
-// 64-reply batch, so a segment's replies arrive in one round trip; the fold
-// (a2, :66-88) then runs over them in array order on wave-uniform values.
-// a1 (:89-105) is evaluated after each successful reply exactly as :78 calls
-// it, but its log reads are deferred to the end of the batch: the fold never
-// reads commitIndex, and while the replica stays leader its term is the
-// segment's initial term, so every evaluation is "the highest index in
-// (H, top] whose term is currentTerm", with H the largest top evaluated so
-// far (an evaluation that scanned (commit, top] leaves no entry of that term
-// above the new commit up to top). The ranges of one batch are disjoint and
-// ascending: their top words are probed in parallel (one round trip; on a
-// log whose last entries carry the current term, every range ends there) and
-// only ranges whose top word differs are scanned, wave-cooperatively.
-// Appends the lanes' pending a1 ranges (pred) to k_fold_scan's compact list:
+// Appends the lanes' pending a1 ranges (pred) to k_fold_tail's compact list:
 // one atomic per wave on the list's counter. Record: {lo, hi, slot,
 // currentTerm}, {dummy, ring head, reply index, 0}. Wave-uniform call.
 __device__ __forceinline__ void push_pending(int4 *__restrict__ pend, unsigned *__restrict__ pcount, bool pred,
@@ -1038,23 +936,34 @@ __device__ __forceinline__ void push_pending(int4 *__restrict__ pend, unsigned *
   }
 }
 
-template <int P, bool PUSH = (MRAFT_FOLD_SPLIT != 0)>
+// A long segment (more replies than a lane group: k_fold_tail), one wave.
+// Lane k loads reply k of a 64-reply batch, so a segment's replies arrive in
+// one round trip; the fold
+// (a2, :66-88) then runs over them in array order on wave-uniform values.
+// a1 (:89-105) is evaluated after each successful reply exactly as :78 calls
+// it, but its log reads are deferred to the end of the batch: the fold never
+// reads commitIndex, and while the replica stays leader its term is the
+// segment's initial term, so every evaluation is "the highest index in
+// (H, top] whose term is currentTerm", with H the largest top evaluated so
+// far (an evaluation that scanned (commit, top] leaves no entry of that term
+// above the new commit up to top). The ranges of one batch are disjoint and
+// ascending: their top words are probed in parallel (one round trip; on a
+// log whose last entries carry the current term, every range ends there) and
+// only ranges whose top word differs are scanned, wave-cooperatively.
+template <int P>
 __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result *__restrict__ items,
                                              const int64_t *__restrict__ seg_begin, int64_t sg,
                                              const int32_t *__restrict__ seg_err,
                                              const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount) {
+                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err) {
   const int lane = lane_id();
   const int64_t b = seg_begin ? seg_begin[sg] : sg, e = seg_begin ? seg_begin[sg + 1] : sg + 1;
   int bad = uni(seg_err[sg]);  // the claim verdict: a bad segment's slot may be out of range
   if (b >= e) return;
   const int64_t cnt = e - b;
-  FOLD_STAMP(0, (int)sg);
   mraft_ae_result it{};
   if (lane < cnt) it = items[b + lane];
   const int slot = __builtin_amdgcn_readfirstlane(it.slot);
-  FOLD_STAMP(1, slot);
   const int me = slot % P;
   const int64_t mrow = (int64_t)slot * P;
   // The replica's state in one round trip: one load per lane, lanes 0..P-1
@@ -1081,7 +990,6 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       commit = __builtin_amdgcn_readlane(vs, 18);
   const int last = __builtin_amdgcn_readlane(vs, 19), dummy = __builtin_amdgcn_readlane(vs, 20),
             head = __builtin_amdgcn_readlane(vs, 21), srt = __builtin_amdgcn_readlane(vs, 22);
-  FOLD_STAMP(2, term + role + commit + last + dummy);
   for (int64_t base = 0; base < cnt; base += 64) {
     const int64_t i = base + lane;
     int sl = it.slot, pr = it.peer;
@@ -1143,48 +1051,21 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
       if (lane == k) myfl = fl;
     }
     // The batch's a1 ranges: probe every top word at once, scan the rest.
-    FOLD_STAMP(3, myfl + H);
     int x = -1;
-    if (MRAFT_FOLD_EXP == 1) plo = phi + 1;  // timing experiment only: no a1 log reads
-    if (MRAFT_FOLD_EXP == 2) plo = phi;      // timing experiment only: probes, no scans
-    const unsigned long long rm = __ballot(plo <= phi);  // replies whose evaluation has a range
-    if (PUSH) {
-      // probes here, scans in k_fold_scan (as fold_group4); with sorted terms
-      // a top term below currentTerm settles the range (include/mraft.h)
-      bool settled = false;
-      if (MRAFT_FOLD_PROBE && plo <= phi) {
-        const int pv = lrow[ring(phi - dummy + head, s.L)];
-        if (pv == t0) x = phi;                                           // :98
-        else settled = srt && pv < t0;
-      }
-      push_pending(pend, pcount, plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled,
-                   make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0),
-                   make_int4(dummy, head, (int)(b + base + lane), 0));
-    } else if (MRAFT_FOLD_MERGED_PROBE && !PUSH && rm && !(rm & (rm - 1))) {
-      // One range (the usual batch): no separate probe of its top word — the
-      // scan's first window starts there (one round trip fewer when the top
-      // term is not currentTerm, a 1-KiB window instead of one word when it is).
-      const int src = first_lane(rm);
-      const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64);
-      const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);
-      if (lane == src && r >= lo) x = r;
-    } else {
-      bool settled = false;
-      if (plo <= phi) {
-        const int pv = lrow[ring(phi - dummy + head, s.L)];
-        if (pv == t0) x = phi;                                           // :98
-        else settled = srt && pv < t0;
-      }
-      unsigned long long pend = __ballot(plo < phi && x < 0 && !settled);
-      while (pend) {
-        const int src = first_lane(pend);
-        pend &= pend - 1;
-        const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
-        const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
-        if (lane == src && r >= lo) x = r;
-      }
+    bool settled = false;
+    if (plo <= phi) {
+      const int pv = lrow[ring(phi - dummy + head, s.L)];
+      if (pv == t0) x = phi;                                             // :98
+      else settled = srt && pv < t0;
     }
-    FOLD_STAMP(4, x);
+    unsigned long long pend = __ballot(plo < phi && x < 0 && !settled);
+    while (pend) {
+      const int src = first_lane(pend);
+      pend &= pend - 1;
+      const int lo = __shfl(plo, src, 64), hi = __shfl(phi, src, 64) - 1;
+      const int r = fold_scan_down_eq<kFoldScanU>(lrow, dummy, head, s.L, lo, hi, t0);  // lo - 1 if none
+      if (lane == src && r >= lo) x = r;
+    }
     if (x >= 0) myfl |= MRAFT_F_COMMITTED;                               // :99-100
     const unsigned long long fm = __ballot(x >= 0);
     if (fm) commit = __shfl(x, 63 - __builtin_clzll(fm), 64);           // the latest range that found one
@@ -1206,13 +1087,11 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     for (int j = 0; j < P; ++j) if (lane == j) { om = m[j]; on = nx[j]; }
     if (lane < P) { s.match[mrow + lane] = om; s.next[mrow + lane] = on; }
   }
-  FOLD_STAMP(5, commit);
 }
-
 
 // a1's scans of the reply fold (raft_append_entry.go:89-105; the loop reads
 // terms from the top of the range down to the first one equal to currentTerm),
-// for the ranges k_fold's probes left open: wave per MRAFT_FSCAN_W replies, each
+// for the ranges k_fold's probes left open: wave per kFscanW replies, each
 // pending range scanned with the whole wave from its top down, stopping at the
 // first hit as Go does. Split from k_fold so the scans of every segment stream
 // at once instead of behind each segment's chain of dependent loads (bounds ->
@@ -1225,12 +1104,12 @@ __device__ __forceinline__ void fold_scan_blocks(const Dev &s, const int4 *__res
   const int lane = lane_id();
   const int64_t cnt = (int64_t)*pcount;  // k_fold's compact list: nothing pending, nothing to do
   const int L = s.L;
-  for (int64_t b0 = bid * MRAFT_FSCAN_W; b0 < cnt; b0 += nblk * MRAFT_FSCAN_W) {
+  for (int64_t b0 = bid * kFscanW; b0 < cnt; b0 += nblk * kFscanW) {
     const int64_t i = b0 + lane;
     // the record in one round trip: {lo, hi, slot, currentTerm}, {dummy,
     // head, reply index}
     int4 ra = make_int4(0, -1, 0, 0), rb = make_int4(0, 0, 0, 0);
-    if (lane < MRAFT_FSCAN_W && i < cnt) {
+    if (lane < kFscanW && i < cnt) {
       ra = pend[2 * i];
       rb = pend[2 * i + 1];
     }
@@ -1240,7 +1119,7 @@ __device__ __forceinline__ void fold_scan_blocks(const Dev &s, const int4 *__res
       const int klo = __builtin_amdgcn_readlane(lo, k), khi = __builtin_amdgcn_readlane(hi, k);
       const int kslot = __builtin_amdgcn_readlane(ra.z, k), kt0 = __builtin_amdgcn_readlane(ra.w, k);
       const int kd = __builtin_amdgcn_readlane(rb.x, k), kh = __builtin_amdgcn_readlane(rb.y, k);
-      const int x = fold_scan_down_eq<MRAFT_FSCAN_U1, MRAFT_FSCAN_U>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
+      const int x = fold_scan_down_eq<kFscanU>(s.log + (int64_t)kslot * L, kd, kh, L, klo, khi,
                                                                      kt0);  // klo - 1 if none
       if (lane == k && x >= klo) {
         flags[rb.z] |= MRAFT_F_COMMITTED;                                // :99-100
@@ -1248,12 +1127,6 @@ __device__ __forceinline__ void fold_scan_blocks(const Dev &s, const int4 *__res
       }
     }
   }
-}
-
-__global__ __launch_bounds__(64, 8) void k_fold_scan(Dev s, const int4 *__restrict__ pend,
-                                                     const unsigned *__restrict__ pcount,
-                                                     int32_t *__restrict__ flags) {
-  fold_scan_blocks(s, pend, pcount, flags, blockIdx.x, gridDim.x);
 }
 
 // Lane groups of GW lanes (the wave as 64 / GW groups).
@@ -1279,7 +1152,6 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount,
                                             unsigned *__restrict__ lcount, int64_t *__restrict__ llist) {
-  constexpr int NG = 64 / GW;
   static_assert(GW >= P && GW >= 7, "a group holds the replica's match / next rows and seven scalars");
   const int lane = lane_id(), gl = lane & (GW - 1);
   const int64_t sg = sg0 + lane / GW;
@@ -1292,10 +1164,10 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
     bad = seg_err[sg];  // the claim verdict: a bad segment's slot may be out of range
   }
   int cnt = (int)(e > b ? min(e - b, (int64_t)(GW + 1)) : 0);  // 0: nothing to fold (empty or inverted)
-  if constexpr (MRAFT_FOLD_LONG_SPLIT) {
-    // a segment longer than a group goes to k_fold_long's list (64-lane
-    // path, its own launch: this kernel stays at 8 waves per SIMD); its
-    // group folds nothing here
+  {
+    // a segment longer than a group goes to the long-segment list (the 64-lane
+    // path, k_fold_tail: this kernel stays at 8 waves per SIMD); its group
+    // folds nothing here
     const unsigned long long lm = __ballot(gl == 0 && cnt > GW);
     if (lm) {
       const int l0 = first_lane(lm);
@@ -1305,11 +1177,6 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
       if (gl == 0 && cnt > GW) llist[base + (unsigned)__popcll(lm & ((1ull << lane) - 1))] = sg;
     }
     if (cnt > GW) cnt = 0;
-  } else if (__ballot(cnt > GW)) {  // a segment longer than a group: all of them on the 64-lane path
-    for (int j = 0; j < NG; ++j)
-      if (sg0 + j < n_seg)
-        fold_segment<P>(s, items, seg_begin, sg0 + j, seg_err, claim, epoch, flags, item_err, pend, pcount);
-    return;
   }
   (void)n_items;
   mraft_ae_result it{};
@@ -1406,33 +1273,18 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   // currentTerm settles the range: no lower entry carries currentTerm.
   int x = -1;
   bool settled = false;
-  if ((MRAFT_FOLD_PROBE || !MRAFT_FOLD_SPLIT) && go && plo <= phi) {
+  if (go && plo <= phi) {
     const int pv = lrow[ring(phi - dummy + head, s.L)];
     if (pv == t0) x = phi;  // :98
     else settled = srt && pv < t0;
   }
-  if (MRAFT_FOLD_SPLIT) {
-    // the ranges whose top word differs are scanned by k_fold_scan, after this
-    // launch: it ORs MRAFT_F_COMMITTED into the reply's flags and raises the
-    // replica's commitIndex to the highest index it finds (the ranges of a
-    // segment are disjoint and ascending, so "the latest range that found
-    // one" is the maximum over all of them, probes included)
-    push_pending(pend, pcount, go && plo + MRAFT_FOLD_PROBE <= phi && x < 0 && !settled,
-                 make_int4(plo, phi - MRAFT_FOLD_PROBE, slot, t0), make_int4(dummy, head, (int)(b + gl), 0));
-  }
-  // the ranges whose top word differs, of all four groups, one after another
-  // with the whole wave (a 16-lane scan moves a quarter of the terms per round
-  // trip and measured 33 % slower over the call)
-  for (unsigned long long pw = MRAFT_FOLD_SPLIT ? 0ull : __ballot(go && plo < phi && x < 0 && !settled); pw;
-       pw &= pw - 1) {
-    const int src = first_lane(pw);
-    const int lo = __builtin_amdgcn_readlane(plo, src), hi = __builtin_amdgcn_readlane(phi, src) - 1;
-    const int sslot = __builtin_amdgcn_readlane(slot, src), sd = __builtin_amdgcn_readlane(dummy, src),
-              sh = __builtin_amdgcn_readlane(head, src), st0 = __builtin_amdgcn_readlane(t0, src);
-    const int r = fold_scan_down_eq<MRAFT_FOLD_SCANU, MRAFT_FOLD_SCANU2>(s.log + (int64_t)sslot * s.L, sd, sh, s.L,
-                                                                         lo, hi, st0);  // lo - 1 if none
-    if (lane == src && r >= lo) x = r;
-  }
+  // the ranges whose top word differs are scanned by k_fold_tail, after this
+  // launch: it ORs MRAFT_F_COMMITTED into the reply's flags and raises the
+  // replica's commitIndex to the highest index it finds (the ranges of a
+  // segment are disjoint and ascending, so "the latest range that found one"
+  // is the maximum over all of them, probes included)
+  push_pending(pend, pcount, go && plo + 1 <= phi && x < 0 && !settled, make_int4(plo, phi - 1, slot, t0),
+               make_int4(dummy, head, (int)(b + gl), 0));
   if (go && x >= 0) myfl |= MRAFT_F_COMMITTED;                           // :99-100
   const unsigned fm = gw_mask<GW>(go && x >= 0);
   if (fm) commit = __shfl(x, gw_base<GW>() + 31 - __clz((int)fm), 64);   // the latest range that found one
@@ -1454,58 +1306,32 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
 }
 
 template <int P>
-__global__ __launch_bounds__(64, MRAFT_FOLD_MINW) void k_fold(Dev s, const mraft_ae_result *__restrict__ items,
-                                             int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t n_seg,
-                                             const int32_t *__restrict__ seg_err,
-                                             const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                             int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                             int4 *__restrict__ pend, unsigned *__restrict__ pcount,
-                                             unsigned *__restrict__ lcount, int64_t *__restrict__ llist) {
-  if constexpr (MRAFT_FOLD_GROUP > 1) {
-    // lane groups of GW lanes, one segment each (fold_groupw); with
-    // MRAFT_FOLD_LONG_SPLIT the 64-lane path is not in this kernel at all
-    constexpr int NG = MRAFT_FOLD_GROUP, GW = 64 / NG;
-    if (MRAFT_FOLD_XCD && (int64_t)gridDim.x * NG >= n_seg) {
-      // each XCD a contiguous range of waves: neighbouring waves' segments
-      // share the lines of the replica arrays in one L2
-      const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
-      const int64_t wb = x * per + min(x, rem) + (b >> 3);
-      fold_groupw<P, GW>(s, items, n_items, seg_begin, NG * wb, n_seg, seg_err, claim, epoch, flags, item_err, pend,
-                         pcount, lcount, llist);
-      return;
-    }
-    for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
-      fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
-                         pcount, lcount, llist);
-  } else if (MRAFT_FOLD_XCD && (int64_t)gridDim.x >= n_seg) {  // neighbouring segments share scalar lines in one L2
+__global__ __launch_bounds__(64, 8) void k_fold(Dev s, const mraft_ae_result *__restrict__ items,
+                                                int64_t n_items, const int64_t *__restrict__ seg_begin, int64_t n_seg,
+                                                const int32_t *__restrict__ seg_err,
+                                                const unsigned long long *__restrict__ claim, uint32_t epoch,
+                                                int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
+                                                int4 *__restrict__ pend, unsigned *__restrict__ pcount,
+                                                unsigned *__restrict__ lcount, int64_t *__restrict__ llist) {
+  // lane groups of GW lanes, one segment each (fold_groupw)
+  constexpr int NG = kFoldGroups, GW = 64 / NG;
+  if ((int64_t)gridDim.x * NG >= n_seg) {
+    // each XCD a contiguous range of waves: neighbouring waves' segments
+    // share the lines of the replica arrays in one L2
     const int64_t nb = gridDim.x, b = blockIdx.x, x = b & 7, per = nb >> 3, rem = nb & 7;
-    const int64_t sg = x * per + min(x, rem) + (b >> 3);
-    if (sg < n_seg) fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
-  } else {
-    for (int64_t sg = blockIdx.x; sg < n_seg; sg += gridDim.x)
-      fold_segment<P>(s, items, seg_begin, sg, seg_err, claim, epoch, flags, item_err, pend, pcount);
+    const int64_t wb = x * per + min(x, rem) + (b >> 3);
+    fold_groupw<P, GW>(s, items, n_items, seg_begin, NG * wb, n_seg, seg_err, claim, epoch, flags, item_err, pend,
+                       pcount, lcount, llist);
+    return;
   }
+  for (int64_t sg0 = NG * (int64_t)blockIdx.x; sg0 < n_seg; sg0 += NG * (int64_t)gridDim.x)
+    fold_groupw<P, GW>(s, items, n_items, seg_begin, sg0, n_seg, seg_err, claim, epoch, flags, item_err, pend,
+                       pcount, lcount, llist);
 }
 
-// The segments k_fold left for the 64-lane path (longer than a lane group:
-// more replies than GW in one batch), wave per segment over its list.
-template <int P>
-__global__ __launch_bounds__(64, 8) void k_fold_long(Dev s, const mraft_ae_result *__restrict__ items,
-                                                     const int64_t *__restrict__ seg_begin,
-                                                     const int32_t *__restrict__ seg_err,
-                                                     const unsigned long long *__restrict__ claim, uint32_t epoch,
-                                                     int32_t *__restrict__ flags, int32_t *__restrict__ item_err,
-                                                     int4 *__restrict__ pend, unsigned *__restrict__ pcount,
-                                                     const unsigned *__restrict__ lcount,
-                                                     const int64_t *__restrict__ llist) {
-  const int64_t cnt = (int64_t)*lcount;
-  for (int64_t k = blockIdx.x; k < cnt; k += gridDim.x)
-    fold_segment<P>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err, pend, pcount);
-}
-
-// k_fold_long and k_fold_scan as one launch (MRAFT_FOLD_TAIL): the first
-// n_long workgroups fold the long segments, scanning their own ranges (so
-// they push nothing), the rest scan the ranges k_fold left open. The two
+// The fold's second launch: the first n_long workgroups fold the segments
+// k_fold left for the 64-lane path (longer than a lane group), scanning their
+// own ranges, the rest scan the ranges k_fold's probes left open. The two
 // halves touch different replicas (one segment per replica slot, the
 // claim), so they need no order between them: one kernel boundary fewer per
 // fold call.
@@ -1521,8 +1347,7 @@ __global__ __launch_bounds__(64, 8) void k_fold_tail(Dev s, const mraft_ae_resul
   if ((int)blockIdx.x < n_long) {
     const int64_t cnt = (int64_t)*lcount;
     for (int64_t k = blockIdx.x; k < cnt; k += n_long)
-      fold_segment<P, false>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err, nullptr,
-                             nullptr);
+      fold_segment<P>(s, items, seg_begin, llist[k], seg_err, claim, epoch, flags, item_err);
   } else {
     fold_scan_blocks(s, pend, pcount, flags, (int64_t)blockIdx.x - n_long, (int64_t)gridDim.x - n_long);
   }
@@ -2073,61 +1898,42 @@ void launch_handle_ae_host(const Dev &s, const mraft_ae_args *args, int64_t n, c
   launch_set<1, HM_HOST>(ka, n, st);
 }
 
-#if MRAFT_FOLD_TRACE
-extern "C" int mraft_debug_fold_trace(void *dst, long long nbytes) {
-  if (nbytes > (long long)sizeof(g_fold_trace)) nbytes = sizeof(g_fold_trace);
-  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fold_trace), (size_t)nbytes, 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess ? 0 : -3;
-}
-#endif
-
 void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const int64_t *seg_begin,
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
                  int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st) {
   // one launch for the claims and the zeroed outputs, one for the fold, one
-  // for the a1 scans the fold's probes left open (MRAFT_FOLD_SPLIT; scan_buf:
-  // fold_scan_bytes(n) of scratch)
+  // for the long segments and the a1 scans the fold's probes left open
+  // (scan_buf: fold_scan_bytes(n, n_seg) of scratch)
   const int64_t nt = max(n_seg, n);
-  if (nt <= 0) return;
-  const bool split = MRAFT_FOLD_SPLIT;  // the ABI always passes scan_buf
-  if (split && !scan_buf) return;
+  if (nt <= 0 || !scan_buf) return;
   // scan_buf: pend [2 int4 per reply] | pcount | lcount | llist [n_seg int64]
-  int4 *pend = split ? (int4 *)scan_buf : nullptr;                          // 2 int4 per pending reply
-  unsigned *pcount = split ? (unsigned *)(pend + 2 * n) : nullptr;          // the a1 list's length
-  unsigned *lcount = (unsigned *)((int4 *)scan_buf + 2 * n) + 1;            // the long-segment list's length
-  int64_t *llist = (int64_t *)((int4 *)scan_buf + 2 * n + 1);
+  int4 *pend = (int4 *)scan_buf;                                      // 2 int4 per pending reply
+  unsigned *pcount = (unsigned *)(pend + 2 * n);                      // the a1 list's length
+  unsigned *lcount = pcount + 1;                                      // the long-segment list's length
+  int64_t *llist = (int64_t *)(pend + 2 * n + 1);
   hipLaunchKernelGGL(k_claim_zero, dim3(blocks_for(nt, kMsgBlock)), dim3(kMsgBlock), 0, st, (const char *)items, n_seg,
                      (int)sizeof(mraft_ae_result), (int)offsetof(mraft_ae_result, slot), seg_begin, gp, claim,
                      epoch, seg_err, n, flags, item_err, pcount, lcount);
   if (n_seg <= 0) return;
-  const int64_t waves = (n_seg + MRAFT_FOLD_GROUP - 1) / MRAFT_FOLD_GROUP;
+  const int64_t waves = (n_seg + kFoldGroups - 1) / kFoldGroups;
   const dim3 gr((unsigned)min(waves, (int64_t)MRAFT_FOLD_GRID)), bl(64);
+  // the tail's grids: both halves grid-stride over lists whose lengths are
+  // read on the device
+  const int nl = (int)min(n_seg, (int64_t)MRAFT_FOLD_TAIL_NL);
+  const int64_t ns = min((n + kFscanW - 1) / kFscanW, (int64_t)MRAFT_FOLD_TAIL_NS);
   switch (s.P) {
-#define MRAFT_FOLD_CASE(PP)                                                                   \
-  case PP:                                                                                    \
-    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, \
-                       flags, item_err, pend, pcount, lcount, llist);                         \
-    if (MRAFT_FOLD_TAIL && split && MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1) {            \
-      const int nl = (int)min(n_seg, (int64_t)MRAFT_FOLD_TAIL_NL);                            \
-      const int64_t ns = min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)MRAFT_FOLD_TAIL_NS); \
-      hipLaunchKernelGGL(k_fold_tail<PP>, dim3((unsigned)(nl + ns)), bl, 0, st, s, items, seg_begin, \
-                         seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist, nl); \
-      return;                                                                                 \
-    }                                                                                         \
-    if (MRAFT_FOLD_LONG_SPLIT && MRAFT_FOLD_GROUP > 1)                                        \
-      hipLaunchKernelGGL(k_fold_long<PP>, dim3((unsigned)min(n_seg, (int64_t)4096)), bl, 0, st, s, items,  \
-                         seg_begin, seg_err, claim, epoch, flags, item_err, pend, pcount, lcount, llist); \
+#define MRAFT_FOLD_CASE(PP)                                                                              \
+  case PP:                                                                                               \
+    hipLaunchKernelGGL(k_fold<PP>, gr, bl, 0, st, s, items, n, seg_begin, n_seg, seg_err, claim, epoch, flags, \
+                       item_err, pend, pcount, lcount, llist);                                           \
+    hipLaunchKernelGGL(k_fold_tail<PP>, dim3((unsigned)(nl + ns)), bl, 0, st, s, items, seg_begin, seg_err, claim, \
+                       epoch, flags, item_err, pend, pcount, lcount, llist, nl);                         \
     break;
     MRAFT_FOLD_CASE(1) MRAFT_FOLD_CASE(2) MRAFT_FOLD_CASE(3) MRAFT_FOLD_CASE(4)
     MRAFT_FOLD_CASE(5) MRAFT_FOLD_CASE(6) MRAFT_FOLD_CASE(7) MRAFT_FOLD_CASE(8)
 #undef MRAFT_FOLD_CASE
     default: return;
   }
-  // the scans: grid-stride over the list k_fold left (its length read on the
-  // device); at most 8 waves per SIMD's worth of workgroups
-  if (split)
-    hipLaunchKernelGGL(k_fold_scan, dim3((unsigned)min((n + MRAFT_FSCAN_W - 1) / MRAFT_FSCAN_W, (int64_t)8192)),
-                       dim3(64), 0, st, s, pend, pcount, flags);
 }
 
 size_t fold_scan_bytes(int64_t n, int64_t n_seg) {

@@ -1,11 +1,12 @@
-"""The compile-time alternatives kept in the kernel sources (DESIGN.md §5:
-each was measured against the default and lost, and stays selectable for
-A/B runs, tools/build_variants.sh) still compile for gfx950: the unpipelined
-compare / copy loops, plain (temporal) loads and stores, two dwordx4 per lane
-per compare chunk, the state pointers held across the pass, linear group
-order, four groups per workgroup, the handler without its LDS stash, and the
-fold's one-width a1 scan, its a1 scans inside k_fold (no k_fold_scan), the
-handler holding its kernel arguments across the pass. CPU only (device-only compile, no GPU)."""
+"""The compile-time alternatives kept in the kernel sources still compile for
+gfx950. The tick's (each was measured against the default and
+lost, and stays selectable for A/B runs, tools/build_variants.sh): the
+unpipelined compare / copy loops, plain (temporal) loads and stores, two
+dwordx4 per lane per compare chunk, the state pointers held across the pass,
+linear group order, four groups per workgroup. The message path's grid knobs
+at their smallest (one workgroup for the fold, the deferred launch and each
+half of the fold's tail: every loop grid-strides). CPU only (device-only
+compile, no GPU)."""
 import os
 import subprocess
 
@@ -17,9 +18,8 @@ HIPCC = "/opt/rocm/bin/hipcc"
 VARIANTS = {
     "mraft_tick.hip": ["-DMRAFT_PASS_PIPE=0", "-DMRAFT_TICK_NT=0", "-DMRAFT_TICK_V=2", "-DMRAFT_TICK_RELOAD=0",
                        "-DMRAFT_TICK_XCD=0", "-DMRAFT_TICK_WPB=4", "-DMRAFT_TICK_MINW=6", "-DMRAFT_COPY_DEPTH=3"],
-    "mraft_kernels.hip": ["-DMRAFT_AE_PIPE=0", "-DMRAFT_AE_STASH=0", "-DMRAFT_TICK_NT=1", "-DMRAFT_FOLD_XCD=1",
-                          "-DMRAFT_FOLD_SCANU2=12", "-DMRAFT_FOLD_MERGED_PROBE=1",
-                          "-DMRAFT_FOLD_GROUP=1", "-DMRAFT_FOLD_SPLIT=0", "-DMRAFT_AE_RELOAD=0"],
+    "mraft_kernels.hip": ["-DMRAFT_TICK_NT=1", "-DMRAFT_FOLD_GRID=1", "-DMRAFT_AE_DGRID=1", "-DMRAFT_FOLD_TAIL_NL=1",
+                          "-DMRAFT_FOLD_TAIL_NS=1"],
 }
 
 

@@ -150,7 +150,7 @@ def test_fold_long_segments_gpu(P, seed):
 def test_fold_short_segments_gpu(P, seed):
     """Segments of at most eight replies (the eight-segments-per-wave fold),
     several a1 evaluations each, so one segment's pending ranges land in
-    different k_fold_scan waves and the replica's commitIndex is the maximum
+    different k_fold_tail scan waves and the replica's commitIndex is the maximum
     of their hits and the probes' (atomicMax); Figure-8 logs included."""
     from oracle_lib import random_reply_segments
     G, L = 1024, 512
