@@ -45,38 +45,23 @@ struct RingRow {
   }
 };
 
-#ifndef MRAFT_TICK_NT
-#define MRAFT_TICK_NT 3    // non-temporal streams: 1 = stores, 2 = loads, 3 = both
-#endif
-
-// Streaming (read-once / write-once) log accesses of the pass.
+// Streaming (read-once / write-once) log accesses of the pass: non-temporal
+// loads and stores (plain temporal accesses measured slower in both the tick
+// and the handler, round 2; git history keeps the variant).
 __device__ __forceinline__ int4 ld4(const int32_t *p) {
-  if (MRAFT_TICK_NT & 2) {
-    const int4 *q = reinterpret_cast<const int4 *>(p);
-    return make_int4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
-                     __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
-  }
-  return *reinterpret_cast<const int4 *>(p);
+  const int4 *q = reinterpret_cast<const int4 *>(p);
+  return make_int4(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y),
+                   __builtin_nontemporal_load(&q->z), __builtin_nontemporal_load(&q->w));
 }
-__device__ __forceinline__ int ld1(const int32_t *p) {
-  if (MRAFT_TICK_NT & 2) return __builtin_nontemporal_load(p);
-  return *p;
-}
+__device__ __forceinline__ int ld1(const int32_t *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st4(int32_t *p, int a, int b, int c, int d) {
-  if (MRAFT_TICK_NT & 1) {
-    int4 *q = reinterpret_cast<int4 *>(p);
-    __builtin_nontemporal_store(a, &q->x);
-    __builtin_nontemporal_store(b, &q->y);
-    __builtin_nontemporal_store(c, &q->z);
-    __builtin_nontemporal_store(d, &q->w);
-  } else {
-    *reinterpret_cast<int4 *>(p) = make_int4(a, b, c, d);
-  }
+  int4 *q = reinterpret_cast<int4 *>(p);
+  __builtin_nontemporal_store(a, &q->x);
+  __builtin_nontemporal_store(b, &q->y);
+  __builtin_nontemporal_store(c, &q->z);
+  __builtin_nontemporal_store(d, &q->w);
 }
-__device__ __forceinline__ void st1(int32_t *p, int a) {
-  if (MRAFT_TICK_NT & 1) __builtin_nontemporal_store(a, p);
-  else *p = a;
-}
+__device__ __forceinline__ void st1(int32_t *p, int a) { __builtin_nontemporal_store(a, p); }
 // EPL entries (4 or 2) of one lane: one dwordx4 or dwordx2 access.
 template <int EPL>
 __device__ __forceinline__ void ldv(const int32_t *p, int (&x)[EPL]) {
@@ -85,12 +70,7 @@ __device__ __forceinline__ void ldv(const int32_t *p, int (&x)[EPL]) {
     x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
   } else {
     const int2 *q = reinterpret_cast<const int2 *>(p);
-    if (MRAFT_TICK_NT & 2) {
-      x[0] = __builtin_nontemporal_load(&q->x); x[1] = __builtin_nontemporal_load(&q->y);
-    } else {
-      const int2 v = *q;
-      x[0] = v.x; x[1] = v.y;
-    }
+    x[0] = __builtin_nontemporal_load(&q->x); x[1] = __builtin_nontemporal_load(&q->y);
   }
 }
 template <int EPL>
@@ -99,11 +79,7 @@ __device__ __forceinline__ void stv(int32_t *p, const int (&x)[EPL]) {
     st4(p, x[0], x[1], x[2], x[3]);
   } else {
     int2 *q = reinterpret_cast<int2 *>(p);
-    if (MRAFT_TICK_NT & 1) {
-      __builtin_nontemporal_store(x[0], &q->x); __builtin_nontemporal_store(x[1], &q->y);
-    } else {
-      *q = make_int2(x[0], x[1]);
-    }
+    __builtin_nontemporal_store(x[0], &q->x); __builtin_nontemporal_store(x[1], &q->y);
   }
 }
 
@@ -207,7 +183,11 @@ struct DescTrack {
 // whose term equals T (kept in `found`, the pass ascends).
 // VEC: lane j owns entries c+256v+4j .. +3 (one dwordx4 per stream and v);
 // otherwise lane j owns c+64(4v+u)+j. Entry idx is at src.at(idx), follower
-// q's term of Index idx at fo.at(q, idx).
+// q's term of Index idx at fo.at(q, idx). The tick and the handler call the
+// dword form (V = 1, !VEC: rows not 16-B aligned alike, or a flat buffer whose
+// ends a dwordx4 would cross); their dwordx4 form is pass_pipe. (A dword-only
+// restatement of this template changed the tick kernel's register assignment,
+// so the measured code is kept as it is.)
 template <int V, bool VEC, bool COUNT, class Src, class F, class D = NoDesc>
 __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int slo, int shi, int T,
                                            int &found, int c, int plo, int phi, D &&dt = D{}) {
@@ -343,7 +323,7 @@ __device__ __forceinline__ void pass_chunk(const Src &src, F &fo, int nend, int 
   }
 }
 
-// The compare chunks of the pass (VEC, 64 * EPL entries per chunk: EPL = 4,
+// The compare chunks of the pass (dwordx4 form, 64 * EPL entries per chunk: EPL = 4,
 // one dwordx4 per lane and stream, or 2, one dwordx2) software-pipelined:
 // chunk c is compared, then chunk c+CW's loads (the leader's entries and the
 // words of every follower still comparing after chunk c) are issued, then
@@ -446,79 +426,10 @@ __device__ __forceinline__ int pass_pipe(const Src &src, F &fo, int nend, int sl
 // same loads. Software-pipelined: chunk c+256 is loaded before chunk c is
 // stored, so a wave never waits for its own stores before issuing the next
 // load (gfx9's vmcnt counts both in order). The next chunk is loaded only when
-// the loop will run for it: no extra traffic. (Two chunks ahead,
-// MRAFT_COPY_PIPE=2, measured no faster: the copy is memory-system-bound at 8
-// waves per SIMD, profiles/r2_experiments.)
-#ifndef MRAFT_COPY_DEPTH
-#define MRAFT_COPY_DEPTH 1  // copy-only loop: chunks loaded ahead of the one being stored
-#endif
-
-// The copy-only loop with D chunks loaded ahead (D >= 2), meant to shorten
-// the last groups of a launch (a lone wave's streaming rate is latency-bound).
-// Measured (same state copies, profiles/r3_experiments/ab_copydepth_g65536.txt):
-// D = 2, 3, 4 are all 3-4 % SLOWER than one chunk ahead (0.350 vs 0.339 ms):
-// more bytes in flight per wave only queue in the memory system. Kept as an
-// A/B alternative.
-template <int D, bool COUNT, class Src, class F, class DT>
-__device__ __forceinline__ void copy_loop_deep(const Src &src, const F &fo, int c, int nend, int plo, int phi,
-                                               int slo, int shi, int T, int &found, DT &dt) {
-  constexpr int NI = F::kNI;
-  constexpr int CW = 256;
-  const int lane = lane_id();
-  const int cmask = fo.copy;
-  const bool scan = slo <= shi;
-  // chunk cc is needed: a follower still copies there, or the commit scan runs there
-  auto need = [&](int cc) { return cc <= phi && ((cmask && cc < nend) || (scan && cc <= shi)); };
-  auto load = [&](int cc) {
-    int4 v = make_int4(0, 0, 0, 0);
-    if (need(cc) && cc + 4 * lane + 3 >= plo && cc + 4 * lane <= phi) v = ld4(src.at(cc + 4 * lane));
-    return v;
-  };
-  if (!need(c)) return;
-  int4 buf[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) buf[d] = load(c + d * CW);
-  for (;;) {
-    const int i0 = c + 4 * lane;
-    const int4 cur = buf[0];
-#pragma unroll
-    for (int d = 0; d + 1 < D; ++d) buf[d] = buf[d + 1];
-    buf[D - 1] = load(c + D * CW);  // issued before this chunk's stores
-    {
-      const int ce[4] = {cur.x, cur.y, cur.z, cur.w};
-      dt.template see<4>(ce, c, plo, phi);
-    }
-    if (scan && c <= shi && c + CW - 1 >= slo) {
-      const int e[4] = {cur.x, cur.y, cur.z, cur.w};
-      int lu = -1;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (i0 + u >= slo && i0 + u <= shi && e[u] == T) lu = u;
-      const unsigned long long m = __ballot(lu >= 0);
-      if (m) {
-        const int l = 63 - __clzll((long long)m);
-        found = c + 4 * l + __shfl(lu, l, 64);
-      }
-    }
-    if (!COUNT && cmask && c < nend) {
-#pragma unroll
-      for (int q = 0; q < NI; ++q) {
-        if (!((cmask >> q) & 1)) continue;
-        if (i0 + 3 < nend) {
-          st4(fo.at(q, i0), cur.x, cur.y, cur.z, cur.w);
-        } else {
-          const int e[4] = {cur.x, cur.y, cur.z, cur.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (i0 + u < nend) st1(fo.at(q, i0 + u), e[u]);
-        }
-      }
-    }
-    c += CW;
-    if (!need(c)) return;
-  }
-}
-
+// the loop will run for it: no extra traffic. (Two to four chunks ahead
+// measured no faster in round 2 and 3-4 % slower in round 3: the copy is
+// memory-system-bound at 8 waves per SIMD and more bytes in flight per wave
+// only queue, profiles/r2_experiments, r3_experiments/ab_copydepth_g65536.txt.)
 template <bool VEC, bool COUNT, class Src, class F, class D = NoDesc>
 __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, int nend, int plo, int phi,
                                           int slo, int shi, int T, int &found, D &&dt = D{}) {
@@ -526,10 +437,6 @@ __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, in
   constexpr int CW = 256;
   const int lane = lane_id();
   int cmask = fo.copy;
-  if constexpr (VEC && MRAFT_COPY_DEPTH > 1) {
-    copy_loop_deep<MRAFT_COPY_DEPTH, COUNT>(src, fo, c, nend, plo, phi, slo, shi, T, found, dt);
-    return;
-  }
   if constexpr (VEC) {
     if (c > phi || (!cmask && !(slo <= shi && c <= shi))) return;
     int4 cur = make_int4(0, 0, 0, 0);

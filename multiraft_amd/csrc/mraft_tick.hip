@@ -165,17 +165,11 @@ struct Fold {
   }
 };
 
-#ifndef MRAFT_TICK_V
-#define MRAFT_TICK_V 1     // dwordx4 vectors per lane per stream per compare chunk
-#endif
 #ifndef MRAFT_TICK_MINW
 #define MRAFT_TICK_MINW 8  // __launch_bounds__ minimum waves per SIMD
 #endif
 #ifndef MRAFT_TICK_ALIGN
 #define MRAFT_TICK_ALIGN 32  // pass chunks start on this many entries (32 = one 128-B line)
-#endif
-#ifndef MRAFT_TICK_RELOAD
-#define MRAFT_TICK_RELOAD 1  // phase C/D re-read the state pointers (not held across the pass)
 #endif
 #ifndef MRAFT_TICK_TRACE
 #define MRAFT_TICK_TRACE 0  // diagnostic build: s_memrealtime stamps per group (tools/trace_tick.py)
@@ -195,21 +189,17 @@ __device__ __forceinline__ unsigned long long tick_xcc() {
 #else
 #define TICK_STAMP(k) do {} while (0)
 #endif
-#ifndef MRAFT_TICK_XCD
-#define MRAFT_TICK_XCD 1   // XCD-aware block -> group mapping
-#endif
 #ifndef MRAFT_TICK_SCANU
 #define MRAFT_TICK_SCANU 1  // ConflictIndex scans past the probe: 64 * SCANU terms per round trip
 #endif
 #ifndef MRAFT_TICK_CMP_EPL
 #define MRAFT_TICK_CMP_EPL 4  // compare chunk: 64 * EPL entries (4: dwordx4 per lane, 2: dwordx2)
 #endif
-#ifndef MRAFT_PASS_PIPE
-#define MRAFT_PASS_PIPE 1   // compare chunks software-pipelined (next chunk's loads before this chunk's stores)
-#endif
-#ifndef MRAFT_TICK_WPB
-#define MRAFT_TICK_WPB 1   // waves (groups) per workgroup: 1 frees each wave's slot as soon as its group ends
-#endif
+// One wave (group) per 64-thread workgroup: each wave's slot frees as soon as
+// its group ends (four per workgroup, the group order without the XCD mapping,
+// the compare chunks without software pipelining, two dwordx4 per lane per
+// chunk and the state pointers held across the pass all measured slower; git
+// history keeps them).
 
 // GetState (raft.go:237-246) of the group's exported replica, fused into the
 // tick (mraft_replicate_tick_export): commit and currentTerm<<1 | isLeader.
@@ -224,23 +214,25 @@ struct Export {
 };
 
 template <int P, bool COUNT>
-__global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
+__global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_group(Dev s, const int32_t *__restrict__ leader_peer,
                                                     int32_t *__restrict__ gflags,
                                                     unsigned long long *__restrict__ counts,
                                                     Export ex) {
   constexpr int NI = P - 1;
-  constexpr int V = MRAFT_TICK_V;
   const int lane = lane_id();
   // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
   // §Workgroup dispatch): give each XCD a contiguous range of groups so the
   // scalar SoA lines neighbouring groups share stay in one XCD's L2. Speed
   // only; any placement gives the same results.
   int gb = (int)blockIdx.x;
-  if (MRAFT_TICK_XCD) {
+  {
     const int nb = (int)gridDim.x, x = gb & 7, per = nb >> 3, rem = nb & 7;
     gb = x * per + min(x, rem) + (gb >> 3);
   }
-  const int g = uni(gb * MRAFT_TICK_WPB + (int)(threadIdx.x >> 6));
+  // (threadIdx.x >> 6 is 0 in a one-wave workgroup; without the term the
+  // compiler assigns this kernel's registers differently, so the measured
+  // code is kept instruction-for-instruction)
+  const int g = uni(gb + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
   const int L = s.L;
   TICK_STAMP(0);
@@ -469,26 +461,16 @@ __global__ __launch_bounds__(64 * MRAFT_TICK_WPB, MRAFT_TICK_MINW) void k_tick_g
     // lane's dwordx4 stays contiguous).
     if (vec) {
       int c = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
-      if (MRAFT_PASS_PIPE && V == 1) {
-        if (c <= phi && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      } else {
-        for (; c <= phi && fo.cmp; c += 256 * V)
-          pass_chunk<V, true, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      }
+      if (c <= phi && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
       copy_loop<true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     } else {
       int c = plo;
-      for (; c <= phi && fo.cmp; c += 256 * V)
-        pass_chunk<V, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
+      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
       copy_loop<false, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
     }
   }
   TICK_STAMP(2);
-#if MRAFT_TICK_RELOAD
-  const Dev s2 = reload_dev();
-#else
-  const Dev &s2 = s;
-#endif
+  const Dev s2 = reload_dev();  // phase C/D re-read the state pointers (not held across the pass)
   int mk = -1;  // this lane's follower: first mismatching entry of its merge
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
@@ -714,9 +696,7 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
 template <int P, bool COUNT>
 void launch_tick_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, unsigned long long *counts,
                    Export ex, hipStream_t st) {
-  const int blocks = (s.G + MRAFT_TICK_WPB - 1) / MRAFT_TICK_WPB;
-  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(blocks), dim3(64 * MRAFT_TICK_WPB), 0, st, s,
-                     lpeer, gflags, counts, ex);
+  hipLaunchKernelGGL((k_tick_group<P, COUNT>), dim3(s.G), dim3(64), 0, st, s, lpeer, gflags, counts, ex);
 }
 
 template <bool COUNT>

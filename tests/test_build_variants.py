@@ -1,12 +1,10 @@
-"""The compile-time alternatives kept in the kernel sources still compile for
-gfx950. The tick's (each was measured against the default and
-lost, and stays selectable for A/B runs, tools/build_variants.sh): the
-unpipelined compare / copy loops, plain (temporal) loads and stores, two
-dwordx4 per lane per compare chunk, the state pointers held across the pass,
-linear group order, four groups per workgroup. The message path's grid knobs
-at their smallest (one workgroup for the fold, the deferred launch and each
-half of the fold's tail: every loop grid-strides). CPU only (device-only
-compile, no GPU)."""
+"""The numeric knobs kept in the kernel sources (the losing code variants were
+removed in round 5; git history keeps them) still compile for gfx950 at other
+values: the tick at 6 waves per SIMD, dwordx2 compare chunks and 256-term
+ConflictIndex scans, and its s_memrealtime trace build (tools/trace_tick.py);
+the message path's grids at their smallest (one workgroup for the fold, the
+deferred launch and each half of the fold's tail: every loop grid-strides).
+CPU only (device-only compile, no GPU)."""
 import os
 import subprocess
 
@@ -16,9 +14,8 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 HIPCC = "/opt/rocm/bin/hipcc"
 
 VARIANTS = {
-    "mraft_tick.hip": ["-DMRAFT_PASS_PIPE=0", "-DMRAFT_TICK_NT=0", "-DMRAFT_TICK_V=2", "-DMRAFT_TICK_RELOAD=0",
-                       "-DMRAFT_TICK_XCD=0", "-DMRAFT_TICK_WPB=4", "-DMRAFT_TICK_MINW=6", "-DMRAFT_COPY_DEPTH=3"],
-    "mraft_kernels.hip": ["-DMRAFT_TICK_NT=1", "-DMRAFT_FOLD_GRID=1", "-DMRAFT_AE_DGRID=1", "-DMRAFT_FOLD_TAIL_NL=1",
+    "mraft_tick.hip": ["-DMRAFT_TICK_MINW=6", "-DMRAFT_TICK_CMP_EPL=2", "-DMRAFT_TICK_SCANU=4", "-DMRAFT_TICK_TRACE=1"],
+    "mraft_kernels.hip": ["-DMRAFT_FOLD_GRID=1", "-DMRAFT_AE_DGRID=1", "-DMRAFT_FOLD_TAIL_NL=1",
                           "-DMRAFT_FOLD_TAIL_NS=1"],
 }
 

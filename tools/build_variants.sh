@@ -1,7 +1,7 @@
 #!/bin/bash
 # Builds tick-kernel variants as tools/variants/libmraft_hip_<tag>.so (same
 # sources, different compile-time knobs); tools/ab_tick_pmc.sh and tools/ab_message_path.py time them.
-# Each argument is  tag[@SRCDIR]=DEFINES  e.g.  "v2=-DMRAFT_TICK_V=2 -DMRAFT_TICK_MINW=6"
+# Each argument is  tag[@SRCDIR]=DEFINES  e.g.  "w6=-DMRAFT_TICK_MINW=6 -DMRAFT_TICK_CMP_EPL=2"
 # or "head@/tmp/head/multiraft_amd/csrc=" (another source tree, e.g. git archive HEAD).
 # TICK_ONLY=1: recompile only mraft_tick.hip per variant (the rest from build/).
 set -e
