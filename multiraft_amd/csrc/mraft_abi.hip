@@ -551,6 +551,7 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
+  if (entry_terms && n_entry_terms < 0) return fail(MRAFT_E_INVAL, "n_entry_terms < 0");
   if (n == 0) return MRAFT_OK;
   HIP_TRY(hipSetDevice(h->device));
   TRY(ensure_claim(h));
@@ -627,8 +628,8 @@ int mraft_process_append_replies(mraft_engine *h, const mraft_ae_result *items, 
   void *sc;
   TRY(scratch(h, 7, mraft::fold_scan_bytes(n, ns), &sc));
   // three launches: the segment claims with the outputs zeroed, the fold
-  // (which rejects a segment whose slot another one claimed), the a1 scans
-  // its probes left open
+  // (which rejects a segment whose slot another one claimed), the tail (the
+  // segments longer than a lane group, and the a1 scans the probes left open)
   mraft::launch_fold(dev_of(h), (const mraft_ae_result *)it, n, (const int64_t *)sb, ns, gp_of(h), h->claim,
                      h->epoch, (int32_t *)se, (int32_t *)fl, (int32_t *)e, sc, h->stream);
   return sg.finish();

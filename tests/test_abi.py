@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from multiraft_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -68,3 +70,39 @@ def test_persistent_codec_round_trip_host_only():
         except MraftError:
             continue
         raise AssertionError("malformed buffer accepted")
+
+
+@pytest.mark.gpu
+def test_message_calls_reject_bad_arguments_gpu():
+    """The message-path entry points check their arguments before any launch:
+    a negative item count, a null output, a negative entry-word count with a
+    caller buffer, n_seg < 0, a stage capacity outside [0, 2^31) — each
+    MRAFT_E_INVAL with a message, and the engine ticks on afterwards."""
+    import numpy as np
+    from oracle_lib import Oracle, assert_states_equal
+    from multiraft_amd import Engine, synth_tick_state
+    from multiraft_amd._abi import AE_ARGS, AE_REPLY, AE_RESULT, HOST, ptr
+    lib = _abi.lib()
+    G, P, L = 8, 3, 16
+    st, lp, _ = synth_tick_state(G, P, L, seed=7)
+    a, r, err = np.zeros(2, AE_ARGS), np.zeros(2, AE_REPLY), np.zeros(2, np.int32)
+    terms = np.zeros(4, np.int32)
+    res, fl, seg = np.zeros(2, AE_RESULT), np.zeros(2, np.int32), np.zeros(3, np.int64)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        h = e._h
+        assert lib.mraft_handle_append_entries_ex(h, ptr(a), -1, None, 0, ptr(r), None, ptr(err), HOST) == _abi.E_INVAL
+        assert lib.mraft_handle_append_entries_ex(h, ptr(a), 2, None, 0, None, None, ptr(err), HOST) == _abi.E_INVAL
+        assert b"null argument" in lib.mraft_last_error_string()
+        assert lib.mraft_handle_append_entries_ex(h, ptr(a), 2, ptr(terms), -4, ptr(r), None, ptr(err),
+                                                  HOST) == _abi.E_INVAL
+        assert b"n_entry_terms" in lib.mraft_last_error_string()
+        assert lib.mraft_process_append_replies(h, ptr(res), 2, ptr(seg), -1, ptr(fl), ptr(err), HOST) == _abi.E_INVAL
+        assert lib.mraft_process_append_replies(h, ptr(res), -2, None, 0, ptr(fl), ptr(err), HOST) == _abi.E_INVAL
+        assert lib.mraft_set_stage_capacity(h, -1) == _abi.E_INVAL
+        assert lib.mraft_set_stage_capacity(h, 1 << 31) == _abi.E_INVAL
+        assert lib.mraft_get_stage_capacity(h) == 4 << 20  # unchanged default
+        gf = e.replicate_tick(lp)
+        o = Oracle(G, P, L, st)
+        assert np.array_equal(gf, o.replicate_tick(lp))
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "after rejected calls")
