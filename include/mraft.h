@@ -358,7 +358,7 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
 
 /* a4, HandleAppendEntries (raft_append_entry.go:108-162 with matchLog,
  * raft_log.go:92-96) for n items at distinct slots. entry_terms holds the
- * entries' terms (n_entry_terms words; pass NULL to read entries by reference
+ * entries' terms (n_entry_terms >= 0 words; pass NULL to read entries by reference
  * from the engine's own log, as produced by mraft_gather_append_args: every
  * item then sees the log as it was before the call, like the reference's copy
  * of args.Entries at gather time, raft_append_entry.go:50-54). By reference,
