@@ -9,11 +9,14 @@ non-monotone terms), rings started at random heads, against the C oracle:
 * the fused tick, 1 or 2 shards, three ticks with Start() between them;
 * the message path gather -> handle -> fold, entries by reference and by
   value, with and without stale second leaders (deferred and staged items);
+* rings of stale leaders at stage capacities 0 / 64 / default (the ordered
+  fallback and its cycle buffer included);
 * the election storm, the voters' last terms read through the wrap."""
 import numpy as np
 import pytest
 
-from message_cases import all_follower_items, external_entries, results_of, stale_second_leader_state
+from message_cases import (all_follower_items, external_entries, results_of, stale_cycle_state,
+                           stale_second_leader_state)
 from oracle_lib import Oracle, assert_states_equal, rotate_rings
 from random_states import random_tick_state
 
@@ -77,6 +80,32 @@ def test_message_path_odd_capacity_gpu(L, stale, by):
             of, oferr = o.process_append_replies(res, seg)
             assert np.array_equal(f, of) and np.array_equal(ferr, oferr), (L, step)
             assert_states_equal(e.store_state(), o.state(), G, P, L, f"L {L}, {by}, stale {stale}, step {step}")
+
+
+@pytest.mark.parametrize("L", [13, 37, 99])
+@pytest.mark.parametrize("cap", [0, 64, None])
+def test_stale_rings_odd_capacity_gpu(L, cap):
+    """Rings of 2..P stale leaders sending to each other: every item deferred,
+    its entries staged (capacity 64 words or the default) or, with no stage,
+    run in order with each cycle broken through the L-word cycle buffer."""
+    rng = np.random.default_rng(7300 + L + (cap or 1))
+    G, P = 160, 5
+    st, lp, _ = synth_tick_state(G, P, L, seed=7400 + L)
+    st, slots, peers = stale_cycle_state(st, lp, G, P, L, rng, range(1, G, 4), int(rng.integers(2, P + 1)))
+    st = rotate_rings(st, G, P, L, rng, frac=0.8)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        if cap is not None:
+            e.set_stage_capacity(cap)
+        args, gerr = e.gather_append_args(slots, peers)
+        oargs, ogerr = o.gather_append_args(slots, peers)
+        assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr), L
+        ok = gerr == 0
+        rep, herr = e.handle_append_entries(args[ok], None)
+        orep, oherr = o.handle_append_entries(args[ok], None)
+        assert np.array_equal(herr, oherr) and np.array_equal(rep, orep), (L, cap)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"L {L}, stage {cap}")
 
 
 @pytest.mark.parametrize("L", [5, 13, 37])
