@@ -11,13 +11,15 @@ non-monotone terms), rings started at random heads, against the C oracle:
   value, with and without stale second leaders (deferred and staged items);
 * rings of stale leaders at stage capacities 0 / 64 / default (the ordered
   fallback and its cycle buffer included);
-* the election storm, the voters' last terms read through the wrap."""
+* the election storm, the voters' last terms read through the wrap;
+* L = 4k with the log bound 4 B past a 16-B boundary (mraft_bind_state): the
+  same dword forms, chosen by the base address instead of the capacity."""
 import numpy as np
 import pytest
 
 from message_cases import (all_follower_items, external_entries, results_of, stale_cycle_state,
                            stale_second_leader_state)
-from oracle_lib import Oracle, assert_states_equal, rotate_rings
+from oracle_lib import Oracle, assert_states_equal, rotate_rings, terms_sorted_exact
 from random_states import random_tick_state
 
 from multiraft_amd import Engine, synth_election_state, synth_tick_state
@@ -119,3 +121,40 @@ def test_election_storm_odd_capacity_gpu(L):
         for launch in range(2):
             assert np.array_equal(e.election_rounds(mask), o.election_rounds(mask)), (L, launch)
             assert_states_equal(e.store_state(), o.state(), G, P, L, f"L {L}, launch {launch}")
+
+
+@pytest.mark.parametrize("off", [1, 2, 3])
+def test_misaligned_log_base_gpu(off):
+    """A caller-bound state whose log_term starts `off` words past a 16-B
+    boundary: the tick and the by-reference handler cannot use dwordx4 loads
+    on it and take the dword forms; two ticks, then a message step."""
+    import torch
+    from multiraft_amd._abi import DEVICE  # noqa: F401  (device-bound state)
+    rng = np.random.default_rng(6100 + off)
+    G, P, L = 256, 5, 64
+    st, lp = random_tick_state(rng, G, P, L, monotone=True)
+    st = rotate_rings(st, G, P, L, rng, frac=0.8)
+    st["terms_sorted"] = terms_sorted_exact(st, G, P, L).astype(np.int32)  # bind takes the proof as given
+    dev = torch.device("cuda", 0)
+    d = {k: torch.from_numpy(v.copy()).to(dev) for k, v in st.items()}
+    big = torch.zeros(len(st["log_term"]) + 4, dtype=torch.int32, device=dev)
+    big[off:off + len(st["log_term"])] = d["log_term"]
+    d["log_term"] = big[off:off + len(st["log_term"])]
+    assert d["log_term"].data_ptr() % 16 == 4 * off
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L, alloc=False) as e:
+        e.bind(d)
+        for step in range(2):
+            gf = e.replicate_tick(lp)
+            assert np.array_equal(gf, o.replicate_tick(lp)), (off, step)
+        slots, peers = all_follower_items(np.clip(lp, 0, P - 1), G, P)
+        args, gerr = e.gather_append_args(slots, peers)
+        oargs, ogerr = o.gather_append_args(slots, peers)
+        assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr), off
+        ok = gerr == 0
+        rep, herr = e.handle_append_entries(args[ok], None)
+        orep, oherr = o.handle_append_entries(args[ok], None)
+        assert np.array_equal(herr, oherr) and np.array_equal(rep, orep), off
+        e.synchronize()
+    got = {k: v.cpu().numpy() for k, v in d.items()}
+    assert_states_equal(got, o.state(), G, P, L, f"log base +{off} words")
