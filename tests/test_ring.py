@@ -145,10 +145,11 @@ def test_message_path_rotated_gpu(mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,L", [(3, 16), (5, 40), (7, 32)])
+@pytest.mark.parametrize("P,L", [(3, 16), (5, 40), (7, 32), (3, 13), (5, 37), (7, 99)])
 def test_snapshot_and_persistence_rotated_gpu(P, L):
     """Snapshot / InstallSnapshot as ring rebases, then persistence read-out
-    (in Index order across the wrap), restore (head back to 0) and Start."""
+    (in Index order across the wrap), restore (head back to 0) and Start; at
+    capacities that are and are not a multiple of four."""
     from snapshot_cases import run_snapshot_scenario
     G = 300
     rng = np.random.default_rng(4100 + P + L)
