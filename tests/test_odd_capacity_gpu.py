@@ -12,6 +12,7 @@ non-monotone terms), rings started at random heads, against the C oracle:
 * rings of stale leaders at stage capacities 0 / 64 / default (the ordered
   fallback and its cycle buffer included);
 * the election storm, the voters' last terms read through the wrap;
+* the smallest engines (G, P, L down to 1, 1, 1);
 * L = 4k with the log bound 4 B past a 16-B boundary (mraft_bind_state): the
   same dword forms, chosen by the base address instead of the capacity."""
 import numpy as np
@@ -158,3 +159,36 @@ def test_misaligned_log_base_gpu(off):
         e.synchronize()
     got = {k: v.cpu().numpy() for k, v in d.items()}
     assert_states_equal(got, o.state(), G, P, L, f"log base +{off} words")
+
+
+@pytest.mark.parametrize("G,P,L", [(1, 1, 1), (1, 2, 1), (2, 3, 2), (3, 8, 3), (1, 8, 4), (2, 5, 1), (5, 2, 2)])
+def test_tiny_shapes_gpu(G, P, L):
+    """The smallest engines: one group, one peer, a log holding only the dummy
+    entry (every append overflows: MRAFT_ITEM_LOG_FULL), all eight peers on a
+    three-entry ring. Three ticks with Start() between, then a message step."""
+    rng = np.random.default_rng(100 + G * 10 + P + L)
+    st, lp = random_tick_state(rng, G, P, L)
+    st = rotate_rings(st, G, P, L, rng, frac=0.8)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        for step in range(3):
+            assert np.array_equal(e.replicate_tick(lp), o.replicate_tick(lp)), (G, P, L, step)
+            assert_states_equal(e.store_state(), o.state(), G, P, L, f"{G}x{P}x{L}, step {step}")
+            slots = (np.arange(G) * P + np.clip(lp, 0, P - 1)).astype(np.int32)
+            for a, b in zip(e.start(slots, np.ones(G, np.int32)), o.start(slots, np.ones(G, np.int32))):
+                assert np.array_equal(a, b), (G, P, L, step, "start")
+        slots, peers = all_follower_items(np.clip(lp, 0, P - 1), G, P)
+        if len(slots):
+            args, gerr = e.gather_append_args(slots, peers)
+            oargs, ogerr = o.gather_append_args(slots, peers)
+            assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr)
+            ok = gerr == 0
+            rep, herr = e.handle_append_entries(args[ok], None)
+            orep, oherr = o.handle_append_entries(args[ok], None)
+            assert np.array_equal(herr, oherr) and np.array_equal(rep, orep)
+            res, seg = results_of(slots[ok], peers[ok], args[ok], rep, herr, G, P)
+            f, ferr = e.process_append_replies(res, seg)
+            of, oferr = o.process_append_replies(res, seg)
+            assert np.array_equal(f, of) and np.array_equal(ferr, oferr)
+        assert_states_equal(e.store_state(), o.state(), G, P, L, f"{G}x{P}x{L}, message step")
