@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5 GPU pass, parametrised: TAG names the output directory
-# (gpurun_out/$TAG); DO lists what to run (tests bench pmc valu elect cmp trace smoke ...).
+# (gpurun_out/$TAG); DO lists what to run (tests bench pmc valu elect cmp tlb trace smoke ...).
 #   TESTS   pytest selection (-k expression) for the tests step ("" = all -m gpu)
 #   BENCH   extra bench.py arguments
 set -uo pipefail
@@ -117,6 +117,20 @@ for st in ${DO:-tests bench}; do
       done
       python3 tools/pmc_kernels.py "$OUT/cmp_counters.json" "$OUT"/cmp[0-9]* --kernels "k_tick_group<5, false>;k_handle_set<4, 0>;k_handle_deferred;k_gather_args;k_claim_ae" > /dev/null
       python3 tools/cmp_summary.py "$OUT" "$OUT/cmp_summary.json" | head -60 ;;
+    tlb)
+      # address-translation counters of the message path's kernels: are the gather's and the
+      # fold's dependent round trips stretched by UTCL1 misses? k_handle_set
+      # (row streams) is the comparison
+      echo "== tlb"
+      i=0
+      for grp in "TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE" \
+                 "TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_PENDING_STALL_CYCLES_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum"; do
+        i=$((i+1))
+        SHARDS=1 timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/tlb$i" -o t -- python3 tools/ab_message_path.py \
+          > "$OUT/tlb$i.json" 2> "$OUT/tlb$i.err" || { tail -5 "$OUT/tlb$i.err"; exit 1; }
+      done
+      python3 tools/pmc_kernels.py "$OUT/tlb_counters.json" "$OUT"/tlb1 "$OUT"/tlb2 \
+        --kernels "k_gather_args;k_fold<5>;k_handle_set<4, 0>;k_claim_zero;k_claim_ae;k_fold_tail<5>" | head -80 ;;
     ctest)
       echo "== ctest"
       make -s -C tests/c_host && timeout -k 10 120 tests/c_host/mraft_host_tick tests/golden/tick_vectors.bin 0 | tee "$OUT/c_host.txt" ;;
