@@ -1209,11 +1209,9 @@ def main():
             log(rank, f"config #4 on one GPU, {sk} shard(s): {c['ms_per_step']:.4f} ms/step, device "
                       f"{c['roofline']['kernel_ms_mean']:.4f} ms ({c['roofline']['frac']:.3f} of 8 TB/s) over "
                       f"{c4['steps']} fresh copies")
-    if rank == 0 and not args.no_cpu_baseline:
-        # rank 0 only (the other ranks wait at the barrier below); a shorter
-        # sample with more than one rank
-        budget = args.cpu_seconds if world == 1 else min(args.cpu_seconds, 6.0)
-        out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, budget, rank)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # at N = 1 only (the driver's N > 1 lines carry cpu_baseline null)
+        out["cpu_baseline"] = cpu_baseline(G_total, P, L, seed, args.cpu_seconds, rank)
     if rank == 0:
         print(json.dumps(out), file=result_out, flush=True)
     if dist_on:
