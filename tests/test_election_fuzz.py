@@ -21,7 +21,7 @@ def test_election_storm_fuzz_gpu(seed):
     rng = np.random.default_rng(9100 + seed)
     P = 1 + seed % 8
     G = int(rng.integers(100, 1500))
-    L = int(rng.choice([8, 16, 64]))
+    L = int(rng.choice([8, 13, 16, 64]))
     R = int(rng.integers(1, 97))
     st, mask = synth_election_state(G, P, L, seed=9300 + seed, rounds=R)
     if seed % 3 == 1:

@@ -23,10 +23,10 @@ def test_fold_fuzz_gpu(seed):
     P = int(rng.choice([2, 3, 5, 7, 8]))
     max_len = int(rng.choice([8, 40, 150]))
     if seed % 2:
-        G, L = int(rng.integers(64, 400)), int(rng.choice([64, 128]))
+        G, L = int(rng.integers(64, 400)), int(rng.choice([64, 65, 128]))
         st, lp = random_tick_state(rng, G, P, L, monotone=bool(rng.random() < 0.5))
     else:
-        G, L = int(rng.choice([256, 1024])), int(rng.choice([128, 512]))
+        G, L = int(rng.choice([256, 1024])), int(rng.choice([128, 131, 512]))
         st, lp, _ = synth_tick_state(G, P, L, seed=5700 + seed)
     if rng.random() < 0.6:
         st = rotate_rings(st, G, P, L, rng, frac=0.8)

@@ -32,7 +32,7 @@ def _case(seed):
     rng = np.random.default_rng(1000 + seed)
     G = int(rng.choice([64, 128, 192]))
     P = int(rng.choice([3, 5, 7]))
-    L = int(rng.choice([64, 128, 256]))
+    L = int(rng.choice([64, 77, 128, 141, 256]))
     st, lp, _ = synth_tick_state(G, P, L, seed=4242 + seed)
     kind = seed % 3
     if kind == 0:

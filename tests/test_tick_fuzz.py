@@ -5,7 +5,8 @@ InstallSnapshot branch :27-34 and raft_snapshot.go:15-69) against the C
 oracle: seeded random states (tests/random_states.py: diverging follower
 tails, snapshot-heavy variants, monotone and non-monotone term sequences,
 bad-state leaders), rings started at random heads, the tick as 1, 2 or 3
-engine-owned shards, and between ticks Start() on random leaders
+engine-owned shards, log capacities with and without L % 4 == 0 (the
+passes' dwordx4 and dword forms), and between ticks Start() on random leaders
 (raft.go:90-104) and leader changes — four ticks per case, every group flag
 and the whole state equal to the oracle's after each."""
 import numpy as np
@@ -23,7 +24,7 @@ pytestmark = pytest.mark.gpu
 def test_tick_multistep_fuzz_gpu(seed):
     rng = np.random.default_rng(7700 + seed)
     P = int(rng.choice([3, 5, 7]))
-    L = int(rng.choice([32, 64, 128, 256]))
+    L = int(rng.choice([32, 37, 64, 99, 128, 256]))
     G = int(rng.integers(150, 500))
     st, lp = random_tick_state(rng, G, P, L, monotone=bool(rng.random() < 0.5), snap=bool(rng.random() < 0.3))
     if rng.random() < 0.7:
