@@ -13,7 +13,9 @@ not: its dwordx4 and dword forms, include/mraft.h log layout):
 * by value: the same items' entries copied into a caller buffer at
   misaligned positions.
 
-Each case: replies, item errors and the whole state equal the oracle's."""
+Group sizes P = 2..8 (one to seven messages per set) and log capacities with
+and without L % 4 == 0. Each case: replies, item errors and the whole state
+equal the oracle's."""
 import numpy as np
 import pytest
 
@@ -31,7 +33,7 @@ SEEDS = list(range(40))
 def _case(seed):
     rng = np.random.default_rng(1000 + seed)
     G = int(rng.choice([64, 128, 192]))
-    P = int(rng.choice([3, 5, 7]))
+    P = int(rng.choice([2, 3, 5, 7, 8]))
     L = int(rng.choice([64, 77, 128, 141, 256]))
     st, lp, _ = synth_tick_state(G, P, L, seed=4242 + seed)
     kind = seed % 3

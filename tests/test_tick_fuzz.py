@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("seed", list(range(48)))
 def test_tick_multistep_fuzz_gpu(seed):
     rng = np.random.default_rng(7700 + seed)
-    P = int(rng.choice([3, 5, 7]))
+    P = int(rng.choice([2, 3, 5, 7, 8]))
     L = int(rng.choice([32, 37, 64, 99, 128, 256]))
     G = int(rng.integers(150, 500))
     st, lp = random_tick_state(rng, G, P, L, monotone=bool(rng.random() < 0.5), snap=bool(rng.random() < 0.3))
