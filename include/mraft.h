@@ -18,7 +18,13 @@
  *    (or per-group) error/flag array and left unmodified; the CPU oracle flags
  *    the same items.
  *  - All integers are int32 on the device. Go's `int` is 64-bit; values must be
- *    in [-1, 2^31) and the engine rejects nothing silently.
+ *    in [-1, 2^31) and the engine rejects nothing silently. Raft Indexes
+ *    (dummy, last, commit, matchIndex, an AppendEntries' last entry
+ *    prevLogIndex + len(Entries)) are at most 2^31 - 2, so that nextIndex =
+ *    Index + 1 is an int32: an AppendEntries past that is malformed
+ *    (MRAFT_ITEM_BAD_SLOT) and a Start past it MRAFT_ITEM_LOG_FULL. Every
+ *    Index up to that bound is handled exactly (the streaming
+ *    pass runs on Indexes relative to its first one).
  *  - The engine owns its device state (hipMalloc) unless created with
  *    MRAFT_CREATE_NO_ALLOC and bound to caller-owned device buffers with
  *    mraft_bind_state(). Batch buffers belong to the caller and are read/written
@@ -55,6 +61,10 @@ extern "C" {
 #endif
 
 #define MRAFT_ABI_VERSION 5
+
+/* Largest log capacity L (entries per replica ring): ring offsets are formed
+ * as 32-bit byte offsets (4 * (position + 32) < 2^32). */
+#define MRAFT_MAX_LOG_CAPACITY ((1 << 30) - 64)
 
 /* Node states, raft_rpc.go:8-12 (values preserved). */
 enum { MRAFT_LEADER = 1, MRAFT_CANDIDATE = 2, MRAFT_FOLLOWER = 3 };
@@ -308,20 +318,22 @@ typedef struct mraft_engine mraft_engine;
 /* Replaces Make (raft.go:51-87) for G groups x P peers at once: allocates the
  * device SoA (unless MRAFT_CREATE_NO_ALLOC) and initialises every slot as Make
  * does: Follower, term 0, votedFor -1, dummy entry {0,0}, commit = lastApplied
- * = dummyIndex. peers in [1, 8]; log_capacity >= 1. */
+ * = dummyIndex. peers in [1, 8]; log_capacity in [1, MRAFT_MAX_LOG_CAPACITY]. */
 int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity,
                  int32_t device, uint32_t flags, mraft_engine **out);
 /* Replaces Kill (utility.go:9-19): waits for the engine's queues, frees device
  * state and every stream / queue the engine created. */
 int mraft_destroy(mraft_engine *h);
 /* Use a caller-provided hipStream_t (NULL = the engine's own stream); tick
- * shard launches still outstanding are ordered before the new stream's work. */
+ * shard launches still outstanding and the work already on the old stream are
+ * ordered before the new stream's work (device-side waits). */
 int mraft_set_stream(mraft_engine *h, void *hip_stream);
 /* The engine stream. With tick shards (mraft_set_tick_shards) a tick's
  * launches run on the shard queues; this call first orders the engine stream
  * after every outstanding shard launch (a device-side wait, no host wait), so
  * work the caller enqueues on the returned stream — a copy of group_flags or
- * of the export words, an event — sees the tick's outputs. */
+ * of the export words, an event — sees the tick's outputs. NULL when the
+ * handle is null or that ordering fails (mraft_last_error_string). */
 void *mraft_get_stream(mraft_engine *h);
 /* Host wait for all work of the handle (engine stream and tick shards). */
 int mraft_synchronize(mraft_engine *h);
@@ -368,7 +380,9 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * after the others (deferred), from a staged copy of its entries when its
  * source row is written in this call too. Every count this takes stays on the
  * device: with MRAFT_DEVICE the call enqueues its launches and returns without
- * waiting (calls may be enqueued back to back with no host synchronisation).
+ * waiting (calls may be enqueued back to back with no host synchronisation;
+ * a batch larger than any before grows the engine's buffers in stream order,
+ * without waiting either). n <= 2^31 - 1.
  * Staged entries use the engine's stage (mraft_set_stage_capacity); a batch
  * that needs more runs its deferred items in an order that needs no stage (one
  * wave, slower), with the same results. */
@@ -395,7 +409,8 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args,
 /* Capacity, in entry words, of the device stage mraft_handle_append_entries
  * copies the entries of deferred by-reference items into (default 4 Mi words,
  * 16 MiB; allocated on first use). A batch needing more is still handled
- * exactly, in the ordered fallback. words in [0, 2^31). Returns MRAFT_OK;
+ * exactly, in the ordered fallback (as is every batch when the stage cannot
+ * be allocated). words in [0, 2^31). Returns MRAFT_OK;
  * mraft_get_stage_capacity returns the current capacity (-1: null handle). */
 int mraft_set_stage_capacity(mraft_engine *h, int64_t words);
 int64_t mraft_get_stage_capacity(const mraft_engine *h);

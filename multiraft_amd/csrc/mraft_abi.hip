@@ -217,7 +217,21 @@ int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, in
   return MRAFT_OK;
 }
 
-// Grow-only device scratch slot `idx`.
+// Device memory in stream order on the engine stream (hipMallocAsync /
+// hipFreeAsync): allocating or growing a buffer never waits for the device, so
+// MRAFT_DEVICE calls stay asynchronous when a batch is larger than any before
+// (include/mraft.h). A freed buffer is released after the
+// work already enqueued on the stream, which may still read it.
+int alloc_async(mraft_engine *h, void **p, size_t bytes, const char *what) {
+  *p = nullptr;
+  if (hipMallocAsync(p, bytes, h->stream) != hipSuccess || !*p) {
+    (void)hipGetLastError();
+    return fail(MRAFT_E_NOMEM, "%s: device allocation of %zu B failed", what, bytes);
+  }
+  return MRAFT_OK;
+}
+
+// Grow-only device scratch slot `idx` (stream-ordered: no host wait).
 int scratch(mraft_engine *h, size_t idx, size_t bytes, void **out) {
   if (h->scratch_ptr.size() <= idx) {
     h->scratch_ptr.resize(idx + 1, nullptr);
@@ -225,14 +239,11 @@ int scratch(mraft_engine *h, size_t idx, size_t bytes, void **out) {
   }
   if (bytes == 0) bytes = 16;
   if (h->scratch_cap[idx] < bytes) {
-    if (h->scratch_ptr[idx]) {
-      HIP_TRY(hipStreamSynchronize(h->stream));
-      HIP_TRY(hipFree(h->scratch_ptr[idx]));
-    }
+    if (h->scratch_ptr[idx]) HIP_TRY(hipFreeAsync(h->scratch_ptr[idx], h->stream));
     h->scratch_ptr[idx] = nullptr;
     h->scratch_cap[idx] = 0;
     void *p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return fail(MRAFT_E_NOMEM, "scratch alloc of %zu B failed", bytes);
+    TRY(alloc_async(h, &p, bytes, "scratch"));
     h->scratch_ptr[idx] = p;
     h->scratch_cap[idx] = bytes;
   }
@@ -276,10 +287,12 @@ struct Stage {
 int ensure_claim(mraft_engine *h) {
   if (!h->claim) {
     size_t b = (size_t)gp_of(h) * sizeof(unsigned long long);
-    if (hipMalloc(&h->claim, b) != hipSuccess) return fail(MRAFT_E_NOMEM, "claim alloc failed");
+    void *c = nullptr, *m = nullptr;
+    TRY(alloc_async(h, &c, b, "claim"));
+    h->claim = (unsigned long long *)c;
     HIP_TRY(hipMemsetAsync(h->claim, 0, b, h->stream));
-    if (hipMalloc(&h->srcmark, (size_t)gp_of(h) * sizeof(uint32_t)) != hipSuccess)
-      return fail(MRAFT_E_NOMEM, "srcmark alloc failed");
+    TRY(alloc_async(h, &m, (size_t)gp_of(h) * sizeof(uint32_t), "srcmark"));
+    h->srcmark = (uint32_t *)m;
     HIP_TRY(hipMemsetAsync(h->srcmark, 0, (size_t)gp_of(h) * sizeof(uint32_t), h->stream));
   }
   if (++h->epoch == 0) {  // wrapped: reset
@@ -312,9 +325,9 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
                  uint32_t flags, mraft_engine **out) {
   if (!out) return fail(MRAFT_E_INVAL, "out is null");
   *out = nullptr;
-  if (groups < 1 || peers < 1 || peers > 8 || log_capacity < 1)
-    return fail(MRAFT_E_INVAL, "bad dims G=%d P=%d L=%d (need G>=1, 1<=P<=8, L>=1)", groups, peers,
-                log_capacity);
+  if (groups < 1 || peers < 1 || peers > 8 || log_capacity < 1 || log_capacity > MRAFT_MAX_LOG_CAPACITY)
+    return fail(MRAFT_E_INVAL, "bad dims G=%d P=%d L=%d (need G>=1, 1<=P<=8, 1<=L<=%d)", groups, peers,
+                log_capacity, MRAFT_MAX_LOG_CAPACITY);
   if ((int64_t)groups * peers > INT32_MAX)
     return fail(MRAFT_E_INVAL, "G*P must fit in int32");
   HIP_TRY(hipSetDevice(device));
@@ -366,11 +379,12 @@ int mraft_destroy(mraft_engine *h) {
   (void)hipSetDevice(h->device);
   drain(h);
   free_owned(h);
+  // stream-ordered buffers (alloc_async): freed on the engine stream, then waited for
   for (void *p : h->scratch_ptr)
-    if (p) (void)hipFree(p);
-  if (h->claim) (void)hipFree(h->claim);
-  if (h->srcmark) (void)hipFree(h->srcmark);
-  if (h->ae_total) (void)hipFree(h->ae_total);
+    if (p) (void)hipFreeAsync(p, h->stream);
+  for (void *p : {(void *)h->claim, (void *)h->srcmark, (void *)h->ae_total})
+    if (p) (void)hipFreeAsync(p, h->stream);
+  (void)hipStreamSynchronize(h->stream);
   if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
   if (h->fanin_masked) (void)hipStreamSynchronize(h->fanin_masked);
   destroy_shard_queues(h);
@@ -384,19 +398,39 @@ int mraft_destroy(mraft_engine *h) {
 
 int mraft_set_stream(mraft_engine *h, void *stream) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
-  h->stream = stream ? (hipStream_t)stream : (h->tick_masked ? h->tick_masked : h->own_stream);
-  // outstanding shard ticks are ordered before the new stream's work
-  return join_shards(h);
+  HIP_TRY(hipSetDevice(h->device));
+  const hipStream_t ns = stream ? (hipStream_t)stream : (h->tick_masked ? h->tick_masked : h->own_stream);
+  // outstanding shard ticks, then everything on the old stream (the engine's
+  // stream-ordered buffers may still be in use there), are ordered before the
+  // new stream's work: device-side waits, no host wait
+  TRY(join_shards(h));
+  if (ns != h->stream) {
+    hipEvent_t ev = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e1 = hipEventRecord(ev, h->stream);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(ns, ev, 0) : e1;
+    (void)hipEventDestroy(ev);  // released once the wait is satisfied
+    if (e2 != hipSuccess) return fail(MRAFT_E_HIP, "ordering the new stream: %s", hipGetErrorString(e2));
+  }
+  h->stream = ns;
+  return MRAFT_OK;
 }
 
 // With tick shards, the engine stream is first ordered after the outstanding
 // shard launches (a device-side wait), so work the caller puts on the returned
-// stream sees the tick's outputs.
+// stream sees the tick's outputs. NULL when that ordering fails
+// (mraft_last_error_string says why): the stream would not see the outputs.
 void *mraft_get_stream(mraft_engine *h) {
-  if (!h) return nullptr;
+  if (!h) {
+    fail(MRAFT_E_INVAL, "null engine handle");
+    return nullptr;
+  }
   if (h->shards_pending) {
-    (void)hipSetDevice(h->device);
-    (void)join_shards(h);
+    if (hipSetDevice(h->device) != hipSuccess) {
+      fail(MRAFT_E_HIP, "hipSetDevice failed");
+      return nullptr;
+    }
+    if (join_shards(h) != MRAFT_OK) return nullptr;
   }
   return (void *)h->stream;
 }
@@ -551,6 +585,8 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   TRY(enter(h));
   if (n < 0 || (n > 0 && (!args || !replies || !item_err)))
     return fail(MRAFT_E_INVAL, "null argument");
+  // item indices are 32-bit in the claims and the ordered fallback
+  if (n > INT32_MAX) return fail(MRAFT_E_INVAL, "n = %lld items exceeds 2^31 - 1", (long long)n);
   if (entry_terms && n_entry_terms < 0) return fail(MRAFT_E_INVAL, "n_entry_terms < 0");
   if (n == 0) return MRAFT_OK;
   HIP_TRY(hipSetDevice(h->device));
@@ -575,9 +611,10 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   // they need stays on the device, nothing waits on the host (mraft_kernels.hip
   // "a4" for the rules).
   if (!h->ae_total) {
-    if (hipMalloc(&h->ae_total, 2 * sizeof(unsigned long long)) != hipSuccess)
-      return fail(MRAFT_E_NOMEM, "AppendEntries counters alloc failed");
-    HIP_TRY(hipMemsetAsync(h->ae_total, 0, 2 * sizeof(unsigned long long), h->stream));
+    void *t = nullptr;
+    TRY(alloc_async(h, &t, 4 * sizeof(unsigned long long), "AppendEntries counters"));
+    h->ae_total = (unsigned long long *)t;
+    HIP_TRY(hipMemsetAsync(h->ae_total, 0, 4 * sizeof(unsigned long long), h->stream));
   }
   void *sethd, *soff, *defer, *order, *stage = nullptr;
   TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
@@ -585,7 +622,9 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
   // the ordered fallback's in-degrees and queue (n each) and cycle buffer (L)
   TRY(scratch(h, 19, sizeof(int32_t) * (2 * (size_t)n + (size_t)h->L), &order));
-  if (h->stage_cap > 0) TRY(scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage));
+  // the stage: when it cannot be allocated the batch runs with none (every
+  // staged item then takes the ordered fallback: the same results, slower)
+  if (h->stage_cap > 0 && scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage) != MRAFT_OK) stage = nullptr;
   const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
   const int64_t n_log = gp_of(h) * h->L;
   int32_t *kin = (int32_t *)order, *kq = kin + n, *cyc = kq + n;

@@ -205,12 +205,19 @@ __device__ __forceinline__ bool ae_ref_ok(const mraft_ae_args &a, int64_t n_log,
            a.entries_offset % L + a.n_entries > L);
 }
 
+// The Index domain (include/mraft.h): the last entry's Index prev + n must
+// leave room for nextIndex = Index + 1 in int32. Outside it the item is
+// malformed (MRAFT_ITEM_BAD_SLOT), as in the oracle.
+__device__ __forceinline__ bool ae_index_ok(const mraft_ae_args &a) {
+  return (int64_t)a.prev_log_index + a.n_entries <= (int64_t)INT32_MAX - 1;
+}
+
 __device__ __forceinline__ unsigned long long claim_tag(uint32_t epoch, int64_t i) {
   return ((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i);
 }
 
 __device__ __forceinline__ AeKey ae_key(const mraft_ae_args &a, int64_t gp, int64_t n_log, int L) {
-  if (a.slot < 0 || a.slot >= gp || !ae_ref_ok(a, n_log, L)) return AeKey{-1, 0, 0};
+  if (a.slot < 0 || a.slot >= gp || !ae_ref_ok(a, n_log, L) || !ae_index_ok(a)) return AeKey{-1, 0, 0};
   return AeKey{a.entries_offset / L, (int)(a.entries_offset % L) - (a.prev_log_index + 1),
                a.prev_log_index + a.n_entries};
 }
@@ -447,14 +454,18 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   // whether the item runs here: no extra dependent round trip)
   int fterm = 0, fdummy = 0, flast = 0, fc = 0, fhead = 0;
   if (!e) { fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fc = s.commit[f]; fhead = s.head[f]; }
-  // Where the entries are: Index x of this lane's message at src.at(x).
-  RingRow src{k0.ent0, 0, 0, INT32_MAX};
+  // Where the entries are: Index x of this lane's message at src.at(x). A
+  // flat source (host buffer, staged copy, cycle buffer) is built relative to
+  // its first entry (row = that entry's word, base = -(prev + 1)), so at()'s
+  // 32-bit lane offset is x - (prev + 1), small whatever the Raft Index
+  // (flat_src; an absolute Index above 2^30 wrapped it).
+  RingRow src = flat_src(k0.ent0, 0, prev);
   int64_t n_ent = k0.n_ent0;
   bool ok = true, dup = false, dfr = false, stg = false;
   int64_t srow = 0;  // by reference: the source row
   int rhead = 0;
   if (MODE == HM_HOST) {
-    if (!e) src.row = a.entries_offset - (prev + 1);
+    if (!e) src = flat_src(k0.ent0, a.entries_offset, prev);
   } else if (!e) {
     ok = ae_ref_ok(a, gp * L, L);
     srow = ok ? a.entries_offset / L : 0;
@@ -473,9 +484,8 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     }
     const int64_t so = MODE == HM_MAIN ? -2 : so0;
     if (so >= 0) {  // staged copy (or the fallback's cycle buffer)
-      src.p = k0.stage;
+      src = flat_src(k0.stage, so, prev);
       n_ent = k0.stage_cap;  // (HM_ORDER: the cycle buffer, capacity L)
-      src.row = so - (prev + 1);
       a.entries_offset = so;
     } else {        // in place through the source ring
       src.p = s.log;
@@ -488,7 +498,7 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   int cls = e ? AE_NONE : AE_DONE;
   if (dup) cls = AE_NONE;
   else if (dfr) cls = AE_DEFER;
-  else if (!e && (!ok || nn < 0 || a.entries_offset < 0 ||
+  else if (!e && (!ok || nn < 0 || a.entries_offset < 0 || !ae_index_ok(a) ||
                   (nn > 0 && src.L == INT32_MAX && a.entries_offset + nn > n_ent)))
     cls = AE_BAD;
   const bool live = cls == AE_DONE;
@@ -507,12 +517,10 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   // MRAFT_AE_ENTRIES_SORTED is the sender's claim (it crosses the network):
   // honoured only where the terms prevLogTerm, entry 0, ... really never
   // decrease. Here the first step (prevLogTerm <= entry 0, in the round trip
-  // of the follower's log[prev]; a flat source addressed in 64 bits, whatever
-  // the Index); the entries themselves are checked on the pass's loads
-  // (DescTrack). Same rule in the oracle (ae_flag_holds).
+  // of the follower's log[prev]); the entries themselves are checked on the
+  // pass's loads (DescTrack). Same rule in the oracle (ae_flag_holds).
   const bool claim = live && nn > 0 && (a.flags & MRAFT_AE_ENTRIES_SORTED) != 0;
-  const bool claim0 =
-      claim && a.prev_log_term <= (src.L == INT32_MAX ? src.p[src.row + prev + 1] : *src.at(prev + 1));
+  const bool claim0 = claim && a.prev_log_term <= *src.at(prev + 1);
   mraft_ae_reply r = {0, 0, 0, 0};
   int ftp = 0;
   if (live) {
@@ -549,8 +557,9 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   const int merge_m = (int)(__ballot(cls == AE_MERGE) & ((1ull << NI) - 1));
   // terms_sorted after an append from Index k (include/mraft.h): the args'
   // flag when k - 1 is the dummy, cleared without it, else unchanged — the
-  // flag as checked (claim0 here, the entries' descents after the pass)
-  int shint = claim0 ? fdummy + 1 : -1;
+  // flag as checked (claim0 here, the entries' descents after the pass);
+  // shint: -1 no flag, 1 flag and prev is the dummy, 0 flag otherwise
+  int shint = claim0 ? (prev == fdummy ? 1 : 0) : -1;
   if (merge_m) {
     Fol<NI, true> fo;
     fo.log = s.log;
@@ -561,11 +570,18 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     fo.copy = 0;
     fo.capok = (int)(__ballot(cls == AE_MERGE && (int64_t)prev + nn - fdummy <= (int64_t)L - 1) & ((1ull << NI) - 1));
     fo.full = 0;
-    const int phi = uni(__shfl(prev + nn, first_lane((unsigned long long)merge_m), 64)), nend = phi + 1;
+    const int phi = uni(__shfl(prev + nn, first_lane((unsigned long long)merge_m), 64));
     int plo = phi + 1;
 #pragma unroll
     for (int q = 0; q < NI; ++q)
       if ((merge_m >> q) & 1) plo = min(plo, uni(__shfl(prev, q, 64)) + 1);
+    // The pass runs on Indexes relative to B = plo - kPassBias (pass_bias):
+    // every Index it forms stays in [kPassBias - 35, kPassBias + L + 256], so
+    // no chunk end (c + 256) overflows int32 near 2^31 and the lane offsets a
+    // source's at() forms stay small. Rows see the same words (their bases
+    // absorb B).
+    const int B = pass_bias(plo);
+    const int pl = plo - B, ph = phi - B, nend = ph + 1;
     // the source as the first merging message sees it (the same for every message of a set)
     const int q0 = first_lane((unsigned long long)merge_m);
     RingRow ss;
@@ -576,29 +592,22 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
       const uint64_t ra = (uint64_t)src.row;
       const uint32_t rlo = (uint32_t)__shfl((int)(uint32_t)ra, q0, 64), rhi = (uint32_t)__shfl((int)(ra >> 32), q0, 64);
       ss.row = (long long)(((uint64_t)uni((int)rhi) << 32) | (uint32_t)uni((int)rlo));
-      ss.base = uni(__shfl(src.base, q0, 64));
+      ss.base = uni(__shfl(src.base, q0, 64)) + B;
       ss.L = uni(__shfl(src.L, q0, 64));
-    }
-    // A flat source (host buffer or staged copy) is addressed from the pass's
-    // first Index: the lane offset at_u forms is then Index - plo >= -3 for
-    // every lane that loads (32-bit byte offsets stay small whatever the Raft
-    // Index; with the absolute Index they would wrap past 2^30).
-    if (ss.L == INT32_MAX) {
-      ss.row += (long long)ss.base + plo;
-      ss.base = -plo;
     }
     bool vec = (L & 3) == 0 && ((uintptr_t)s.log & 15) == 0;
 #pragma unroll
     for (int q = 0; q < NI; ++q) {
       fo.slot[q] = uni(__shfl(f, q, 64));
       const int sp = uni(__shfl(prev, q, 64)), sl = uni(__shfl(flast, q, 64));
-      fo.base[q] = uni(__shfl(fhead - fdummy, q, 64));
-      fo.start[q] = sp + 1;
-      fo.cend[q] = min(phi, sl) + 1;
-      fo.cfrom[q] = 0;
-      if ((merge_m >> q) & 1) {
+      fo.base[q] = 0; fo.start[q] = 0; fo.cend[q] = 0;
+      fo.cfrom[q] = 0;  // 0: no mismatch (a relative Index is >= kPassBias - 35 > 0)
+      if ((merge_m >> q) & 1) {  // (only merging messages are ever addressed)
+        fo.base[q] = uni(__shfl(fhead - fdummy, q, 64)) + B;
+        fo.start[q] = sp + 1 - B;
+        fo.cend[q] = min(phi, sl) + 1 - B;
         // dwordx4 when the entries and this follower's row are 16-B aligned alike
-        vec = vec && ((((uintptr_t)ss.at(sp + 1) ^ (uintptr_t)fo.at(q, sp + 1)) & 15) == 0);
+        vec = vec && ((((uintptr_t)ss.at(fo.start[q]) ^ (uintptr_t)fo.at(q, fo.start[q])) & 15) == 0);
       }
     }
     if (ss.L == INT32_MAX) {  // a flat buffer: every dwordx4 read must stay inside it
@@ -608,8 +617,8 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
       const uint64_t nb = (uint64_t)n_ent;
       const uint32_t nlo = (uint32_t)__shfl((int)(uint32_t)nb, q0, 64), nhi = (uint32_t)__shfl((int)(nb >> 32), q0, 64);
       const int64_t sn = (int64_t)(((uint64_t)uni((int)nhi) << 32) | (uint32_t)uni((int)nlo));
-      vec = vec && (((uintptr_t)ss.at(plo)) & ~(uintptr_t)15) >= (uintptr_t)ss.p &&
-            (((uintptr_t)ss.at(phi)) | 15) < (uintptr_t)(ss.p + sn);
+      vec = vec && (((uintptr_t)ss.at(pl)) & ~(uintptr_t)15) >= (uintptr_t)ss.p &&
+            (((uintptr_t)ss.at(ph)) | 15) < (uintptr_t)(ss.p + sn);
     }
     // the pass is wave-wide (ballots, shuffles): one choice for every lane
     vec = __ballot(!vec) == 0;
@@ -628,13 +637,13 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     stash[11][lane] = shint;
     asm volatile("" ::: "memory");
     if (vec) {
-      int c = plo - (int)(((uintptr_t)ss.at(plo) >> 2) & 31);          // 128-B aligned chunks
-      if (c <= phi && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
-      copy_loop<true, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
+      int c = pl - (int)(((uintptr_t)ss.at(pl) >> 2) & 31);            // 128-B aligned chunks
+      if (c <= ph && fo.cmp) c = pass_pipe<false>(ss, fo, nend, 1, 0, 0, found, c, pl, ph, dt);
+      copy_loop<true, false>(ss, fo, c, nend, pl, ph, 1, 0, 0, found, dt);
     } else {
-      int c = plo;
-      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, plo, phi, dt);
-      copy_loop<false, false>(ss, fo, c, nend, plo, phi, 1, 0, 0, found, dt);
+      int c = pl;
+      for (; c <= ph && fo.cmp; c += 256) pass_chunk<1, false, false>(ss, fo, nend, 1, 0, 0, found, c, pl, ph, dt);
+      copy_loop<false, false>(ss, fo, c, nend, pl, ph, 1, 0, 0, found, dt);
     }
     asm volatile("" ::: "memory");
     cls = stash[0][lane]; f = stash[1][lane]; fterm = stash[2][lane]; flast = stash[3][lane];
@@ -660,7 +669,9 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
           // a descent among this message's entries (Index start+1 .. phi)
           // voids its flag
           if (dt.last > fo.start[q]) shint = -1;
-          srt_new = shint < 0 ? 0 : (fo.cfrom[q] == shint ? 1 : -1);
+          // appended from the dummy's successor (prev == dummy, first mismatch
+          // at start): the entries are the whole log
+          srt_new = shint < 0 ? 0 : (shint == 1 && fo.cfrom[q] == fo.start[q] ? 1 : -1);
         }
         if (a.leader_commit > fc) fcommit_new = min(a.leader_commit, last_after);  // :157-160
         r.term = a.term; r.success = 1;                                // :161
@@ -1366,7 +1377,7 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
       err[i] = MRAFT_ITEM_BAD_SLOT;
     } else if (s.role[sl] == kLeader) {                                // raft.go:93-95
       const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl], h = s.head[sl];
-      if ((int64_t)last + k - dummy > (int64_t)s.L - 1) {
+      if ((int64_t)last + k - dummy > (int64_t)s.L - 1 || (int64_t)last + k > (int64_t)INT32_MAX - 1) {
         err[i] = MRAFT_ITEM_LOG_FULL;
       } else {
         // terms_sorted: k entries of currentTerm after the last one
@@ -2050,3 +2061,4 @@ void launch_export(const Dev &s, const int32_t *lpeer, int32_t *commit, int32_t 
 
 }  // namespace mraft
 
+MRAFT_BOUNDS_READER(mraft_debug_bounds_kernels)

@@ -20,10 +20,34 @@ enum : int { M_CMP = 0, M_COPY = 1, M_DONE = 2 };  // a follower's state in the 
 // dwordx4 group that holds the first entry of a range may begin up to 3
 // entries before it (a flat entries buffer indexed from its first Index: k < 0
 // there while the address is inside the buffer).
+// The offset wraps for k >= 2^30 - 32: capacities are capped below that
+// (MRAFT_MAX_LOG_CAPACITY), flat sources are built relative to their first
+// entry (flat_src) and the pass runs on rebased Indexes (pass_bias), so every
+// k formed is within a row length (plus a chunk) of 0. MRAFT_DEBUG_BOUNDS
+// builds count every dereferenced k outside [-32, 2^30 - 32) instead of
+// trusting that (bounds_note; read with mraft_debug_bounds_violations).
+#ifndef MRAFT_DEBUG_BOUNDS
+#define MRAFT_DEBUG_BOUNDS 0
+#endif
+#if MRAFT_DEBUG_BOUNDS
+__device__ unsigned long long g_bounds_violations;
+__device__ __forceinline__ void bounds_note(long long k) {
+  if (k < -32 || k >= (1ll << 30) - 32) atomicAdd(&g_bounds_violations, 1ull);
+}
+#else
+__device__ __forceinline__ void bounds_note(long long) {}
+#endif
 template <class T>
 __device__ __forceinline__ T *at_u(T *base, int k) {
   return reinterpret_cast<T *>(reinterpret_cast<char *>(const_cast<int32_t *>(base - 32)) + (uint32_t)(k + 32) * 4u);
 }
+
+// Indexes inside the pass are relative to B = pass_bias(plo) (plo: the pass's
+// first Index), so they lie in [kPassBias - 35, kPassBias + L + 256]: a chunk
+// end c + 256 cannot overflow int32 however close the Raft Index is to 2^31,
+// and 0 stays free as "no Index" (Fol::cfrom). Rows absorb B in their bases.
+constexpr int kPassBias = 64;
+__device__ __forceinline__ int pass_bias(int plo) { return plo - kPassBias; }
 
 // Where the term of Index idx of a stream lives. Entries come from a
 // contiguous buffer (a network batch or staged copy: L = INT32_MAX, never
@@ -41,9 +65,17 @@ struct RingRow {
   int base, L;
   __device__ __forceinline__ const int32_t *at(int idx) const {
     const int k = idx + base;
+    bounds_note(k >= L ? (long long)k - L : k);
     return at_u(p + row, k >= L ? k - L : k);
   }
 };
+
+// A flat source whose entry 0 (Index prev + 1) is word `first` of p: at(x) is
+// p + first + (x - (prev + 1)), never wrapping (L = INT32_MAX), the lane
+// offset relative to entry 0 whatever the Index.
+__device__ __forceinline__ RingRow flat_src(const int32_t *p, int64_t first, int prev) {
+  return RingRow{p, (long long)first, -(prev + 1), INT32_MAX};
+}
 
 // Streaming (read-once / write-once) log accesses of the pass: non-temporal
 // loads and stores (plain temporal accesses measured slower in both the tick
@@ -106,6 +138,7 @@ struct Fol {
   __device__ __forceinline__ int32_t *at(int q, int idx) const {
     const long long row = (SLOTS ? (long long)slot[SLOTS ? q : 0] : slot0 + q + (q >= skip ? 1 : 0)) * (long long)L;
     const int k = idx + base[q];  // >= 0 for every lane that loads or stores (see RingRow)
+    bounds_note(k >= L ? (long long)k - L : k);
     return at_u(log + row, k >= L ? k - L : k);
   }
   __device__ __forceinline__ bool is_cmp(int q) const { return (cmp >> q) & 1; }
@@ -519,3 +552,24 @@ __device__ __forceinline__ void copy_loop(const Src &src, const F &fo, int c, in
 
 }  // namespace
 }  // namespace mraft
+
+// MRAFT_DEBUG_BOUNDS builds: an exported reader of this translation unit's
+// violation count (reset = 1 zeroes it after reading; -1 on a HIP error).
+#if MRAFT_DEBUG_BOUNDS
+#define MRAFT_BOUNDS_READER(fn)                                                                     \
+  extern "C" long long fn(int reset) {                                                              \
+    unsigned long long v = 0;                                                                       \
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(mraft::g_bounds_violations), sizeof v, 0,               \
+                            hipMemcpyDeviceToHost) != hipSuccess)                                   \
+      return -1;                                                                                    \
+    if (reset) {                                                                                    \
+      const unsigned long long z = 0;                                                               \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(mraft::g_bounds_violations), &z, sizeof z, 0,               \
+                            hipMemcpyHostToDevice) != hipSuccess)                                   \
+        return -1;                                                                                  \
+    }                                                                                               \
+    return (long long)v;                                                                            \
+  }
+#else
+#define MRAFT_BOUNDS_READER(fn)
+#endif

@@ -411,7 +411,6 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_group(Dev s, const
   fo.capok = 0;
   fo.full = 0;
   int mlo = last + 1, maybe_full = 0;
-  const RingRow lsrc{s.log, lrow, lb, L};
   bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
 #pragma unroll
   for (int q = 0; q < NI; ++q) {
@@ -420,7 +419,7 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_group(Dev s, const
     fo.base[q] = sh - sd;
     fo.start[q] = sp + 1;
     fo.cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
-    fo.cfrom[q] = 0;
+    fo.cfrom[q] = 0;                 // 0: no mismatch (the pass's relative Indexes are > 0)
     const bool capok = (long long)last - sd <= (long long)L - 1;
     fo.capok |= capok ? 1 << q : 0;
     if ((merge_m >> q) & 1) {
@@ -456,18 +455,32 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_group(Dev s, const
   if (merge_m || slo <= shi) {
     const int plo = min(mlo, slo <= shi ? slo : mlo);
     const int phi = merge_m ? last : shi;
+    // The pass runs on Indexes relative to B = pass_bias(plo) (mraft_pass.h:
+    // no chunk end overflows int32 near 2^31); the rows absorb B.
+    const int B = pass_bias(plo);
+#pragma unroll
+    for (int q = 0; q < NI; ++q) {
+      if (!((merge_m >> q) & 1)) continue;  // (only merging followers are ever addressed)
+      fo.base[q] += B;
+      fo.start[q] -= B;
+      fo.cend[q] -= B;
+    }
+    const RingRow lsrc{s.log, lrow, lb + B, L};
+    const int pl = plo - B, ph = phi - B, nend = last + 1 - B;
+    const int sl = slo <= shi ? slo - B : 1, sh = slo <= shi ? shi - B : 0;
     // Chunks start on a 128-B line of the leader's row (physical position of
     // plo rounded down; the ring wraps at a multiple of 4 entries, so every
     // lane's dwordx4 stays contiguous).
     if (vec) {
-      int c = plo - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
-      if (c <= phi && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      copy_loop<true, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
+      int c = pl - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
+      if (c <= ph && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, nend, sl, sh, T, found, c, pl, ph);
+      copy_loop<true, COUNT>(lsrc, fo, c, nend, pl, ph, sl, sh, T, found);
     } else {
-      int c = plo;
-      for (; c <= phi && fo.cmp; c += 256) pass_chunk<1, false, COUNT>(lsrc, fo, last + 1, slo, shi, T, found, c, plo, phi);
-      copy_loop<false, COUNT>(lsrc, fo, c, last + 1, plo, phi, slo, shi, T, found);
+      int c = pl;
+      for (; c <= ph && fo.cmp; c += 256) pass_chunk<1, false, COUNT>(lsrc, fo, nend, sl, sh, T, found, c, pl, ph);
+      copy_loop<false, COUNT>(lsrc, fo, c, nend, pl, ph, sl, sh, T, found);
     }
+    if (found >= 0) found += B;  // the a1 hit back in Raft Indexes
   }
   TICK_STAMP(2);
   const Dev s2 = reload_dev();  // phase C/D re-read the state pointers (not held across the pass)
@@ -739,3 +752,5 @@ void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned lo
 }
 
 }  // namespace mraft
+
+MRAFT_BOUNDS_READER(mraft_debug_bounds_tick)

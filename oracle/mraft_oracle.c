@@ -248,6 +248,13 @@ static int ae_flag_holds(const mraft_ae_args *a, const int32_t *ent) {
   return 1;
 }
 
+/* The Index domain (engine limit, include/mraft.h; Go's int has none): the
+ * last entry's Index prev + n must leave room for nextIndex = Index + 1 in
+ * int32, else the item is malformed (MRAFT_ITEM_BAD_SLOT). */
+static int ae_index_ok(const mraft_ae_args *a) {
+  return (int64_t)a->prev_log_index + a->n_entries <= (int64_t)INT32_MAX - 1;
+}
+
 /* ent = entries' terms (entry k has Index prev+1+k); cnt_src = the leader
  * replica whose log the entries were copied from (for counting its words), or
  * -1. */
@@ -379,7 +386,7 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
     for (int64_t i = 0; i < n; ++i) {
       const mraft_ae_args *a = &args[i];
       soff[i] = -1;
-      if (item_err[i] || a->n_entries < 0 || a->entries_offset < 0 ||
+      if (item_err[i] || a->n_entries < 0 || a->entries_offset < 0 || !ae_index_ok(a) ||
           (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n) ||
           a->entries_offset % e->L + a->n_entries > e->L)
         continue;
@@ -398,7 +405,7 @@ int ora_handle_append_entries(ora_engine *e, const mraft_ae_args *args,
     memset(&replies[i], 0, sizeof(replies[i]));
     if (item_err[i]) continue;
     const mraft_ae_args *a = &args[i];
-    if (a->n_entries < 0 || a->entries_offset < 0 ||
+    if (a->n_entries < 0 || a->entries_offset < 0 || !ae_index_ok(a) ||
         (a->n_entries > 0 && a->entries_offset + a->n_entries > src_n) ||
         (!entry_terms && a->entries_offset % e->L + a->n_entries > e->L)) {
       item_err[i] = MRAFT_ITEM_BAD_SLOT;
@@ -876,7 +883,8 @@ int ora_start(ora_engine *e, const int32_t *slots, const int32_t *counts,
     if (k < 1) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
     if (S.state[s] != MRAFT_LEADER) continue;                         /* :93-95 */
     int32_t last = S.last_index[s], dummy = S.dummy_index[s];
-    if ((int64_t)last + k - dummy > (int64_t)e->L - 1) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
+    if ((int64_t)last + k - dummy > (int64_t)e->L - 1 ||   /* capacity, or the Index domain (engine limits) */
+        (int64_t)last + k > (int64_t)INT32_MAX - 1) { item_err[i] = MRAFT_ITEM_LOG_FULL; continue; }
     if (last > dummy && term_at(e, s, last) > S.current_term[s]) S.terms_sorted[s] = 0;
     for (int32_t j = 1; j <= k; ++j)                                  /* :96-100 */
       S.log_term[lpos(e, s, last + j)] = S.current_term[s];

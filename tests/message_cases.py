@@ -131,3 +131,23 @@ def stale_cycle_state(st, lp, G, P, L, rng, groups, k):
             st["next_index"][a * P + (b % P)] = int(rng.integers(1, int(st["last_index"][a]) + 2))
             pairs.append((a, b % P))
     return st, np.array([a for a, _ in pairs], np.int32), np.array([b for _, b in pairs], np.int32)
+
+
+def shift_indices(st, off):
+    """The same logs with every Raft Index moved up by `off` (terms, rings and
+    every relation between Indexes unchanged): dummy, last, commit, lastApplied,
+    matchIndex and nextIndex. Raft's decisions depend on Index differences
+    only, so a step on the shifted state equals the step on the original with
+    its Index outputs shifted (the Index-domain invariance tests)."""
+    st = {k: v.copy() for k, v in st.items()}
+    for k in ("dummy_index", "last_index", "commit_index", "last_applied", "match_index", "next_index"):
+        st[k] = (st[k].astype(np.int64) + off).astype(np.int32)
+    return st
+
+
+def top_offset(st, j=0):
+    """The shift that puts the highest Index of `st` (its last, or a
+    nextIndex - 1) at 2^31 - 2 - j: the top of the engine's Index domain
+    (include/mraft.h: nextIndex = Index + 1 must be an int32)."""
+    hi = max(int(st["last_index"].max()), int(st["next_index"].max()) - 1)
+    return (2**31 - 2 - j) - hi

@@ -84,6 +84,70 @@ def test_back_to_back_steps_without_host_sync_gpu():
     assert_states_equal(got, o.state(), G, P, L, f"{K} steps, no host sync")
 
 
+def test_growing_batches_without_host_sync_gpu():
+    """K message steps whose batches GROW (each larger than
+    any before, so every call enlarges the engine's buffers: the handler's
+    set/deferral/order slots and the fold's segment and scan slots, plus the
+    first call's claims, counters and stage) enqueued behind a device spin on
+    a fresh engine: every call returns with the stream still busy (buffers
+    grow in stream order, no host wait) and the K steps equal K oracle steps
+    on the same growing batches."""
+    import torch
+    G, P, L, K = 1024, 5, 256, 4
+    st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3) + 11)
+    dev = torch.device("cuda", 0)
+    lib = _abi.lib()
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+    batches = []
+    for k in range(K):
+        gk = G * (k + 1) // K                      # groups [0, gk): a strictly larger batch each step
+        lpk = np.where(np.arange(G) < gk, lp, -1).astype(np.int32)
+        slots, peers = all_follower_items(lpk, G, P)
+        n = len(slots)
+        seg = np.concatenate([[0], np.cumsum(np.bincount(slots // P, minlength=G)[lpk >= 0])]).astype(np.int64)
+        batches.append(dict(slots=slots, peers=peers, n=n, seg=seg,
+                            sl=torch.from_numpy(slots).to(dev), pe=torch.from_numpy(peers).to(dev),
+                            sg=torch.from_numpy(seg).to(dev), args=z(n, 10), gerr=z(n), herr=z(n), ferr=z(n),
+                            flags=z(n), rep=z(n, 4), res=z(n, 8)))
+    assert all(batches[k]["n"] > batches[k - 1]["n"] for k in range(1, K))
+    torch.cuda.synchronize()
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        e.synchronize()
+        stream = torch.cuda.ExternalStream(e.stream(), device=dev)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(2e8))  # ~0.1 s of device spin ahead of the calls
+        for b in batches:
+            n = b["n"]
+            assert lib.mraft_gather_append_args(e._h, b["sl"].data_ptr(), b["pe"].data_ptr(), n, b["args"].data_ptr(),
+                                                b["gerr"].data_ptr(), DEVICE) == 0, _abi.last_error()
+            assert lib.mraft_handle_append_entries_ex(e._h, b["args"].data_ptr(), n, None, 0, b["rep"].data_ptr(),
+                                                      b["res"].data_ptr(), b["herr"].data_ptr(), DEVICE) == 0, \
+                _abi.last_error()
+            assert lib.mraft_process_append_replies(e._h, b["res"].data_ptr(), n, b["sg"].data_ptr(), len(b["seg"]) - 1,
+                                                    b["flags"].data_ptr(), b["ferr"].data_ptr(), DEVICE) == 0, \
+                _abi.last_error()
+        assert not stream.query(), "a growing message call waited on the device"
+        e.synchronize()
+        got = e.store_state()
+    o = Oracle(G, P, L, st)
+    for k, b in enumerate(batches):
+        oargs, ogerr = o.gather_append_args(b["slots"], b["peers"])
+        assert (ogerr == 0).all()
+        assert np.array_equal(b["args"].cpu().numpy().view(AE_ARGS).reshape(-1), oargs), k
+        orep, oherr = o.handle_append_entries(oargs, None)
+        assert np.array_equal(b["rep"].cpu().numpy().view(AE_REPLY).reshape(-1), orep), k
+        assert np.array_equal(b["herr"].cpu().numpy(), oherr), k
+        ores, oseg = results_of(b["slots"], b["peers"], oargs, orep, oherr, G, P)
+        gres = b["res"].cpu().numpy().view(AE_RESULT).reshape(-1)
+        okh = oherr == 0
+        assert np.array_equal(gres[okh][np.argsort(gres["slot"][okh], kind="stable")], ores), k
+        assert (gres["slot"][~okh] == -1).all(), k
+        of, oferr = o.process_append_replies(gres, b["seg"])
+        assert np.array_equal(b["flags"].cpu().numpy(), of) and np.array_equal(b["ferr"].cpu().numpy(), oferr), k
+    assert_states_equal(got, o.state(), G, P, L, f"{K} growing steps, no host sync")
+
+
 def test_back_to_back_copies_without_host_sync_gpu():
     """The bench's pattern: K steps, each on its own pristine state copy
     (mraft_bind_state), enqueued back to back with no synchronisation: every

@@ -10,6 +10,7 @@ another of their items reads."""
 import numpy as np
 import pytest
 
+from index_domain_cases import MSG_MODES, message_case
 from message_cases import all_follower_items, external_entries, results_of, stale_second_leader_state
 from oracle_lib import Oracle, assert_states_equal
 
@@ -164,36 +165,17 @@ def test_handle_sets_gpu(order):
             assert (herr != 0).any() and (herr == 0).any()
 
 
-def _shift_indices(st, off):
-    """The same logs with every Raft Index moved up by `off` (terms, rings and
-    every relation between indices unchanged)."""
-    st = {k: v.copy() for k, v in st.items()}
-    for k in ("dummy_index", "last_index", "commit_index", "last_applied", "match_index", "next_index"):
-        st[k] = (st[k].astype(np.int64) + off).astype(np.int32)
-    return st
-
-
-@pytest.mark.parametrize("mode", ["aligned", "misaligned", "staged"])
-def test_handle_high_indices_gpu(mode):
-    """prev_log_index above 2^30 (Go's int allows any Index; the engine any
-    below 2^31): entries from a host buffer and from the staged copy are
-    addressed relative to the pass's first Index, so nothing wraps."""
-    G, P, L = 96, 5, 256
-    off = (1 << 30) + 12345
-    st, lp, _ = synth_tick_state(G, P, L, seed=404)
-    if mode == "staged":
-        rng = np.random.default_rng(41)
-        st, slots, peers = stale_second_leader_state(st, lp, G, P, L, rng, range(0, G, 2))
-    else:
-        slots, peers = all_follower_items(lp, G, P)
-    st = _shift_indices(st, off)
-    assert int(st["dummy_index"].min()) >= off and int(st["last_index"].max()) < 2**31 - 1
-    o = Oracle(G, P, L, st)
-    with Engine(G, P, L) as e:
-        e.load_state(st)
-        rep, herr = _message_round(e, o, st, slots, peers, G, P, L,
-                                   "reference" if mode == "staged" else mode, assert_states_equal)
-    assert (rep["success"][herr == 0] == 1).any()
+@pytest.mark.parametrize("j", [0, 7])
+@pytest.mark.parametrize("mode", MSG_MODES)
+def test_handle_high_indices_gpu(mode, j):
+    """The highest Index at 2^31 - 2 - j (the top of the engine's domain,
+    include/mraft.h), prevLogIndex far above 2^30: entries from a host buffer
+    (aligned / misaligned), by reference in place, deferred in place, staged,
+    and in the ordered fallback (stage capacity 0 and 64), with the
+    sorted-terms flag set — GPU == oracle through gather, handle and fold
+    (tests/index_domain_cases.py; the flat-source read that faulted in round
+    5, DESIGN.md §5 r5_v1, runs on every one of these)."""
+    assert message_case(mode, j) > 0
 
 
 @pytest.mark.parametrize("S", [2, 3])
