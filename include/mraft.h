@@ -423,7 +423,9 @@ int64_t mraft_get_stage_capacity(const mraft_engine *h);
  * every item_err of it set, in this order: its first record's slot out of
  * range (MRAFT_ITEM_BAD_SLOT); an earlier non-empty segment names the same
  * slot (MRAFT_ITEM_DUP_SLOT, whatever that segment's own outcome); a record
- * of another slot or a bad peer (MRAFT_ITEM_BAD_SLOT); commitIndex below
+ * of another slot or a bad peer, or one whose args_n_entries is negative or
+ * ends past the Index domain, args_prev_log_index + args_n_entries >
+ * 2^31 - 2 (MRAFT_ITEM_BAD_SLOT); commitIndex below
  * dummyIndex (MRAFT_ITEM_BAD_STATE). The same rule holds for
  * mraft_process_install_snapshot_replies and mraft_process_vote_replies
  * (without the last). */
@@ -548,7 +550,9 @@ int mraft_gather_install_snapshot_args(mraft_engine *h, const int32_t *slots,
  * slots; out_flags[i] gets MRAFT_F_SNAPSHOT_INSTALLED when the log was
  * replaced (the host then delivers the snapshot to the service, raft.go:168-177).
  * A LastIncludedIndex in (commitIndex, lastIndex] but below the follower's own
- * dummyIndex makes Go's sliceFrom panic: MRAFT_ITEM_BELOW_DUMMY, no change. */
+ * dummyIndex makes Go's sliceFrom panic: MRAFT_ITEM_BELOW_DUMMY, no change.
+ * A LastIncludedIndex past the Index domain (> 2^31 - 2) is malformed:
+ * MRAFT_ITEM_BAD_SLOT (also in mraft_process_install_snapshot_replies). */
 int mraft_handle_install_snapshot(mraft_engine *h, const mraft_is_args *args,
                                   int64_t n, mraft_is_reply *replies,
                                   int32_t *out_flags, int32_t *item_err,

@@ -192,9 +192,11 @@ __device__ __forceinline__ void wave_copy_from_ring(const int32_t *__restrict__ 
 // hot path: load_state and restore only.
 __device__ __forceinline__ bool wave_terms_sorted(const int32_t *__restrict__ row, int base, int head, int L,
                                                   int lo, int hi) {
-  for (int b = lo; b < hi; b += kWave) {
-    const int idx = b + lane_id();
-    const bool bad = idx < hi && row[ring(idx - base + head, L)] > row[ring(idx + 1 - base + head, L)];
+  // (offsets from lo: an Index loop `b += 64` would overflow int32 within 64
+  // of 2^31 - 1, include/mraft.h's Index domain)
+  for (int d = 0; d < hi - lo; d += kWave) {
+    const int k = d + lane_id();  // Index lo + k
+    const bool bad = k < hi - lo && row[ring(lo + k - base + head, L)] > row[ring(lo + k + 1 - base + head, L)];
     if (__ballot(bad)) return false;
   }
   return true;

@@ -861,6 +861,14 @@ __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_deferred(HsArgs ka
 }
 
 // ---------------------------------------------------------------- a2 + a1
+// A reply record inside the Index domain (include/mraft.h): the acknowledged
+// entries end at prevLogIndex + n <= 2^31 - 2 with n >= 0 (matchIndex and
+// nextIndex stay int32); else the segment is malformed, as in the oracle
+// (reply_index_ok).
+__device__ __forceinline__ bool reply_index_ok(int prev, int n) {
+  return n >= 0 && (int64_t)prev + n <= (int64_t)INT32_MAX - 1;
+}
+
 template <int P>
 __device__ __forceinline__ int quorum_rt(const int (&m)[8], int me) {
   constexpr int h = P / 2;
@@ -1007,7 +1015,12 @@ __device__ __forceinline__ void fold_segment(const Dev &s, const mraft_ae_result
     if (base > 0 && i < cnt) { sl = items[b + i].slot; pr = items[b + i].peer; }
     // (a segment that does not own its slot stays MRAFT_ITEM_DUP_SLOT: the
     // claim decides first, include/mraft.h)
-    if (__ballot(i < cnt && (sl != slot || pr < 0 || pr >= P || pr == me)) && !bad) bad = MRAFT_ITEM_BAD_SLOT;
+    bool dok = true;  // the record inside the Index domain (reply_index_ok)
+    if (i < cnt) {
+      const mraft_ae_result &r = base > 0 ? items[b + i] : it;
+      dok = reply_index_ok(r.args_prev_log_index, r.args_n_entries);
+    }
+    if (__ballot(i < cnt && (sl != slot || pr < 0 || pr >= P || pr == me || !dok)) && !bad) bad = MRAFT_ITEM_BAD_SLOT;
   }
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {
@@ -1223,7 +1236,8 @@ __device__ __forceinline__ void fold_groupw(const Dev &s, const mraft_ae_result 
   const int srt = gw_bcast<GW>(vb, 6);
   // (a segment that does not own its slot stays MRAFT_ITEM_DUP_SLOT: the
   // claim decides first, include/mraft.h)
-  if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me)) && !bad)
+  if (gw_mask<GW>(gl < cnt && (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == me ||
+                               !reply_index_ok(it.args_prev_log_index, it.args_n_entries))) && !bad)
     bad = MRAFT_ITEM_BAD_SLOT;
   if (!bad && commit < dummy) bad = MRAFT_ITEM_BAD_STATE;
   if (bad) {
@@ -1542,6 +1556,12 @@ __global__ __launch_bounds__(256) void k_handle_is(Dev s, const mraft_is_args *_
     return;
   }
   const mraft_is_args a = args[i];
+  if (a.last_included_index > INT32_MAX - 1) {  // past the Index domain (include/mraft.h): malformed
+    rep[i] = mraft_is_reply{0, 0};
+    flags[i] = 0;
+    err[i] = MRAFT_ITEM_BAD_SLOT;
+    return;
+  }
   const int f = a.slot, fterm = s.term[f];
   int fl = 0;
   if (a.term < fterm) {                                                // :20-22
@@ -1594,7 +1614,9 @@ __global__ void k_process_is(Dev s, const mraft_is_result *__restrict__ items, i
   if (!bad)
     for (int64_t i = b; i < e; ++i) {
       const mraft_is_result it = items[i];
-      if (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+      if (it.slot != slot || it.peer < 0 || it.peer >= P || it.peer == slot % P ||
+          it.args_last_included_index > INT32_MAX - 1)  // (past the Index domain, include/mraft.h)
+        bad = MRAFT_ITEM_BAD_SLOT;
     }
   if (bad) {
     for (int64_t i = b; i < e; ++i) { item_err[i] = bad; flags[i] = 0; }

@@ -502,6 +502,16 @@ static int32_t process_reply_one(ora_engine *e, int32_t slot, int32_t peer,
   return flags;
 }
 
+/* A reply record inside the Index domain (engine limit, include/mraft.h): the
+ * entries it acknowledges end at args_prev_log_index + args_n_entries <=
+ * 2^31 - 2 (matchIndex, and nextIndex = matchIndex + 1, stay int32), with a
+ * non-negative count; else the record is malformed (MRAFT_ITEM_BAD_SLOT, the
+ * segment rejected like one with a bad peer). */
+static int reply_index_ok(const mraft_ae_result *it) {
+  return it->args_n_entries >= 0 &&
+         (int64_t)it->args_prev_log_index + it->args_n_entries <= (int64_t)INT32_MAX - 1;
+}
+
 int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
                                int64_t n, const int64_t *seg_begin,
                                int64_t n_seg, int32_t *out_flags,
@@ -521,7 +531,7 @@ int ora_process_append_replies(ora_engine *e, const mraft_ae_result *items,
     else {
       for (int64_t i = b; i < en; ++i)
         if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
-            items[i].peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+            items[i].peer == slot % P || !reply_index_ok(&items[i])) bad = MRAFT_ITEM_BAD_SLOT;
     }
     if (!bad && S.commit_index[slot] < S.dummy_index[slot]) bad = MRAFT_ITEM_BAD_STATE;
     if (bad) {
@@ -656,6 +666,8 @@ int ora_handle_install_snapshot(ora_engine *e, const mraft_is_args *args, int64_
     memset(&replies[i], 0, sizeof(replies[i]));
     out_flags[i] = 0;
     if (item_err[i]) continue;
+    /* LastIncludedIndex past the Index domain (engine limit, include/mraft.h): malformed */
+    if (args[i].last_included_index > INT32_MAX - 1) { item_err[i] = MRAFT_ITEM_BAD_SLOT; continue; }
     int inst = 0;
     item_err[i] = handle_is_one(e, args[i].slot, &args[i], &replies[i], &inst);
     if (inst) out_flags[i] = MRAFT_F_SNAPSHOT_INSTALLED;
@@ -702,7 +714,8 @@ int ora_process_install_snapshot_replies(ora_engine *e, const mraft_is_result *i
     else
       for (int64_t i = b; i < en; ++i)
         if (items[i].slot != slot || items[i].peer < 0 || items[i].peer >= P ||
-            items[i].peer == slot % P) bad = MRAFT_ITEM_BAD_SLOT;
+            items[i].peer == slot % P || items[i].args_last_included_index > INT32_MAX - 1)
+          bad = MRAFT_ITEM_BAD_SLOT;  /* (the last: past the Index domain, include/mraft.h) */
     if (bad) { for (int64_t i = b; i < en; ++i) item_err[i] = bad; continue; }
     for (int64_t i = b; i < en; ++i)
       out_flags[i] = process_is_reply_one(e, slot, items[i].peer, items[i].args_term,

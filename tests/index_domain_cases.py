@@ -35,6 +35,7 @@ from message_cases import (all_follower_items, external_entries, results_of, shi
 from oracle_lib import Oracle, assert_states_equal  # noqa: E402
 
 from multiraft_amd import Engine, synth_tick_state  # noqa: E402
+from multiraft_amd._abi import AE_REPLY, IS_ARGS  # noqa: E402
 
 MSG_MODES = ("aligned", "misaligned", "reference", "deferred", "staged", "ordered", "ordered64")
 TOP = 2**31 - 2
@@ -144,6 +145,34 @@ def malformed_case(G: int = 16, P: int = 3, L: int = 64, seed: int = 406):
         assert np.array_equal(herr, oherr) and np.array_equal(rep, orep), "malformed: handle"
         assert (herr[1::2] == 6).all(), "past the domain: MRAFT_ITEM_BAD_SLOT"
         assert_states_equal(e.store_state(), o.state(), G, P, L, "malformed: after handle")
+        # reply records: every other segment holds one record whose entries would end
+        # past the domain (or a negative count): the whole segment is malformed
+        gargs, gerr = e.gather_append_args(slots, peers)
+        oka = gerr == 0
+        res, seg = results_of(slots[oka], peers[oka], gargs[oka],
+                              np.zeros(int(oka.sum()), dtype=AE_REPLY), np.zeros(int(oka.sum()), np.int32), G, P)
+        res = res.copy()
+        for sgi in range(0, len(seg) - 1, 2):
+            r0 = int(seg[sgi])
+            if sgi % 4 == 0:
+                res["args_n_entries"][r0] = TOP - int(res["args_prev_log_index"][r0]) + 1
+            else:
+                res["args_n_entries"][r0] = -1
+        f, ferr = e.process_append_replies(res, seg)
+        of, oferr = o.process_append_replies(res, seg)
+        assert np.array_equal(ferr, oferr) and np.array_equal(f, of), "malformed: fold"
+        assert (ferr[int(seg[0]):int(seg[1])] == 6).all()
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "malformed: after fold")
+        # InstallSnapshot args past the domain
+        isa = np.zeros(len(ldr), dtype=IS_ARGS)
+        isa["slot"] = ldr
+        isa["term"] = 1 << 20
+        isa["leader_id"] = (ldr + 1) % P
+        isa["last_included_index"] = np.where(np.arange(len(ldr)) % 2 == 0, 2**31 - 1, TOP)
+        isa["last_included_term"] = 3
+        for x_ in zip(e.handle_install_snapshot(isa), o.handle_install_snapshot(isa)):
+            assert np.array_equal(*x_), "malformed: InstallSnapshot"
+        assert_states_equal(e.store_state(), o.state(), G, P, L, "malformed: after InstallSnapshot")
         for k in (1, 2, 1):
             r = e.start(np.array([x], np.int32), np.array([k], np.int32))
             orr = o.start(np.array([x], np.int32), np.array([k], np.int32))

@@ -25,6 +25,7 @@ from message_cases import (all_follower_items, external_entries, results_of, shi
 from oracle_lib import Oracle, assert_states_equal  # noqa: E402
 
 from multiraft_amd import synth_tick_state  # noqa: E402
+from multiraft_amd._abi import AE_REPLY, IS_ARGS  # noqa: E402
 
 TOP = 2**31 - 2
 
@@ -114,3 +115,34 @@ def test_past_the_index_domain_oracle():
     k = (TOP - last + 1).astype(np.int32)  # one past the top for every leader
     idx, term, isl, err = o.start(ldr, k)
     assert (err == 3).all() and (idx == -1).all()
+
+
+def test_past_the_index_domain_fold_and_snapshot_oracle():
+    """Reply records whose acknowledged entries would end past 2^31 - 2 (or
+    with a negative count) make their segment malformed; an InstallSnapshot
+    whose LastIncludedIndex is past it is malformed; everything else is
+    folded / installed as usual."""
+    G, P, L = 8, 3, 32
+    st0, lp, _ = synth_tick_state(G, P, L, seed=521, nthreads=1)
+    st = shift_indices(st0, top_offset(st0, 0))
+    o = Oracle(G, P, L, st)
+    slots, peers = all_follower_items(lp, G, P)
+    args, gerr = o.gather_append_args(slots, peers)
+    ok = gerr == 0
+    res, seg = results_of(slots[ok], peers[ok], args[ok], np.zeros(int(ok.sum()), dtype=AE_REPLY),
+                          np.zeros(int(ok.sum()), np.int32), G, P)
+    res = res.copy()
+    r0 = int(seg[0])
+    res["args_n_entries"][r0] = TOP - int(res["args_prev_log_index"][r0]) + 1
+    r1 = int(seg[1])
+    res["args_n_entries"][r1] = -1
+    f, ferr = o.process_append_replies(res, seg)
+    assert (ferr[int(seg[0]):int(seg[2])] == 6).all() and not ferr[int(seg[2]):].any()
+    ldr = np.array([g * P + int(lp[g]) for g in range(G) if lp[g] >= 0], np.int32)
+    isa = np.zeros(len(ldr), dtype=IS_ARGS)
+    isa["slot"], isa["term"], isa["leader_id"] = ldr, 1 << 20, (ldr + 1) % P
+    isa["last_included_index"] = np.where(np.arange(len(ldr)) % 2 == 0, 2**31 - 1, TOP)
+    isa["last_included_term"] = 3
+    rep, fl, err = o.handle_install_snapshot(isa)
+    assert (err[0::2] == 6).all() and (err[1::2] == 0).all() and (fl[1::2] != 0).all()
+    assert (o.state()["dummy_index"][ldr[1::2]] == TOP).all()
