@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -20,6 +21,17 @@
 constexpr int kMaxShards = 8;
 // Default capacity of the AppendEntries stage (mraft_set_stage_capacity): 16 MiB.
 constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
+// The deferred launch's grid (mraft_handle_append_entries by reference): the
+// last call's deferred count, read from a pinned word the device writes, in
+// [kDeferGridMin, kDeferGridMax] workgroups (grid-stride beyond). With no
+// deferred item the launch exits at once on kDeferGridMin workgroups (a small
+// blind launch finds wave slots beside another queue's kernels at once:
+// profiles/r5_g1); a deferred-heavy batch gets a workgroup per item from the
+// next call on (round 5's fixed 8 ran such batches on 0.4 % of the chip).
+constexpr int kDeferGridMin = 8;
+constexpr int kDeferGridMax = 1 << 16;
+// Words of the fallback's per-workgroup cycle buffers (nslot x L, at most this).
+constexpr int64_t kCycSlotWords = (int64_t)1 << 24;
 
 struct mraft_engine {
   int32_t G = 0, P = 0, L = 0, device = 0;
@@ -45,6 +57,8 @@ struct mraft_engine {
   uint32_t epoch = 0;
   unsigned long long *ae_total = nullptr;  // AppendEntries by reference: staged words, deferred items << 32
   int64_t stage_cap = kDefaultStageWords;  // words of staged entries the deferred launch may use
+  long long *dhint = nullptr;  // pinned host word: the last by-reference call's deferred count (device-written)
+  long long *dhint_dev = nullptr;  // its device-side address
   std::vector<void *> scratch_ptr;
   std::vector<size_t> scratch_cap;
 };
@@ -344,6 +358,24 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
     return fail(MRAFT_E_HIP, "hipStreamCreate failed");
   }
   h->stream = h->own_stream;
+  {
+    void *hp = nullptr;
+    if (hipHostMalloc(&hp, sizeof(long long), hipHostMallocMapped) != hipSuccess) {
+      (void)hipStreamDestroy(h->own_stream);
+      delete h;
+      return fail(MRAFT_E_NOMEM, "pinned host word allocation failed");
+    }
+    h->dhint = (long long *)hp;
+    *(volatile long long *)h->dhint = 0;
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+      (void)hipHostFree(hp);
+      (void)hipStreamDestroy(h->own_stream);
+      delete h;
+      return fail(MRAFT_E_HIP, "hipHostGetDevicePointer failed");
+    }
+    h->dhint_dev = (long long *)dp;
+  }
   if (!(flags & MRAFT_CREATE_NO_ALLOC)) {
     h->owned = true;
     for (const auto &a : kArrays) {
@@ -351,6 +383,7 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
       if (hipMalloc(&p, arr_bytes(h, a.kind)) != hipSuccess) {
         free_owned(h);
         (void)hipStreamDestroy(h->own_stream);
+        (void)hipHostFree(h->dhint);
         delete h;
         return fail(MRAFT_E_NOMEM, "device state allocation failed (G=%d P=%d L=%d)", groups, peers,
                     log_capacity);
@@ -366,6 +399,7 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
     if (e != hipSuccess) {
       free_owned(h);
       (void)hipStreamDestroy(h->own_stream);
+      (void)hipHostFree(h->dhint);
       delete h;
       return fail(MRAFT_E_HIP, "init failed: %s", hipGetErrorString(e));
     }
@@ -392,6 +426,7 @@ int mraft_destroy(mraft_engine *h) {
     if (s) (void)hipStreamDestroy(s);
   if (h->fanin_ev) (void)hipEventDestroy(h->fanin_ev);
   if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->dhint) (void)hipHostFree(h->dhint);
   delete h;
   return MRAFT_OK;
 }
@@ -620,19 +655,31 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
   TRY(scratch(h, 15, (size_t)n, &sethd));
   TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
-  // the ordered fallback's in-degrees and queue (n each) and cycle buffer (L)
-  TRY(scratch(h, 19, sizeof(int32_t) * (2 * (size_t)n + (size_t)h->L), &order));
+  // the deferred launch's grid: the last call's deferred count (a pinned word
+  // the device writes; a stale value only changes the grid, never a result)
+  const long long last_nd = *(volatile long long *)h->dhint;
+  mraft::AeDeferBufs db{};
+  db.grid = (int)(last_nd < kDeferGridMin ? kDeferGridMin : last_nd > kDeferGridMax ? kDeferGridMax : last_nd);
+  db.nslot = (int)std::min<int64_t>(db.grid, std::max<int64_t>(1, kCycSlotWords / h->L));
+  // the fallback's per-item records and reader counts, its L-word buffer and
+  // nslot cycle buffers
+  const size_t nn = (size_t)n, L = (size_t)h->L;
+  TRY(scratch(h, 19, nn * (16 + 8) + (1 + (size_t)db.nslot) * L * 4, &order));
+  db.fb = (int4 *)order;
+  db.kin = (unsigned long long *)(db.fb + nn);
+  db.cyc = (int32_t *)(db.kin + nn);
+  db.cslot = db.cyc + L;
+  db.hint = h->dhint_dev;
   // the stage: when it cannot be allocated the batch runs with none (every
   // staged item then takes the ordered fallback: the same results, slower)
   if (h->stage_cap > 0 && scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage) != MRAFT_OK) stage = nullptr;
   const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
   const int64_t n_log = gp_of(h) * h->L;
-  int32_t *kin = (int32_t *)order, *kq = kin + n, *cyc = kq + n;
   mraft::launch_claim_ae((const mraft_ae_args *)a, n, n_log, h->L, gp_of(h), ni, h->claim, h->srcmark, h->epoch,
                          (int32_t *)e, (uint8_t *)sethd, h->ae_total, h->stream);
   mraft::launch_handle_ae_ref(dev_of(h), (const mraft_ae_args *)a, n, ni, h->claim, h->srcmark, h->epoch,
                               (int32_t *)e, (const uint8_t *)sethd, (int64_t *)soff, (int64_t *)defer, h->ae_total,
-                              (int32_t *)stage, stage ? h->stage_cap : 0, kin, kq, cyc, (mraft_ae_reply *)r,
+                              (int32_t *)stage, stage ? h->stage_cap : 0, db, (mraft_ae_reply *)r,
                               (mraft_ae_result *)rs, h->stream);
   return sg.finish();
 }

@@ -32,10 +32,24 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
 void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp, int ni,
                      unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, uint8_t *sethd,
                      unsigned long long *total, hipStream_t st);
+// The deferred launch's buffers and grid (mraft_kernels.hip "deferred
+// launch's fallback"): per item a 16-B record (writer, arrivals, run flag,
+// cycle counter) and a reader count, nslot cycle buffers of L words, the last
+// workgroup's L-word buffer, the pinned host word with the last deferred
+// count, and the grid the host chose from it.
+struct AeDeferBufs {
+  int4 *fb;
+  unsigned long long *kin;
+  int32_t *cslot;
+  int nslot;
+  int32_t *cyc;
+  long long *hint;
+  int grid;
+};
 void launch_handle_ae_ref(const Dev &s, const mraft_ae_args *args, int64_t n, int ni, const unsigned long long *claim,
                           const uint32_t *srcmark, uint32_t epoch, int32_t *err, const uint8_t *sethd, int64_t *soff,
-                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap, int32_t *kin,
-                          int32_t *kq, int32_t *cyc, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st);
+                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap,
+                          const AeDeferBufs &db, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st);
 // AppendEntries with the entries in a caller buffer (claims by launch_claim).
 void launch_handle_ae_host(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                            mraft_ae_reply *rep, int32_t *err, mraft_ae_result *res, hipStream_t st);

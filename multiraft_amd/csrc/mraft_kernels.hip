@@ -247,8 +247,9 @@ __global__ __launch_bounds__(64) void k_claim_ae(const mraft_ae_args *__restrict
   const int t = (int)threadIdx.x;
   const int64_t i = blockIdx.x * (int64_t)64 + t;
   if (i == 0) {
-    total[0] = 0;
-    total[1] = 0;
+    total[0] = 0;  // staged words
+    total[1] = 0;  // deferred items << 32
+    total[3] = 0;  // workgroups of the deferred launch's fallback done (total[2]: the published count)
   }
   AeKey k{-1, 0, 0};
   if (i < n) {
@@ -320,9 +321,6 @@ __device__ __forceinline__ void mark_persist_ae(const Dev &s, int64_t slot, int 
 // wave slots beside another pipeline's handler finds them at once — two
 // pipelines 0.366-0.369 -> 0.358 ms per step, three 0.363-0.365 -> 0.354
 // (profiles/r5_g1; 512 / 256 / 2,048 workgroups before).
-#ifndef MRAFT_AE_DGRID
-#define MRAFT_AE_DGRID 8       // workgroups of the deferred launch (grid-stride over the deferred items)
-#endif
 #ifndef MRAFT_FOLD_TAIL_NL
 #define MRAFT_FOLD_TAIL_NL 16  // k_fold_tail workgroups for the long segments (grid-stride)
 #endif
@@ -350,8 +348,16 @@ struct HsArgs {
   const unsigned long long *claim;
   const uint32_t *srcmark;
   uint32_t epoch;
-  int32_t *kin, *kq;    // fallback order: in-degree per item, queue
-  int32_t *cyc;         // fallback cycle buffer (L words)
+  // The deferred launch's fallback (staged words past the stage capacity),
+  // per item, written by the main launch for its deferred items:
+  int4 *fb;                  // {claimant of the row it reads (its writer, fb_writer), readers of its
+                             // row already run, run flag, short-cycle readiness at the cycle's
+                             // smallest item}: one 16-B record, zeroed but the first word
+  unsigned long long *kin;   // epoch-tagged count of the deferred items that read this item's row
+  int32_t *cslot;            // per-workgroup cycle buffers, nslot x L words
+  int nslot;
+  int32_t *cyc;              // the last workgroup's cycle buffer (L words)
+  long long *hint;           // pinned host word: the last deferred count (the next call's grid)
   mraft_ae_reply *rep;
   int32_t *err;
   mraft_ae_result *res;  // optional: each item's reply as its co-resident leader folds it
@@ -368,7 +374,8 @@ __device__ __forceinline__ HsArgs reload_hs() {
   k.s.head = kp->s.head; k.s.hsnap = kp->s.hsnap; k.s.srt = kp->s.srt; k.s.G = kp->s.G; k.s.P = kp->s.P; k.s.L = kp->s.L;
   k.args = kp->args; k.n = kp->n; k.ent0 = kp->ent0; k.n_ent0 = kp->n_ent0; k.stage = kp->stage;
   k.stage_cap = kp->stage_cap; k.soff = kp->soff; k.sethd = kp->sethd; k.defer = kp->defer; k.total = kp->total;
-  k.claim = kp->claim; k.srcmark = kp->srcmark; k.epoch = kp->epoch; k.kin = kp->kin; k.kq = kp->kq; k.cyc = kp->cyc;
+  k.claim = kp->claim; k.srcmark = kp->srcmark; k.epoch = kp->epoch; k.fb = kp->fb; k.kin = kp->kin;
+  k.cslot = kp->cslot; k.nslot = kp->nslot; k.cyc = kp->cyc; k.hint = kp->hint;
   k.rep = kp->rep; k.err = kp->err; k.res = kp->res;
   return k;
 }
@@ -389,12 +396,56 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// The source row's writer of a deferred item: the item that owns the row it
+// reads (claim winner) when that row is claimed in this call and the owner is
+// itself a deferred item (a well-formed reference; its slot is read, so it
+// was deferred); else -1.
+__device__ __forceinline__ int64_t ae_writer(const HsArgs &k, int64_t x) {
+  const mraft_ae_args a = k.args[x];
+  const int L = k.s.L;
+  const int64_t gp = (int64_t)k.s.G * k.s.P;
+  if (a.n_entries <= 0 || !ae_ref_ok(a, gp * L, L) || !ae_index_ok(a)) return -1;
+  const unsigned long long c = __hip_atomic_load(&k.claim[a.entries_offset / L], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+  if ((uint32_t)(c >> 32) != k.epoch) return -1;
+  const int64_t w = (int64_t)(0xFFFFFFFFull - (c & 0xFFFFFFFFull));
+  return ae_ref_ok(k.args[w], gp * L, L) ? w : -1;
+}
+
+__device__ __forceinline__ int at_load(int32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void at_store(int32_t *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void phase_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+// Epoch-tagged counters (high 32 bits: the call's epoch; a stale tag reads as
+// 0), so no call has to zero them before counting.
+__device__ __forceinline__ void tag_inc(unsigned long long *p, uint32_t epoch) {
+  unsigned long long old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const unsigned long long nv =
+        (uint32_t)(old >> 32) == epoch ? old + 1 : (((unsigned long long)epoch << 32) | 1ull);
+    if (__hip_atomic_compare_exchange_strong(p, &old, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return;
+  }
+}
+__device__ __forceinline__ int tag_count(const unsigned long long *p, uint32_t epoch) {
+  const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)(v >> 32) == epoch ? (int)(uint32_t)v : 0;
+}
+
 // The main launch's bookkeeping for the `written` lanes of a wave (rare: a
 // stale leader both sending and receiving in one batch): their place in the
 // deferred list, and for those that also `read`, a staged offset and the copy
 // of their entries (the source row is pristine: its writer is deferred too).
 __device__ __forceinline__ void defer_lanes(const HsArgs &k0, bool dfr, bool stg, int64_t i, int n, const int32_t *row,
-                                            int head, int from, int L) {
+                                            int head, int from, int L, int wraw) {
   const unsigned long long m = __ballot(dfr);
   const int lane = lane_id(), q0 = first_lane(m);
   unsigned long long b = 0;
@@ -406,6 +457,12 @@ __device__ __forceinline__ void defer_lanes(const HsArgs &k0, bool dfr, bool stg
     int64_t in_place = -2;  // made here (as a hoisted constant pair it was spilled across the pass)
     asm volatile("" : "+v"(in_place));
     if (!stg) k0.soff[i] = in_place;
+    // the fallback's graph (used only when the staged words pass the stage
+    // capacity): the claimant of the row this item reads (its writer when that
+    // claimant is deferred too, which the fallback checks: fb_writer), its
+    // count of readers there, and this item's own counters zeroed
+    k0.fb[i] = make_int4(wraw, 0, 0, 0);  // one store (four separate arrays spilled the main launch)
+    if (wraw >= 0) tag_inc(&k0.kin[wraw], k0.epoch);
   }
   for (unsigned long long sm = __ballot(stg); sm; sm &= sm - 1) {
     const int q = first_lane(sm);
@@ -464,12 +521,13 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
   bool ok = true, dup = false, dfr = false, stg = false;
   int64_t srow = 0;  // by reference: the source row
   int rhead = 0;
+  unsigned long long cr = 0;  // HM_MAIN: the claim word of the source row
   if (MODE == HM_HOST) {
     if (!e) src = flat_src(k0.ent0, a.entries_offset, prev);
   } else if (!e) {
     ok = ae_ref_ok(a, gp * L, L);
     srow = ok ? a.entries_offset / L : 0;
-    unsigned long long cs = 0, cr = 0;
+    unsigned long long cs = 0;
     uint32_t sm = 0;
     if (MODE == HM_MAIN) {
       cs = k0.claim[f];
@@ -503,8 +561,13 @@ __device__ __forceinline__ void handle_one(const HsArgs &k0, int64_t first, int 
     cls = AE_BAD;
   const bool live = cls == AE_DONE;
   if (dup && mine) k0.err[i] = MRAFT_ITEM_DUP_SLOT;
-  if (MODE == HM_MAIN && __ballot(dfr))
-    defer_lanes(k0, dfr, stg, i, nn, s.log + srow * L, rhead, (int)(a.entries_offset % L), L);
+  if (MODE == HM_MAIN && __ballot(dfr)) {
+    // the claimant of the row this item reads (from the claim word loaded above),
+    // for an item that reads anything (the writer check is the fallback's)
+    const int wraw = (nn > 0 && ae_index_ok(a) && (uint32_t)(cr >> 32) == k0.epoch)
+                         ? (int)(0xFFFFFFFFu - (uint32_t)cr) : -1;
+    defer_lanes(k0, dfr, stg, i, nn, s.log + srow * L, rhead, (int)(a.entries_offset % L), L, wraw);
+  }
   if (k0.res && mine && cls != AE_DEFER) {
     // the args half of the item's reply record for its co-resident leader's
     // fold, stored now (no reload of the args at the wave's end); the reply
@@ -736,127 +799,196 @@ __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_set(HsArgs ka) {
   }
 }
 
-// The source row's writer of a deferred item: the item that owns the row it
-// reads (claim winner) when that row is claimed in this call and the owner is
-// itself a deferred item (a well-formed reference; its slot is read, so it
-// was deferred); else -1.
-__device__ __forceinline__ int64_t ae_writer(const HsArgs &k, int64_t x) {
-  const mraft_ae_args a = k.args[x];
-  const int L = k.s.L;
-  const int64_t gp = (int64_t)k.s.G * k.s.P;
-  if (a.n_entries <= 0 || !ae_ref_ok(a, gp * L, L)) return -1;
-  const unsigned long long c = __hip_atomic_load(&k.claim[a.entries_offset / L], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  if ((uint32_t)(c >> 32) != k.epoch) return -1;
-  const int64_t w = (int64_t)(0xFFFFFFFFull - (c & 0xFFFFFFFFull));
-  return ae_ref_ok(k.args[w], gp * L, L) ? w : -1;
+// ---- The deferred launch's fallback: the staged words exceed the stage
+// capacity, so deferred items that are also `read` have no staged copy and
+// must run in an order (round 6; rounds 4-5 ran the whole fallback on one
+// wave). Edge x -> wr[x]: x reads the row its writer wr[x] rewrites, so x runs
+// first. Each item has one writer at most, so the graph is trees feeding
+// chains that end at an item with no writer or at a cycle. Every workgroup
+// takes deferred items grid-stride and nothing ever waits:
+//  * an item no deferred item reads (kin 0) starts a chain: it runs, then
+//    counts itself at its writer (arr); the reader that completes the
+//    writer's count (arr == kin) runs the writer next, and so on;
+//  * a cycle of at most kCycWalk items (found by walking wr) runs as a unit
+//    on one wave, once every tree feeding it has run: its smallest item's
+//    entries are copied to the wave's cycle buffer first, then the members
+//    run around the cycle from its writer, that item last from the copy.
+//    Readiness is one counter at that item (cpend): each member whose other
+//    readers have all run adds 1 (the reader whose arrival leaves only the
+//    cycle predecessor missing, arr == kin - 1), and the smallest item's own
+//    visit adds kBig - F (F: members with such readers): the add that brings
+//    it to kBig runs the cycle;
+//  * what is left — cycles longer than the walk, or completed on a workgroup
+//    with no cycle buffer — the last workgroup to finish runs one cycle at a
+//    time through the L-word buffer (every tree has run by then).
+// Nothing another item reads is written before that item has read it; items
+// of a chain share no row they both read and write, so the hand-offs need no
+// fence beyond the counters' atomics (the runs of a cycle are ordered on one
+// wave). Same results as the staged path (tests/test_handler_async.py,
+// tests/test_deferred_graphs_gpu.py).
+constexpr int kCycWalk = 32;
+constexpr unsigned kCycBig = 1u << 30;  // > kCycWalk: the count cannot reach it early
+
+__device__ __forceinline__ int32_t &fb_dn(const HsArgs &k, int64_t x) { return reinterpret_cast<int32_t *>(k.fb + x)[2]; }
+
+// One deferred item in the fallback: its entries in place (buf null) or from
+// buf (its copy); then marked run.
+__device__ __forceinline__ void fb_run(const HsArgs &k, int64_t x, int32_t *buf) {
+  HsArgs kx = k;
+  kx.stage = buf;
+  kx.stage_cap = k.s.L;
+  handle_one<1, HM_ORDER>(kx, x, 1, buf ? 0 : -2);
+  if (lane_id() == 0) at_store(&fb_dn(k, x), 1);
 }
 
-__device__ __forceinline__ int at_load(int32_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void at_store(int32_t *p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void phase_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-  __builtin_amdgcn_s_waitcnt(0);
+// x's writer: the claimant of the row x reads when that claimant is a
+// well-formed reference (then its slot, read by x, made it deferred too).
+__device__ __forceinline__ int64_t fb_writer(const HsArgs &k, int64_t x) {
+  const int w = __builtin_amdgcn_readfirstlane(reinterpret_cast<const int32_t *>(k.fb + x)[0]);
+  if (w < 0 || (int64_t)w >= k.n) return -1;
+  const int L = k.s.L;
+  return ae_ref_ok(k.args[w], (int64_t)k.s.G * k.s.P * L, L) ? (int64_t)w : -1;
 }
 
-// The ordered fallback (the staged words exceed the stage capacity), on one
-// wave: Kahn's order over the deferred items with the edge x -> writer(x)
-// (x reads the row its writer rewrites, so x runs first); every item reads its
-// source in place, except that when no item is free the remaining ones are
-// all on cycles (each item has one writer at most), and one of them has its
-// entries copied to the cycle buffer first, which frees its writer. Shared
-// words through L2 (agent-scope atomics); wave-uniform control.
-template <int NI>
-__device__ void handle_ordered(const HsArgs &k, int64_t nd) {
-  const int lane = lane_id();
-  for (int64_t j = lane; j < nd; j += 64) at_store(&k.kin[k.defer[j]], 0);
-  phase_fence();
-  for (int64_t j = lane; j < nd; j += 64) {
-    const int64_t w = ae_writer(k, k.defer[j]);
-    if (w >= 0) (void)atomicAdd(&k.kin[w], 1);
+// Whether y lies on a cycle of at most kCycWalk items; then its smallest item
+// and length.
+__device__ __forceinline__ bool fb_short_cycle(const HsArgs &k, int64_t y, int64_t *least, int *len) {
+  int64_t z = y, m = y;
+  for (int st = 1; st <= kCycWalk; ++st) {
+    z = fb_writer(k, z);
+    if (z < 0) return false;
+    if (z == y) {
+      *least = m;
+      *len = st;
+      return true;
+    }
+    m = min(m, z);
   }
-  phase_fence();
-  int64_t qt = 0;  // queue tail (wave-uniform)
-  for (int64_t j0 = 0; j0 < nd; j0 += 64) {
-    const int64_t j = j0 + lane;
-    const int64_t x = j < nd ? k.defer[j] : -1;
-    const bool free0 = x >= 0 && at_load(&k.kin[x]) == 0;
-    const unsigned long long m = __ballot(free0);
-    if (free0) at_store(&k.kq[qt + lanes_below(m)], (int)x);
-    qt += __popcll(m);
-  }
-  phase_fence();
-  int64_t qh = 0, brk = -1;
+  return false;
+}
+
+// A cycle whose feeding trees have all run, from its smallest item b: b's
+// entries (the pristine row of its writer) copied first, then the members
+// from b's writer round to b. With no cycle buffer for this workgroup the
+// cycle is left to the last workgroup.
+__device__ __forceinline__ void fb_run_cycle(const HsArgs &k, int64_t b) {
+  if ((int)blockIdx.x >= k.nslot) return;
+  int32_t *buf = k.cslot + (int64_t)blockIdx.x * k.s.L;
+  const mraft_ae_args a = k.args[b];
   const int L = k.s.L;
-  for (int64_t done = 0; done < nd;) {
-    if (qh == qt) {
-      // every item left is on a cycle: copy one member's entries aside and
-      // free its writer
-      int64_t x = -1;
-      for (int64_t j0 = 0; j0 < nd && x < 0; j0 += 64) {
-        const int64_t j = j0 + lane;
-        const int64_t y = j < nd ? k.defer[j] : -1;
-        const unsigned long long m = __ballot(y >= 0 && at_load(&k.kin[y]) > 0);
-        if (m) {
-          const int q = first_lane(m);
-          x = ((int64_t)__builtin_amdgcn_readlane((int)(y >> 32), q) << 32) |
-              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)y, q);
-        }
-      }
-      if (x < 0) return;  // unreachable: the counts say an item is left
-      const mraft_ae_args a = k.args[x];
-      const int64_t row = a.entries_offset / L;
-      wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L), k.cyc,
-                          a.n_entries);
-      brk = x;
-      const int64_t w = ae_writer(k, x);
-      if (w < 0) return;  // unreachable: an item on a cycle has a writer
-      phase_fence();
-      int fr = 0;
-      if (lane == 0) fr = atomicSub(&k.kin[w], 1) == 1;
-      if (__builtin_amdgcn_readfirstlane(fr)) {
-        if (lane == 0) at_store(&k.kq[qt], (int)w);
-        ++qt;
-      }
-      phase_fence();
+  const int64_t row = a.entries_offset / L;
+  wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L), buf, a.n_entries);
+  phase_fence();
+  int64_t z = fb_writer(k, b);
+  for (int st = 0; z >= 0 && z != b && st < kCycWalk; ++st, z = fb_writer(k, z)) fb_run(k, z, nullptr);
+  fb_run(k, b, buf);
+}
+
+__device__ __forceinline__ void fb_cycle_add(const HsArgs &k, int64_t b, unsigned add) {
+  unsigned old = 0;
+  if (lane_id() == 0) old = atomicAdd(reinterpret_cast<unsigned *>(k.fb + b) + 3, add);
+  old = (unsigned)__builtin_amdgcn_readfirstlane((int)old);
+  if (old + add == kCycBig) fb_run_cycle(k, b);
+}
+
+// x, then every writer whose readers x's run completes.
+__device__ __forceinline__ void fb_chain(const HsArgs &k, int64_t x) {
+  x = ((int64_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+  for (;;) {
+    fb_run(k, x, nullptr);
+    const int64_t w = fb_writer(k, x);
+    if (w < 0) return;
+    unsigned a = 0;
+    if (lane_id() == 0) a = atomicAdd(reinterpret_cast<unsigned *>(k.fb + w) + 1, 1u) + 1u;
+    a = (unsigned)__builtin_amdgcn_readfirstlane((int)a);
+    const unsigned kw = (unsigned)tag_count(&k.kin[w], k.epoch);
+    if (a == kw) {
+      x = w;
       continue;
     }
-    const int64_t x = __builtin_amdgcn_readfirstlane(at_load(&k.kq[qh]));
-    ++qh;
-    HsArgs kx = k;
-    kx.stage = k.cyc;
-    kx.stage_cap = L;
-    handle_one<NI, HM_ORDER>(kx, x, 1, x == brk ? 0 : -2);
-    ++done;
-    phase_fence();
-    const int64_t w = ae_writer(k, x);
-    if (lane == 0) at_store(&k.kin[x], -1);
-    int fr = 0;
-    if (w >= 0 && lane == 0) fr = atomicSub(&k.kin[w], 1) == 1;
-    if (__builtin_amdgcn_readfirstlane(fr)) {
-      if (lane == 0) at_store(&k.kq[qt], (int)w);
-      ++qt;
-    }
-    phase_fence();
+    int64_t b;
+    int len;
+    if (a + 1 == kw && fb_short_cycle(k, w, &b, &len)) fb_cycle_add(k, b, 1);
+    return;
   }
+}
+
+// The last workgroup: every item not yet run lies on a cycle whose feeding
+// trees have run; each such cycle runs from one member x through the L-word
+// buffer.
+__device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd) {
+  const int lane = lane_id();
+  const int L = k.s.L;
+  for (int64_t j0 = 0; j0 < nd; j0 += 64) {
+    const int64_t j = j0 + lane;
+    const int64_t y = j < nd ? k.defer[j] : -1;
+    for (unsigned long long m = __ballot(y >= 0 && at_load(&fb_dn(k, y)) == 0); m; m &= m - 1) {
+      const int q = first_lane(m);
+      const int64_t x = ((int64_t)__builtin_amdgcn_readlane((int)(y >> 32), q) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)y, q);
+      if (__builtin_amdgcn_readfirstlane(at_load(&fb_dn(k, x)))) continue;  // run with an earlier one's cycle
+      const mraft_ae_args a = k.args[x];
+      const int64_t row = a.entries_offset / L;
+      if (a.n_entries > 0) wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L),
+                                               k.cyc, a.n_entries);
+      phase_fence();
+      int64_t z = fb_writer(k, x);
+      for (int64_t st = 0; z >= 0 && z != x && st < nd; ++st) {
+        fb_run(k, z, nullptr);
+        z = fb_writer(k, z);
+      }
+      fb_run(k, x, k.cyc);
+    }
+  }
+}
+
+__device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd) {
+  for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) {
+    const int64_t x = k.defer[j];
+    if (tag_count(&k.kin[x], k.epoch) == 0) {
+      fb_chain(k, x);  // no deferred item reads x's row: a chain starts here
+    } else {
+      int64_t b;
+      int len;
+      if (fb_short_cycle(k, x, &b, &len) && b == x) {
+        // x is its short cycle's smallest item: its visit's share of the count
+        int F = 0;
+        int64_t z = x;
+        for (int st = 0; st < len; ++st) {
+          F += tag_count(&k.kin[z], k.epoch) > 1 ? 1 : 0;
+          z = fb_writer(k, z);
+        }
+        fb_cycle_add(k, x, kCycBig - (unsigned)F);
+      }
+    }
+  }
+  // the last workgroup to finish runs what is left (it sees every other
+  // workgroup's runs: release before the count, acquire after it)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  int last = 0;
+  if (lane_id() == 0) last = atomicAdd(&k.total[3], 1ull) == (unsigned long long)gridDim.x - 1;
+  if (!__builtin_amdgcn_readfirstlane(last)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  fb_leftover(k, nd);
 }
 
 // The deferred launch: every deferred item (a set of one), grid-stride; the
 // counts are read on the device (the host enqueues this launch blind: with no
-// deferred item, every workgroup exits at once).
-// (Each deferred item is a set of one: the one-lane form of the pass.)
+// deferred item, every workgroup exits at once). Its grid is the host's choice
+// from the last call's deferred count, which workgroup 0 publishes to a pinned
+// host word when it changes (total[2] keeps the published value).
 __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_deferred(HsArgs ka) {
   const unsigned long long staged = ka.total[0];
   const int64_t nd = (int64_t)(ka.total[1] >> 32);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ka.hint && ka.total[2] != (unsigned long long)nd) {
+    ka.total[2] = (unsigned long long)nd;
+    __hip_atomic_store(ka.hint, (long long)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (nd == 0) return;
   if ((long long)staged <= ka.stage_cap) {
     for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) handle_one<1, HM_DEFER>(ka, ka.defer[j], 1);
-  } else if (blockIdx.x == 0) {
-    handle_ordered<1>(ka, nd);
+  } else {
+    defer_fallback(ka, nd);
   }
 }
 
@@ -1897,37 +2029,42 @@ static void launch_set(const HsArgs &ka, int64_t nb, hipStream_t st) {
 }
 
 template <int NI>
-static void launch_ref(const HsArgs &ka, hipStream_t st) {
+static void launch_ref(const HsArgs &ka, int grid, hipStream_t st) {
   launch_set<NI, HM_MAIN>(ka, (ka.n + NI - 1) / NI, st);
-  // the deferred launch, enqueued blind (its counts are on the device): a
-  // fixed grid that grid-strides over the deferred items
-  const int64_t g = min(ka.n, (int64_t)MRAFT_AE_DGRID);
+  // the deferred launch, enqueued blind (its counts are on the device), on the
+  // host's grid (from the last call's deferred count) that grid-strides over
+  // the deferred items
+  const int64_t g = max((int64_t)1, min(ka.n, (int64_t)grid));
   hipLaunchKernelGGL(k_handle_deferred, dim3((unsigned)g), dim3(64), 0, st, ka);
 }
 
 void launch_handle_ae_ref(const Dev &s, const mraft_ae_args *args, int64_t n, int ni, const unsigned long long *claim,
                           const uint32_t *srcmark, uint32_t epoch, int32_t *err, const uint8_t *sethd, int64_t *soff,
-                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap, int32_t *kin,
-                          int32_t *kq, int32_t *cyc, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st) {
+                          int64_t *defer, unsigned long long *total, int32_t *stage, int64_t stage_cap,
+                          const AeDeferBufs &db, mraft_ae_reply *rep, mraft_ae_result *res, hipStream_t st) {
   if (n <= 0) return;
-  const HsArgs ka{s,     args,  n,     nullptr, 0,   stage, stage_cap, soff, sethd, defer, total,
-                  claim, srcmark, epoch, kin,   kq,  cyc,   rep,       err,  res};
+  HsArgs ka{};
+  ka.s = s; ka.args = args; ka.n = n; ka.ent0 = nullptr; ka.n_ent0 = 0; ka.stage = stage; ka.stage_cap = stage_cap;
+  ka.soff = soff; ka.sethd = sethd; ka.defer = defer; ka.total = total; ka.claim = claim; ka.srcmark = srcmark;
+  ka.epoch = epoch; ka.fb = db.fb; ka.kin = db.kin;
+  ka.cslot = db.cslot; ka.nslot = db.nslot; ka.cyc = db.cyc; ka.hint = db.hint; ka.rep = rep; ka.err = err;
+  ka.res = res;
   switch (ni) {
-    case 1: launch_ref<1>(ka, st); break;
-    case 2: launch_ref<2>(ka, st); break;
-    case 3: launch_ref<3>(ka, st); break;
-    case 4: launch_ref<4>(ka, st); break;
-    case 5: launch_ref<5>(ka, st); break;
-    case 6: launch_ref<6>(ka, st); break;
-    default: launch_ref<7>(ka, st);
+    case 1: launch_ref<1>(ka, db.grid, st); break;
+    case 2: launch_ref<2>(ka, db.grid, st); break;
+    case 3: launch_ref<3>(ka, db.grid, st); break;
+    case 4: launch_ref<4>(ka, db.grid, st); break;
+    case 5: launch_ref<5>(ka, db.grid, st); break;
+    case 6: launch_ref<6>(ka, db.grid, st); break;
+    default: launch_ref<7>(ka, db.grid, st);
   }
 }
 
 void launch_handle_ae_host(const Dev &s, const mraft_ae_args *args, int64_t n, const int32_t *ent, int64_t n_ent,
                            mraft_ae_reply *rep, int32_t *err, mraft_ae_result *res, hipStream_t st) {
   if (n <= 0) return;
-  const HsArgs ka{s,       args,    n, ent,     n_ent,   nullptr, 0,   nullptr, nullptr, nullptr, nullptr,
-                  nullptr, nullptr, 0, nullptr, nullptr, nullptr, rep, err,     res};
+  HsArgs ka{};
+  ka.s = s; ka.args = args; ka.n = n; ka.ent0 = ent; ka.n_ent0 = n_ent; ka.rep = rep; ka.err = err; ka.res = res;
   launch_set<1, HM_HOST>(ka, n, st);
 }
 

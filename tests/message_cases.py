@@ -3,7 +3,7 @@ gather -> handle -> fold path a host drives for network-delivered batches
 (include/mraft.h; raft_append_entry.go:20-162)."""
 import numpy as np
 
-from multiraft_amd._abi import AE_RESULT, LEADER
+from multiraft_amd._abi import AE_ARGS, AE_RESULT, LEADER
 from multiraft_amd.engine import entry_positions
 
 
@@ -151,3 +151,66 @@ def top_offset(st, j=0):
     (include/mraft.h: nextIndex = Index + 1 must be an int32)."""
     hi = max(int(st["last_index"].max()), int(st["next_index"].max()) - 1)
     return (2**31 - 2 - j) - hi
+
+
+def deferred_graph_state(G, P, L, rng, c=None):
+    """Every replica a follower at term 5 with one common log prefix
+    (Index 0 .. c) and its own suffix of non-decreasing terms up to a random
+    last Index: an AppendEntries at prev = c (prevLogTerm = the prefix's term)
+    from ANY replica's row matches at every receiver and merges that row's
+    suffix — real writes, whatever rows the batch wires together."""
+    n = G * P
+    c = c if c is not None else L // 4
+    st = {k: np.zeros(n, np.int32) for k in ("current_term", "voted_for", "state", "commit_index", "last_applied",
+                                            "dummy_index", "last_index", "granted_votes", "persist_dirty",
+                                            "log_head", "has_snapshot", "terms_sorted")}
+    st["current_term"][:] = 5
+    st["voted_for"][:] = -1
+    st["state"][:] = 3  # Follower
+    st["last_index"][:] = rng.integers(c + 1, L, size=n)
+    st["commit_index"][:] = rng.integers(0, c + 1, size=n)
+    st["last_applied"][:] = st["commit_index"]
+    st["terms_sorted"][:] = 1
+    st["match_index"] = np.zeros(n * P, np.int32)
+    st["next_index"] = np.zeros(n * P, np.int32)
+    log = np.zeros((n, L), np.int32)
+    prefix = np.sort(rng.integers(1, 3, size=c + 1)).astype(np.int32)
+    prefix[0] = 0
+    log[:, :c + 1] = prefix
+    for s in range(n):
+        last = int(st["last_index"][s])
+        log[s, c + 1:last + 1] = np.sort(rng.integers(3, 6, size=last - c))
+    st["log_term"] = log.reshape(-1)
+    return st, c
+
+
+def deferred_graph_batch(st, G, P, L, c, rng, n_items, long_cycle=0, self_refs=0):
+    """n_items AppendEntries by reference at distinct receiving slots, each
+    reading the suffix of a random replica's row (entries_offset = that row,
+    Index c+1 on): the rows read and written form a random functional graph —
+    trees, chains and cycles of deferred items (an item whose slot another
+    item reads is deferred; one whose source row another item writes is
+    staged). Optionally one explicit cycle of `long_cycle` items (longer than
+    the fallback's walk) and `self_refs` items reading their own row."""
+    n = G * P
+    recv = rng.permutation(n)[:n_items]
+    src = rng.integers(0, n, size=n_items)
+    # sources mostly among the receivers: many deferred items
+    among = rng.random(n_items) < 0.8
+    src[among] = recv[rng.integers(0, n_items, size=int(among.sum()))]
+    if long_cycle:
+        k = long_cycle
+        src[:k] = np.roll(recv[:k], -1)   # item j reads the row item j+1 writes: one k-cycle
+    if self_refs:
+        src[k if long_cycle else 0:][:self_refs] = recv[k if long_cycle else 0:][:self_refs]
+    a = np.zeros(n_items, dtype=AE_ARGS)
+    a["slot"] = recv
+    a["term"] = 9
+    a["leader_id"] = (recv + 1) % P
+    a["prev_log_index"] = c
+    a["prev_log_term"] = st["log_term"].reshape(n, L)[0, c]
+    a["n_entries"] = st["last_index"][src] - c
+    a["leader_commit"] = c
+    a["flags"] = 1
+    a["entries_offset"] = src.astype(np.int64) * L + (c + 1)
+    return a

@@ -15,7 +15,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 
 VARIANTS = {
     "mraft_tick.hip": ["-DMRAFT_TICK_MINW=6", "-DMRAFT_TICK_CMP_EPL=2", "-DMRAFT_TICK_SCANU=4", "-DMRAFT_TICK_TRACE=1"],
-    "mraft_kernels.hip": ["-DMRAFT_FOLD_GRID=1", "-DMRAFT_AE_DGRID=1", "-DMRAFT_FOLD_TAIL_NL=1",
+    "mraft_kernels.hip": ["-DMRAFT_FOLD_GRID=1", "-DMRAFT_FOLD_TAIL_NL=1",
                           "-DMRAFT_FOLD_TAIL_NS=1"],
 }
 
