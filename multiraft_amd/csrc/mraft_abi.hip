@@ -265,6 +265,16 @@ int scratch(mraft_engine *h, size_t idx, size_t bytes, void **out) {
   return MRAFT_OK;
 }
 
+// scratch() whose new buffer is zeroed when it is (re)allocated (stream-ordered):
+// for epoch-tagged counters, whose stale contents must never carry a tag a
+// later call could take for its own.
+int scratch_zeroed(mraft_engine *h, size_t idx, size_t bytes, void **out) {
+  const bool grows = h->scratch_ptr.size() <= idx || h->scratch_cap[idx] < (bytes ? bytes : 16);
+  TRY(scratch(h, idx, bytes, out));
+  if (grows) HIP_TRY(hipMemsetAsync(*out, 0, h->scratch_cap[idx], h->stream));
+  return MRAFT_OK;
+}
+
 // Batch pointer staging: for MRAFT_HOST, input buffers are copied to device
 // scratch and output buffers are copied back by finish().
 struct Stage {
@@ -309,9 +319,11 @@ int ensure_claim(mraft_engine *h) {
     h->srcmark = (uint32_t *)m;
     HIP_TRY(hipMemsetAsync(h->srcmark, 0, (size_t)gp_of(h) * sizeof(uint32_t), h->stream));
   }
-  if (++h->epoch == 0) {  // wrapped: reset
+  if (++h->epoch == 0) {  // wrapped: reset (and every epoch-tagged counter)
     HIP_TRY(hipMemsetAsync(h->claim, 0, (size_t)gp_of(h) * sizeof(unsigned long long), h->stream));
     HIP_TRY(hipMemsetAsync(h->srcmark, 0, (size_t)gp_of(h) * sizeof(uint32_t), h->stream));
+    if (h->scratch_ptr.size() > 20 && h->scratch_ptr[20])
+      HIP_TRY(hipMemsetAsync(h->scratch_ptr[20], 0, h->scratch_cap[20], h->stream));
     h->epoch = 1;
   }
   return MRAFT_OK;
@@ -664,10 +676,12 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   // the fallback's per-item records and reader counts, its L-word buffer and
   // nslot cycle buffers
   const size_t nn = (size_t)n, L = (size_t)h->L;
-  TRY(scratch(h, 19, nn * (16 + 8) + (1 + (size_t)db.nslot) * L * 4, &order));
+  TRY(scratch(h, 19, nn * 16 + (1 + (size_t)db.nslot) * L * 4, &order));
+  void *kin = nullptr;
+  TRY(scratch_zeroed(h, 20, nn * 8, &kin));  // epoch-tagged: a buffer of its own, zeroed when new
   db.fb = (int4 *)order;
-  db.kin = (unsigned long long *)(db.fb + nn);
-  db.cyc = (int32_t *)(db.kin + nn);
+  db.kin = (unsigned long long *)kin;
+  db.cyc = (int32_t *)(db.fb + nn);
   db.cslot = db.cyc + L;
   db.hint = h->dhint_dev;
   // the stage: when it cannot be allocated the batch runs with none (every
