@@ -243,6 +243,219 @@ def message_path(master, copies, lp, G, P, L, dev, S, steps, words=False, offset
     return out
 
 
+def deferred_batch_state(host, lp, G, P, L, kind, seed=0xDEF):
+    """Config #3's state with a stale second leader q = (lp + 1) % P in every
+    other group, and the batch a node receives then: every
+    real leader's AppendEntries to its P - 1 followers plus one from each stale
+    leader, to r = (lp + 2) % P ("stale": lp -> q is `written`, q's row being
+    read by q -> r: deferred, in place) or to lp itself ("cycles": lp -> q and
+    q -> lp each read the row the other rewrites: a 2-cycle, both staged, past
+    the stage capacity the fallback's cycles). q is a Leader one term below
+    lp with nextIndex[target] inside its log. Returns (state, slots, peers)."""
+    rng = np.random.default_rng(seed)
+    st = {k: v.copy() for k, v in host.items()}
+    g = np.arange(0, G, 2)
+    g = g[lp[g] >= 0]
+    l = lp[g].astype(np.int64)
+    q, r = (l + 1) % P, (l + 2) % P
+    ls, qs = g * P + l, g * P + q
+    st["state"][qs] = 1  # Leader
+    st["current_term"][qs] = np.maximum(1, st["current_term"][ls] - 1)
+    tgt = l if kind == "cycles" else r
+    d, last = st["dummy_index"][qs].astype(np.int64), st["last_index"][qs].astype(np.int64)
+    st["next_index"][qs * P + tgt] = rng.integers(d + 1, last + 2)
+    lq = np.where(lp >= 0)[0]
+    ldr = (lq * P + lp[lq]).repeat(P - 1)
+    k = np.tile(np.arange(P - 1), len(lq))
+    fp = np.where(k < np.repeat(lp[lq], P - 1), k, k + 1)
+    if kind != "cycles":
+        # r receives from q instead of from lp (one message per receiving
+        # slot, include/mraft.h): the batch keeps the plain batch's size
+        drop = np.zeros(G, bool)
+        drop[g] = True
+        keep = ~(drop[ldr // P] & (fp == np.repeat(np.where(drop, (lp + 2) % P, -1)[lq], P - 1)))
+        ldr, fp = ldr[keep], fp[keep]
+    slots = np.concatenate([ldr, qs]).astype(np.int32)
+    peers = np.concatenate([fp, tgt]).astype(np.int32)
+    return st, slots, peers
+
+
+def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
+    """The handle call (mraft_handle_append_entries_ex by reference) on config
+    #3 batches heavy in deferred items (deferred_batch_state), against the
+    plain batch on the same copies: per call, and per message. Each variant on
+    a fresh engine: its first call runs on the minimal deferred grid (no
+    earlier count: `first_call_ms`), then `steps` timed calls, each on a state
+    copy restored from that variant's master (one event before and one after
+    the handle call)."""
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, _abi
+    lib = _abi.lib()
+    host = {k: v.cpu().numpy() for k, v in master.items()}
+    dm = {k: v.clone() for k, v in master.items()}
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+    out = {}
+    lq = np.where(lp >= 0)[0]
+    plain_slots = (lq * P + lp[lq]).repeat(P - 1).astype(np.int32)
+    kk = np.tile(np.arange(P - 1), len(lq))
+    plain_peers = np.where(kk < np.repeat(lp[lq], P - 1), kk, kk + 1).astype(np.int32)
+    variants = [("plain", None, None), ("stale", "stale", None), ("stale_stage0", "stale", 0),
+                ("cycles", "cycles", None), ("cycles_stage0", "cycles", 0)]
+    for name, kind, cap in variants:
+        if kind is None:
+            st_h, slots, peers = host, plain_slots, plain_peers
+        else:
+            st_h, slots, peers = deferred_batch_state(host, lp, G, P, L, kind)
+        for kx, v in st_h.items():
+            dm[kx].copy_(torch.from_numpy(v))
+        n = len(slots)
+        sl_d, pe_d = torch.from_numpy(slots).to(dev), torch.from_numpy(peers).to(dev)
+        args, gerr, herr, rep, res = z(n, 10), z(n), z(n), z(n, 4), z(n, 8)
+        e = Engine(G, P, L, device=dev.index or 0, alloc=False, dedicated_queue=True)
+        st = torch.cuda.ExternalStream(e.stream(), device=dev)
+        if cap is not None:
+            assert lib.mraft_set_stage_capacity(e._h, cap) == 0
+        times = []
+        ndef = 0
+        for i in range(steps + 1):
+            c = copies[i]
+            for kx, v in dm.items():
+                c[kx].copy_(v)
+            torch.cuda.synchronize()
+            e.bind(c)
+            assert lib.mraft_gather_append_args(e._h, sl_d.data_ptr(), pe_d.data_ptr(), n, args.data_ptr(),
+                                                gerr.data_ptr(), DEVICE) == 0, _abi.last_error()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            assert lib.mraft_handle_append_entries_ex(e._h, args.data_ptr(), n, None, 0, rep.data_ptr(),
+                                                      res.data_ptr(), herr.data_ptr(), DEVICE) == 0, \
+                _abi.last_error()
+            b.record(st)
+            e.synchronize()
+            times.append(a.elapsed_time(b))
+            if i == 0:
+                ah = args.cpu().numpy().view(_abi.AE_ARGS).reshape(-1)
+                ok = gerr.cpu().numpy() == 0
+                src = np.where(ok & (ah["n_entries"] > 0), ah["entries_offset"] // L, -1)
+                ndef = int((ok & np.isin(ah["slot"], src[src >= 0])).sum())
+                assert ok.all(), f"{name}: gather errors"
+        e.close()
+        out[name] = {"messages": n, "deferred_items": ndef, "stage_capacity_words": cap if cap is not None else
+                     "default (4 Mi)", "first_call_ms": times[0], "ms_per_call": float(np.mean(times[1:])),
+                     "ns_per_message": float(np.mean(times[1:])) * 1e6 / n}
+    base = out["plain"]
+    for name in out:
+        if name != "plain":
+            out[name]["vs_plain"] = out[name]["ms_per_call"] / base["ms_per_call"]
+            out[name]["per_message_vs_plain"] = out[name]["ns_per_message"] / base["ns_per_message"]
+    del dm
+    torch.cuda.empty_cache()
+    return out
+
+
+def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
+    """Config #3 ticked in place: one state copy, and per
+    step a Start of 1-4 entries at every leader (mraft_start, raft.go:90-104)
+    then one mraft_replicate_tick — a heartbeat / append round of a running
+    deployment, where followers are caught up after the first rounds. All
+    calls enqueued back to back on one engine stream (one launch per tick, no
+    shards), an event before and after each call; a second pass on a fresh copy
+    interleaves mraft_replicate_tick_count before each tick (side-effect free)
+    for the algorithmic bytes; and the floor of a launch that does no group's
+    work (leader_peer -1 everywhere: every wave exits after one load)."""
+    import torch
+
+    from multiraft_amd import DEVICE, Engine, _abi
+    lib = _abi.lib()
+    rng = np.random.default_rng(seed)
+    lq = np.where(lp >= 0)[0]
+    ldr = torch.from_numpy((lq * P + lp[lq]).astype(np.int32)).to(dev)
+    nl = len(lq)
+    cnts = [torch.from_numpy(rng.integers(1, 5, size=nl).astype(np.int32)).to(dev) for _ in range(steps)]
+    oi, ot, ol, oe = (torch.zeros(nl, dtype=torch.int32, device=dev) for _ in range(4))
+    lp_d = torch.from_numpy(lp.astype(np.int32)).to(dev)
+    gf = torch.zeros(G, dtype=torch.int32, device=dev)
+    c = copies[0]
+    e = Engine(G, P, L, device=dev.index or 0, alloc=False, dedicated_queue=True)
+    st = torch.cuda.ExternalStream(e.stream(), device=dev)
+    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+
+    def restore():
+        for k, v in master.items():
+            c[k].copy_(v)
+        torch.cuda.synchronize()
+        e.bind(c)
+
+    def start(k):
+        assert lib.mraft_start(e._h, ldr.data_ptr(), cnts[k].data_ptr(), nl, oi.data_ptr(), ot.data_ptr(),
+                               ol.data_ptr(), oe.data_ptr(), DEVICE) == 0, _abi.last_error()
+
+    # timed pass
+    restore()
+    marks = [[ev() for _ in range(3)] for _ in range(steps)]
+    for k in range(steps):
+        marks[k][0].record(st)
+        start(k)
+        marks[k][1].record(st)
+        e.replicate_tick(lp_d, gf, where=DEVICE)
+        marks[k][2].record(st)
+    e.synchronize()
+    start_ms = [m[0].elapsed_time(m[1]) for m in marks]
+    tick_ms = [m[1].elapsed_time(m[2]) for m in marks]
+    span_ms = marks[0][0].elapsed_time(marks[-1][2])
+    flags = gf.cpu().numpy()
+    log_full = int((oe.cpu().numpy() == 3).sum())
+    # count pass (same sequence, the count before each tick)
+    restore()
+    words = np.zeros((steps, 3), np.int64)
+    for k in range(steps):
+        start(k)
+        words[k] = e.replicate_tick_count(lp)
+        e.replicate_tick(lp_d, gf, where=DEVICE)
+    e.synchronize()
+    # a launch with no group's work
+    none = torch.full((G,), -1, dtype=torch.int32, device=dev)
+    empty = []
+    for _ in range(5):
+        a, b = ev(), ev()
+        a.record(st)
+        e.replicate_tick(none, gf, where=DEVICE)
+        b.record(st)
+        e.synchronize()
+        empty.append(a.elapsed_time(b))
+    e.close()
+    # steady state: the steps after the first two (the synthetic state's backlog merges there)
+    ss = slice(2, steps)
+    tick_ss = float(np.mean(tick_ms[ss]))
+    bytes_ss = float(np.mean(4 * (words[ss, 0] + words[ss, 1])))
+    act_ss = float(np.mean(words[ss, 2]))
+    span_ss = marks[2][0].elapsed_time(marks[-1][2]) / (steps - 2)
+    empty_ms = float(np.median(empty))
+    return {"workload": "config #3 ticked in place: per step mraft_start of 1-4 entries at each of the %d leaders, "
+                        "then one mraft_replicate_tick (one launch, no shards), %d steps back to back on one "
+                        "engine stream; steady state = steps 3..%d" % (nl, steps, steps),
+            "steps": steps, "tick_ms_steps": [round(x, 4) for x in tick_ms],
+            "start_ms_mean": float(np.mean(start_ms)),
+            "tick_ms_steady": tick_ss, "device_ms_per_step_steady": span_ss,
+            "decisions_per_s_steady": G / (span_ss / 1e3),
+            "tick_decisions_per_s_steady": G / (tick_ss / 1e3),
+            "algorithmic_bytes_per_tick_steady": bytes_ss,
+            "algorithmic_bytes_per_decision_steady": bytes_ss / max(act_ss, 1.0),
+            "tick_achieved_GBps_steady": bytes_ss / tick_ss / 1e6,
+            "tick_hbm_frac_steady": bytes_ss / (tick_ss / 1e3) / HBM_PEAK,
+            "first_tick_ms": tick_ms[0], "first_tick_algorithmic_bytes": int(4 * (words[0, 0] + words[0, 1])),
+            "empty_launch_ms": empty_ms,
+            "launch_share_of_tick_steady": empty_ms / tick_ss,
+            "launch_share_what": "a tick launch over the same 65,536 groups with no leader (each wave loads "
+                                 "leader_peer and exits) over the steady-state tick: the part of a steady tick a "
+                                 "launch with no work already costs",
+            "gaps_share_steady": 1.0 - (float(np.sum(tick_ms[ss])) + float(np.sum(start_ms[ss]))) /
+                                 (span_ss * (steps - 2)),
+            "start_log_full_last_step": log_full,
+            "groups_committed_last_step": int(((flags & 2) != 0).sum())}
+
+
 def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     """The survey's other configurations, measured in the same run so they are
     on the driver's record (rank 0, one GPU, after the headline's timed
@@ -315,6 +528,20 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
                                   "settles the range (currentTerm, or below it on a replica whose terms_sorted "
                                   "proof holds: include/mraft.h), Go's downward scan; k_fold folds the replies and "
                                   "probes each range's top word, k_fold_tail scans the ranges the probes left open"}}
+
+    # -- steady state: config #3 ticked in place with Start between ticks
+    out["steady_state_config3"] = steady_state(master, copies, lp, G, P, L, dev)
+
+    # -- deferred-heavy batches
+    md = message_path_deferred(master, copies, lp, G, P, L, dev)
+    out["message_path_deferred"] = {
+        "workload": "config #3 by reference with a stale second leader in every other group: the real leaders' "
+                    "262,144 AppendEntries with 32,768 from the stale leaders (stale: to another follower, in place "
+                    "of the real leader's message to it — 262,144 messages; each stale leader's row is read and "
+                    "written in the batch, so every lp -> q item is deferred; cycles: in addition, "
+                    "back to the real leader, 2-cycles of staged items, past the stage capacity the fallback's "
+                    "parallel cycles); the handle call alone, vs the plain 262,144-message batch",
+        **md}
 
     # -- config #5 election storm
     Ge, Pe, R = 65536, 7, 64

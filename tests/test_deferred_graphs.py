@@ -50,3 +50,25 @@ def test_graph_batches_have_the_shapes():
     src = a["entries_offset"] // L
     for r, s_ in zip(a["slot"], src):
         assert np.array_equal(log1[r, c + 1:st["last_index"][s_] + 1], log0[s_, c + 1:st["last_index"][s_] + 1])
+
+
+def test_bench_deferred_batches_shape():
+    """bench.py's deferred-heavy config #3 batches (secondary.message_path_deferred),
+    at a small size: every gather succeeds, every stale leader's receiver is
+    deferred (stale) or in a 2-cycle (cycles), and the oracle handles them."""
+    import bench
+    from multiraft_amd import synth_tick_state
+    G, P, L = 64, 5, 128
+    st, lp, _ = synth_tick_state(G, P, L, seed=710, nthreads=1)
+    for kind in ("stale", "cycles"):
+        st2, slots, peers = bench.deferred_batch_state(st, lp, G, P, L, kind)
+        o = Oracle(G, P, L, st2)
+        args, gerr = o.gather_append_args(slots, peers)
+        assert (gerr == 0).all(), kind
+        src = np.where(args["n_entries"] > 0, args["entries_offset"] // L, -1)
+        deferred = np.isin(args["slot"], src[src >= 0])
+        n_stale = int(((lp[::2]) >= 0).sum())
+        assert deferred.sum() >= n_stale * (2 if kind == "cycles" else 1) - 2, kind
+        rep, err = o.handle_append_entries(args, None)
+        assert (err == 0).all() and (rep["success"] == 1).any(), kind
+        assert len(slots) == (4 * int((lp >= 0).sum()) + (n_stale if kind == "cycles" else 0)), kind
