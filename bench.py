@@ -314,8 +314,6 @@ def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
         args, gerr, herr, rep, res = z(n, 10), z(n), z(n), z(n, 4), z(n, 8)
         e = Engine(G, P, L, device=dev.index or 0, alloc=False, dedicated_queue=True)
         st = torch.cuda.ExternalStream(e.stream(), device=dev)
-        if cap is not None:
-            assert lib.mraft_set_stage_capacity(e._h, cap) == 0
         times = []
         ndef = 0
         for i in range(steps + 1):
@@ -324,6 +322,8 @@ def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
                 c[kx].copy_(v)
             torch.cuda.synchronize()
             e.bind(c)
+            if cap is not None and i == 0:  # (a bound engine: the call checks the state)
+                assert lib.mraft_set_stage_capacity(e._h, cap) == 0, _abi.last_error()
             assert lib.mraft_gather_append_args(e._h, sl_d.data_ptr(), pe_d.data_ptr(), n, args.data_ptr(),
                                                 gerr.data_ptr(), DEVICE) == 0, _abi.last_error()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -16,6 +16,10 @@
 #include "mraft_device.h"
 #include "mraft_internal.h"
 
+#ifndef MRAFT_ELECT_LOOP
+#define MRAFT_ELECT_LOOP 1  // the RequestVote delivery loop's form (2: the do-while variant under A/B)
+#endif
+
 namespace mraft {
 
 namespace {
@@ -91,6 +95,28 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     const unsigned long long cb = __ballot(isc);
     int cm = (int)((cb >> seg) & 0xffull);
     pd |= (int)(act && (cm & ~(1 << p)) != 0);                         // :57, every RV this voter handles
+#if MRAFT_ELECT_LOOP == 2
+    // (variant: a do-while on the candidates with c = 8 once a segment is
+    // done — c <= p and upm's bit c are then false by themselves — votedFor
+    // and the step-down carried as term > at after the loop)
+    if (__ballot(cm != 0)) {
+      do {
+        const int c = __builtin_ctz((unsigned)cm | 0x100u);
+        cm &= cm - 1;
+        const int cat = __shfl(mycx, c & 7, 8);
+        pmx = c <= p ? max(pmx, cat) : pmx;                            // (c = 8 > p)
+        const bool h = act && c < 8 && c != p;                         // this voter handles c's RV
+        const bool gt = h && cat > term;                               // :63-66
+        const bool ge = h && cat >= term;                              // :59-62 (stale: no change)
+        term = gt ? cat : term;
+        voted = gt ? -1 : voted;
+        const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
+        voted = grant ? c : voted;
+        gm |= grant ? (1 << c) : 0;
+      } while (__ballot(cm != 0));
+    }
+    role = term > at ? kFollower : role;                               // :63-66 (some RV carried a higher term)
+#else
     // until every segment of the wave has walked its candidates (the ballot is
     // scalar: no cross-lane max of the counts)
     while (__ballot(cm != 0)) {
@@ -111,6 +137,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       voted = grant ? c : voted;
       gm |= (int)grant << c;
     }
+#endif
     // Grants transposed through LDS: byte v of the segment's word = voter v's
     // grant mask; bit v of mine = voter v granted this lane.
     int mine = 0;
