@@ -31,7 +31,7 @@ constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
 constexpr int kDeferGridMin = 8;
 constexpr int kDeferGridMax = 1 << 16;
 // Words of the fallback's per-workgroup cycle buffers (nslot x L, at most this).
-constexpr int64_t kCycSlotWords = (int64_t)1 << 24;
+constexpr int64_t kCycSlotWords = (int64_t)1 << 25;  // 8,192 buffers at L = 4,096 (128 MiB)
 
 struct mraft_engine {
   int32_t G = 0, P = 0, L = 0, device = 0;

@@ -17,7 +17,7 @@
 #include "mraft_internal.h"
 
 #ifndef MRAFT_ELECT_LOOP
-#define MRAFT_ELECT_LOOP 1  // the RequestVote delivery loop's form (2: the do-while variant under A/B)
+#define MRAFT_ELECT_LOOP 1  // the RequestVote delivery loop's form (3: ranked candidates in registers, under A/B)
 #endif
 
 namespace mraft {
@@ -55,6 +55,10 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
   __shared__ int lds_cx[256];
   __shared__ __attribute__((aligned(8))) uint8_t lds_gm[256];
+#if MRAFT_ELECT_LOOP == 3
+  __shared__ int lds_rt[256];                                  // rank k's args.Term, per segment
+  __shared__ __attribute__((aligned(8))) uint8_t lds_rc[256];  // rank k's peer index
+#endif
   const int seg = (int)(threadIdx.x & 63) & ~7;
   int fl = 0, became = 0, pd = 0;  // pd: persist() ran (StartElection :15, HandleRequestVote :57, :45)
   // The round's timeout mask, loaded one round ahead. (Staging 64 rounds of
@@ -95,17 +99,32 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     const unsigned long long cb = __ballot(isc);
     int cm = (int)((cb >> seg) & 0xffull);
     pd |= (int)(act && (cm & ~(1 << p)) != 0);                         // :57, every RV this voter handles
-#if MRAFT_ELECT_LOOP == 2
-    // (variant: a do-while on the candidates with c = 8 once a segment is
-    // done — c <= p and upm's bit c are then false by themselves — votedFor
-    // and the step-down carried as term > at after the loop)
-    if (__ballot(cm != 0)) {
-      do {
-        const int c = __builtin_ctz((unsigned)cm | 0x100u);
-        cm &= cm - 1;
-        const int cat = __shfl(mycx, c & 7, 8);
-        pmx = c <= p ? max(pmx, cat) : pmx;                            // (c = 8 > p)
-        const bool h = act && c < 8 && c != p;                         // this voter handles c's RV
+#if MRAFT_ELECT_LOOP == 3
+    // (variant under A/B: the segment's candidates ranked in peer order, rank
+    // k's args.Term and peer index staged through LDS once per round and held
+    // in registers, so the delivery loop has no LDS round trip per candidate
+    // and a compile-time register index per iteration)
+    {
+      const int ncand = __builtin_popcount(cm);
+      if (isc) {
+        const int rk = __builtin_popcount(cm & ((1 << p) - 1));
+        lds_rt[(threadIdx.x & ~7u) + rk] = at;
+        lds_rc[(threadIdx.x & ~7u) + rk] = (uint8_t)p;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int4 ra = *reinterpret_cast<const int4 *>(&lds_rt[threadIdx.x & ~7u]);
+      const int4 rb = *reinterpret_cast<const int4 *>(&lds_rt[(threadIdx.x & ~7u) + 4]);
+      const unsigned long long rcs = *reinterpret_cast<const unsigned long long *>(&lds_rc[threadIdx.x & ~7u]);
+      __builtin_amdgcn_wave_barrier();
+      const int rt[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+#pragma unroll
+      for (int k = 0; k < P; ++k) {
+        if (!__ballot(k < ncand)) break;
+        const bool valid = k < ncand;
+        const int c = (int)((rcs >> (8 * k)) & 0xffull);
+        const int cat = rt[k];
+        pmx = (valid && c <= p) ? max(pmx, cat) : pmx;
+        const bool h = act && valid && c != p;                         // this voter handles c's RV
         const bool gt = h && cat > term;                               // :63-66
         const bool ge = h && cat >= term;                              // :59-62 (stale: no change)
         term = gt ? cat : term;
@@ -113,9 +132,9 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
         const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
         voted = grant ? c : voted;
         gm |= grant ? (1 << c) : 0;
-      } while (__ballot(cm != 0));
+      }
+      role = term > at ? kFollower : role;                             // :63-66 (some RV carried a higher term)
     }
-    role = term > at ? kFollower : role;                               // :63-66 (some RV carried a higher term)
 #else
     // until every segment of the wave has walked its candidates (the ballot is
     // scalar: no cross-lane max of the counts)

@@ -943,7 +943,11 @@ __device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd) {
 }
 
 __device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd) {
-  for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) {
+  // only workgroups with a cycle buffer take items (any of them may complete
+  // a cycle and must run it: r6_v6 ran 28k of 32k 2-cycles on the last
+  // workgroup when the grid was 16x the buffers); the others only count out
+  const int64_t nb = min((int64_t)gridDim.x, (int64_t)max(k.nslot, 1));
+  for (int64_t j = blockIdx.x; (int64_t)blockIdx.x < nb && j < nd; j += nb) {
     const int64_t x = k.defer[j];
     if (tag_count(&k.kin[x], k.epoch) == 0) {
       fb_chain(k, x);  // no deferred item reads x's row: a chain starts here
