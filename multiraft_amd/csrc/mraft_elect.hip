@@ -10,15 +10,15 @@
 // Round 5 (profiles/r5_e1 README): one lane per group, two lanes per group,
 // a dense voter loop, a branch-free vote-key loop and LDS-staged round masks
 // were all measured (parity green) and all slower; this layout hides its
-// dependent chains with 8 waves per SIMD, and its branchy sparse loop skips
-// the grant evaluation where `a >= term` fails. The alternatives' compile-time
-// knobs are gone (the ISA of this kernel is unchanged by their removal).
+// dependent chains with 8 waves per SIMD. Round 6 (profiles/r6_e1): the
+// instruction account of the round body matched the counters exactly (84 VALU
+// + 19 SALU per wave-round plus 29 + 13 per candidate, 3.0 candidates per
+// wave-round), fewer instructions per candidate alone changed nothing, and
+// taking the per-candidate LDS round trip out of the delivery loop's
+// dependent chain (candidates ranked once per round, held in registers) took
+// the storm 9 % down.
 #include "mraft_device.h"
 #include "mraft_internal.h"
-
-#ifndef MRAFT_ELECT_LOOP
-#define MRAFT_ELECT_LOOP 1  // the RequestVote delivery loop's form (3: ranked candidates in registers, under A/B)
-#endif
 
 namespace mraft {
 
@@ -55,10 +55,8 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
   __shared__ int lds_cx[256];
   __shared__ __attribute__((aligned(8))) uint8_t lds_gm[256];
-#if MRAFT_ELECT_LOOP >= 3
   __shared__ int lds_rt[256];                                  // rank k's args.Term, per segment
   __shared__ __attribute__((aligned(8))) uint8_t lds_rc[256];  // rank k's peer index
-#endif
   const int seg = (int)(threadIdx.x & 63) & ~7;
   int fl = 0, became = 0, pd = 0;  // pd: persist() ran (StartElection :15, HandleRequestVote :57, :45)
   // The round's timeout mask, loaded one round ahead. (Staging 64 rounds of
@@ -77,7 +75,6 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     }
     const int at = term;  // args.Term of this lane's RequestVote (when isc); voter's term before RVs
     int cx[8];
-#if MRAFT_ELECT_LOOP < 4
     // One broadcast per replica per round, through this wave's LDS words: its
     // term with the candidate bit on top.
     const int mycx = at;
@@ -89,64 +86,22 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       cx[0] = a.x; cx[1] = a.y; cx[2] = a.z; cx[3] = a.w;
       cx[4] = b.x; cx[5] = b.y; cx[6] = b.z; cx[7] = b.w;
     }
-#endif
     // RequestVote deliveries: voter p handles the candidates in peer order
     // (HandleRequestVote :54-77). pmx = max args.Term over candidates c <= p,
     // which with the voter's own pre-delivery term gives every reply.Term the
     // tally below needs (a voter's term after handling c is the max of the
     // two, the stale branch included).
     int gm = 0, pmx = INT32_MIN;
-    // Only the candidates: the k-th set bit of the group's candidate mask, for
-    // k below the wave's largest candidate count (ascending peer order kept).
+    // The segment's candidate mask (ascending peer order is the delivery order).
     const unsigned long long cb = __ballot(isc);
-    int cm = (int)((cb >> seg) & 0xffull);
+    const int cm = (int)((cb >> seg) & 0xffull);
     pd |= (int)(act && (cm & ~(1 << p)) != 0);                         // :57, every RV this voter handles
-#if MRAFT_ELECT_LOOP >= 4
-    // (variant under A/B: variant 3 with the broadcast of every replica's term
-    // (peer order, the tally's) and the candidates' ranked terms (the
-    // deliveries') written and read in one LDS phase per round)
-    {
-      const int mycx = at;
-      const int ncand = __builtin_popcount(cm);
-      lds_cx[threadIdx.x] = mycx;
-      if (isc) {
-        const int rk = __builtin_popcount(cm & ((1 << p) - 1));
-        lds_rt[(threadIdx.x & ~7u) + rk] = at;
-        lds_rc[(threadIdx.x & ~7u) + rk] = (uint8_t)p;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const int4 a = *reinterpret_cast<const int4 *>(&lds_cx[threadIdx.x & ~7u]);
-      const int4 b = *reinterpret_cast<const int4 *>(&lds_cx[(threadIdx.x & ~7u) + 4]);
-      const int4 ra = *reinterpret_cast<const int4 *>(&lds_rt[threadIdx.x & ~7u]);
-      const int4 rb = *reinterpret_cast<const int4 *>(&lds_rt[(threadIdx.x & ~7u) + 4]);
-      const unsigned long long rcs = *reinterpret_cast<const unsigned long long *>(&lds_rc[threadIdx.x & ~7u]);
-      __builtin_amdgcn_wave_barrier();
-      cx[0] = a.x; cx[1] = a.y; cx[2] = a.z; cx[3] = a.w;
-      cx[4] = b.x; cx[5] = b.y; cx[6] = b.z; cx[7] = b.w;
-      const int rt[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-#pragma unroll
-      for (int k = 0; k < P; ++k) {
-        if (!__ballot(k < ncand)) break;
-        const bool valid = k < ncand;
-        const int c = (int)((rcs >> (8 * k)) & 0xffull);
-        const int cat = rt[k];
-        pmx = (valid && c <= p) ? max(pmx, cat) : pmx;
-        const bool h = act && valid && c != p;                         // this voter handles c's RV
-        const bool gt = h && cat > term;                               // :63-66
-        const bool ge = h && cat >= term;                              // :59-62 (stale: no change)
-        term = gt ? cat : term;
-        voted = gt ? -1 : voted;
-        const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
-        voted = grant ? c : voted;
-        gm |= grant ? (1 << c) : 0;
-      }
-      role = term > at ? kFollower : role;                             // :63-66 (some RV carried a higher term)
-    }
-#elif MRAFT_ELECT_LOOP == 3
-    // (variant under A/B: the segment's candidates ranked in peer order, rank
-    // k's args.Term and peer index staged through LDS once per round and held
-    // in registers, so the delivery loop has no LDS round trip per candidate
-    // and a compile-time register index per iteration)
+    // The segment's candidates ranked in peer order: rank k's args.Term and
+    // peer index staged through LDS once per round and held in registers, so
+    // the delivery loop has no LDS round trip per candidate and a compile-time
+    // register index per iteration (round 6: 0.164 -> 0.149 ms per storm;
+    // round 5's loop walked the candidate mask with a ds_bpermute per
+    // candidate in its dependent chain, profiles/r6_e1)
     {
       const int ncand = __builtin_popcount(cm);
       if (isc) {
@@ -178,28 +133,6 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       }
       role = term > at ? kFollower : role;                             // :63-66 (some RV carried a higher term)
     }
-#else
-    // until every segment of the wave has walked its candidates (the ballot is
-    // scalar: no cross-lane max of the counts)
-    while (__ballot(cm != 0)) {
-      const bool any = cm != 0;
-      const int c = any ? __builtin_ctz(cm) : 0;
-      cm &= cm - 1;
-      const int cxc = __shfl(mycx, c, 8);
-      const bool cisc = any;
-      const int cat = (cxc);
-      pmx = (cisc && c <= p) ? max(pmx, cat) : pmx;
-      const bool h = act && cisc && c != p;                            // this voter handles c's RV
-      const bool ge = h && cat >= term;                                // :59-62 (stale: no change)
-      const bool gt = h && cat > term;                                 // :63-66
-      term = gt ? cat : term;
-      role = gt ? kFollower : role;
-      voted = gt ? -1 : voted;
-      const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
-      voted = grant ? c : voted;
-      gm |= (int)grant << c;
-    }
-#endif
     // Grants transposed through LDS: byte v of the segment's word = voter v's
     // grant mask; bit v of mine = voter v granted this lane.
     int mine = 0;
@@ -228,14 +161,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       for (int k = 1; k < (P / 2 > 1 ? P / 2 : 1); ++k) mm &= mm - 1;  // the (P/2)-th grant
       const int lpos = mm ? __builtin_ctz(mm) : 32;
       const int spos = smask ? __builtin_ctz(smask) : 32;
-#if MRAFT_ELECT_LOOP >= 5
-      // (variant: the first refusing voter's term from cx[] by a select chain,
-      // not a dependent LDS read)
-#pragma unroll
-      for (int v = P - 1; v >= 0; --v) tv = ((smask >> v) & 1) ? cx[v] : tv;
-#else
       tv = lds_cx[(threadIdx.x & ~7u) + min(spos, 7)];  // used only when spos < P
-#endif
       const bool lead = ok0 && lpos < spos;
       const bool sd = ok0 && spos < lpos;
       const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
