@@ -418,8 +418,10 @@ __device__ __forceinline__ int at_load(int32_t *p) {
 __device__ __forceinline__ void at_store(int32_t *p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void phase_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+// This wave's own global stores complete before its next loads (a copy it
+// reads back): workgroup scope, no cache maintenance.
+__device__ __forceinline__ void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_s_waitcnt(0);
 }
 
@@ -878,7 +880,7 @@ __device__ __forceinline__ void fb_run_cycle(const HsArgs &k, int64_t b) {
   const int L = k.s.L;
   const int64_t row = a.entries_offset / L;
   wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L), buf, a.n_entries);
-  phase_fence();
+  wave_fence();  // this wave reads the copy back: a workgroup-scope fence (r6_v9: an agent-scope one per cycle, an L2 write-back each, cost 5 ms per 32k cycles)
   int64_t z = fb_writer(k, b);
   for (int st = 0; z >= 0 && z != b && st < kCycWalk; ++st, z = fb_writer(k, z)) fb_run(k, z, nullptr);
   fb_run(k, b, buf);
@@ -931,7 +933,7 @@ __device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd) {
       const int64_t row = a.entries_offset / L;
       if (a.n_entries > 0) wave_copy_from_ring(k.s.log + row * L, 0, k.s.head[row], L, (int)(a.entries_offset % L),
                                                k.cyc, a.n_entries);
-      phase_fence();
+      wave_fence();
       int64_t z = fb_writer(k, x);
       for (int64_t st = 0; z >= 0 && z != x && st < nd; ++st) {
         fb_run(k, z, nullptr);

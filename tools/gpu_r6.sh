@@ -40,6 +40,11 @@ for st in ${DO:-tests bench}; do
         done
       done
       unset MRAFT_LIB ;;
+    deferred)
+      # the deferred-heavy handle measurement alone (tools/bench_deferred.py)
+      echo "== deferred"
+      timeout -k 10 400 python3 tools/bench_deferred.py > "$OUT/deferred.json" 2> "$OUT/deferred.err" || { tail -5 "$OUT/deferred.err"; exit 1; }
+      python3 -c "import json; d=json.loads(open('$OUT/deferred.json').read().strip().splitlines()[-1]); [print(k, round(v['ms_per_call'], 4), round(v['first_call_ms'], 3), round(v.get('vs_plain', 1.0), 3)) for k, v in d.items()]" ;;
     abmsg)
       # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
       echo "== abmsg ${VARIANTS:-prebuilt}"
