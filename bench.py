@@ -359,14 +359,18 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     step a Start of 1-4 entries at every leader (mraft_start, raft.go:90-104)
     then one mraft_replicate_tick — a heartbeat / append round of a running
     deployment, where followers are caught up after the first rounds. All
-    calls enqueued back to back on one engine stream (one launch per tick, no
-    shards), an event before and after each call; a second pass on a fresh copy
-    interleaves mraft_replicate_tick_count before each tick (side-effect free)
-    for the algorithmic bytes; and the floor of a launch that does no group's
-    work (leader_peer -1 everywhere: every wave exits after one load)."""
+    calls enqueued back to back on one engine stream (no shards), an event
+    before and after each call, once with the full tick (one launch) and once
+    with the light tick (MRAFT_TICK_LIGHT: its two launches) on a second copy
+    of the same state, whose final state must equal the first's; a third pass
+    on a fresh copy interleaves mraft_replicate_tick_count before each tick
+    (side-effect free) for the algorithmic bytes, and a fourth runs the light
+    sequence with a host wait per step to read each tick's fallback count;
+    then the floor of a launch that does no group's work (leader_peer -1
+    everywhere: every wave exits after one load)."""
     import torch
 
-    from multiraft_amd import DEVICE, Engine, _abi
+    from multiraft_amd import DEVICE, TICK_FULL, TICK_LIGHT, Engine, _abi
     lib = _abi.lib()
     rng = np.random.default_rng(seed)
     lq = np.where(lp >= 0)[0]
@@ -376,12 +380,11 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     oi, ot, ol, oe = (torch.zeros(nl, dtype=torch.int32, device=dev) for _ in range(4))
     lp_d = torch.from_numpy(lp.astype(np.int32)).to(dev)
     gf = torch.zeros(G, dtype=torch.int32, device=dev)
-    c = copies[0]
     e = Engine(G, P, L, device=dev.index or 0, alloc=False, dedicated_queue=True)
     st = torch.cuda.ExternalStream(e.stream(), device=dev)
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
 
-    def restore():
+    def restore(c):
         for k, v in master.items():
             c[k].copy_(v)
         torch.cuda.synchronize()
@@ -391,29 +394,43 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
         assert lib.mraft_start(e._h, ldr.data_ptr(), cnts[k].data_ptr(), nl, oi.data_ptr(), ot.data_ptr(),
                                ol.data_ptr(), oe.data_ptr(), DEVICE) == 0, _abi.last_error()
 
-    # timed pass
-    restore()
-    marks = [[ev() for _ in range(3)] for _ in range(steps)]
-    for k in range(steps):
-        marks[k][0].record(st)
-        start(k)
-        marks[k][1].record(st)
-        e.replicate_tick(lp_d, gf, where=DEVICE)
-        marks[k][2].record(st)
-    e.synchronize()
-    start_ms = [m[0].elapsed_time(m[1]) for m in marks]
-    tick_ms = [m[1].elapsed_time(m[2]) for m in marks]
-    span_ms = marks[0][0].elapsed_time(marks[-1][2])
-    flags = gf.cpu().numpy()
+    def timed(mode, c):
+        restore(c)
+        e.set_tick_mode(mode)
+        marks = [[ev() for _ in range(3)] for _ in range(steps)]
+        for k in range(steps):
+            marks[k][0].record(st)
+            start(k)
+            marks[k][1].record(st)
+            e.replicate_tick(lp_d, gf, where=DEVICE)
+            marks[k][2].record(st)
+        e.synchronize()
+        return ([m[0].elapsed_time(m[1]) for m in marks], [m[1].elapsed_time(m[2]) for m in marks],
+                marks[2][0].elapsed_time(marks[-1][2]) / (steps - 2), gf.cpu().numpy())
+
+    start_ms, tick_ms, span_ss, flags = timed(TICK_FULL, copies[0])
     log_full = int((oe.cpu().numpy() == 3).sum())
+    lstart_ms, ltick_ms, lspan_ss, lflags = timed(TICK_LIGHT, copies[1])
+    same = bool(np.array_equal(flags, lflags)) and all(torch.equal(copies[0][k], copies[1][k]) for k in master)
     # count pass (same sequence, the count before each tick)
-    restore()
+    restore(copies[0])
+    e.set_tick_mode(TICK_FULL)
     words = np.zeros((steps, 3), np.int64)
     for k in range(steps):
         start(k)
         words[k] = e.replicate_tick_count(lp)
         e.replicate_tick(lp_d, gf, where=DEVICE)
     e.synchronize()
+    # the light sequence again, a host wait per step: each tick's fallback count
+    restore(copies[1])
+    e.set_tick_mode(TICK_LIGHT)
+    fallbacks = []
+    for k in range(steps):
+        start(k)
+        e.replicate_tick(lp_d, gf, where=DEVICE)
+        e.synchronize()
+        fallbacks.append(e.tick_light_fallbacks())
+    e.set_tick_mode(TICK_FULL)
     # a launch with no group's work
     none = torch.full((G,), -1, dtype=torch.int32, device=dev)
     empty = []
@@ -428,13 +445,14 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     # steady state: the steps after the first two (the synthetic state's backlog merges there)
     ss = slice(2, steps)
     tick_ss = float(np.mean(tick_ms[ss]))
+    ltick_ss = float(np.mean(ltick_ms[ss]))
     bytes_ss = float(np.mean(4 * (words[ss, 0] + words[ss, 1])))
     act_ss = float(np.mean(words[ss, 2]))
-    span_ss = marks[2][0].elapsed_time(marks[-1][2]) / (steps - 2)
     empty_ms = float(np.median(empty))
     return {"workload": "config #3 ticked in place: per step mraft_start of 1-4 entries at each of the %d leaders, "
-                        "then one mraft_replicate_tick (one launch, no shards), %d steps back to back on one "
-                        "engine stream; steady state = steps 3..%d" % (nl, steps, steps),
+                        "then one mraft_replicate_tick (no shards), %d steps back to back on one engine stream; "
+                        "steady state = steps 3..%d; top-level fields: the full tick (MRAFT_TICK_FULL, one "
+                        "launch), `light`: the same sequence with MRAFT_TICK_LIGHT" % (nl, steps, steps),
             "steps": steps, "tick_ms_steps": [round(x, 4) for x in tick_ms],
             "start_ms_mean": float(np.mean(start_ms)),
             "tick_ms_steady": tick_ss, "device_ms_per_step_steady": span_ss,
@@ -453,7 +471,19 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
             "gaps_share_steady": 1.0 - (float(np.sum(tick_ms[ss])) + float(np.sum(start_ms[ss]))) /
                                  (span_ss * (steps - 2)),
             "start_log_full_last_step": log_full,
-            "groups_committed_last_step": int(((flags & 2) != 0).sum())}
+            "groups_committed_last_step": int(((flags & 2) != 0).sum()),
+            "light": {"what": "MRAFT_TICK_LIGHT: k_tick_lite (eight groups per wave; the steady-state groups "
+                              "settled there) + k_tick_list (the others through the full tick, grid from the "
+                              "previous tick's count)",
+                      "tick_ms_steps": [round(x, 4) for x in ltick_ms],
+                      "tick_ms_steady": ltick_ss, "device_ms_per_step_steady": lspan_ss,
+                      "decisions_per_s_steady": G / (lspan_ss / 1e3),
+                      "tick_decisions_per_s_steady": G / (ltick_ss / 1e3),
+                      "tick_achieved_GBps_steady": bytes_ss / ltick_ss / 1e6,
+                      "tick_hbm_frac_steady": bytes_ss / (ltick_ss / 1e3) / HBM_PEAK,
+                      "speedup_tick_steady": tick_ss / ltick_ss,
+                      "fallback_groups_steps": fallbacks,
+                      "state_equals_full": same}}
 
 
 def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define MRAFT_ABI_VERSION 5
+#define MRAFT_ABI_VERSION 6
 
 /* Largest log capacity L (entries per replica ring): ring offsets are formed
  * as 32-bit byte offsets (4 * (position + 32) < 2^32). */
@@ -467,6 +467,28 @@ int32_t mraft_get_tick_shards(const mraft_engine *h);
 /* The hipStream_t of tick shard `shard` (the engine stream when shards == 1;
  * NULL when out of range): for events that time or order against a shard. */
 void *mraft_shard_stream(mraft_engine *h, int32_t shard);
+
+/* Tick path (ABI 6). MRAFT_TICK_FULL (the default): one wave per group, the
+ * streaming pass of the fused tick. MRAFT_TICK_LIGHT: for a running
+ * deployment's ticks (heartbeats and a few appended entries per leader): a
+ * first launch settles, eight groups per wave, every group whose followers all
+ * reply success without a compare (prevLogTerm matches; a heartbeat, or an
+ * append at the follower's last Index of at most 64 entries that fits the
+ * ring) and whose commitIndex settles at log[last]; a second launch runs every
+ * other group through the full tick. Outputs and state are identical to
+ * MRAFT_TICK_FULL for every state (the groups are independent). Applies to
+ * mraft_replicate_tick[_export] with and without shards (each shard its own
+ * pair of launches); mraft_replicate_tick_count always counts the full tick.
+ * The second launch's grid follows the previous light tick's count (a pinned
+ * word the device writes): a jump from few to many non-settling groups costs
+ * one slow tick, never a wrong one. */
+enum { MRAFT_TICK_FULL = 0, MRAFT_TICK_LIGHT = 1 };
+int mraft_set_tick_mode(mraft_engine *h, int32_t mode);
+int32_t mraft_get_tick_mode(const mraft_engine *h);  /* -1: null handle */
+/* Groups the most recent completed MRAFT_TICK_LIGHT tick sent to the full
+ * tick, summed over its shards (exact after mraft_synchronize); -1 before the
+ * first light tick or for a null handle. */
+int64_t mraft_tick_light_fallbacks(mraft_engine *h);
 
 /* mraft_replicate_tick followed by mraft_export_group_status for the same
  * leader_peer, fused into the one launch (the words the shard router

@@ -18,6 +18,7 @@ SYNTH_PATH = os.path.join(_HERE, "libmraft_synth.so")
 # ---- constants (include/mraft.h) -------------------------------------------
 LEADER, CANDIDATE, FOLLOWER = 1, 2, 3
 HOST, DEVICE = 0, 1
+TICK_FULL, TICK_LIGHT = 0, 1  # mraft_set_tick_mode
 CREATE_NO_ALLOC = 1
 CREATE_DEDICATED_QUEUE = 2
 OK, E_INVAL, E_NOMEM, E_HIP, E_NOSTATE = 0, -1, -2, -3, -4
@@ -31,7 +32,7 @@ G_SNAPSHOT_INSTALLED = 256
 PERSIST_STATE, PERSIST_SNAPSHOT = 1, 2
 TERMS_SORTED = 1
 AE_ENTRIES_SORTED = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 FANIN_OVERLAP = 1
 FANIN_ORDERED = 2
 COMM_ID_BYTES = 128
@@ -99,6 +100,7 @@ ABI_SYMBOLS = (
     "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
     "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream", "mraft_handle_append_entries_ex",
     "mraft_set_stage_capacity", "mraft_get_stage_capacity",
+    "mraft_set_tick_mode", "mraft_get_tick_mode", "mraft_tick_light_fallbacks",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -154,6 +156,9 @@ _SIGS = {
     "mraft_shard_stream": (_vp, [_vp, _i32]),
     "mraft_set_stage_capacity": (ctypes.c_int, [_vp, _i64]),
     "mraft_get_stage_capacity": (_i64, [_vp]),
+    "mraft_set_tick_mode": (ctypes.c_int, [_vp, _i32]),
+    "mraft_get_tick_mode": (_i32, [_vp]),
+    "mraft_tick_light_fallbacks": (_i64, [_vp]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

@@ -30,6 +30,10 @@ constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
 // next call on (round 5's fixed 8 ran such batches on 0.4 % of the chip).
 constexpr int kDeferGridMin = 8;
 constexpr int kDeferGridMax = 1 << 16;
+// The light tick's fallback launch (MRAFT_TICK_LIGHT): at least this many
+// workgroups, twice the previous light tick's count, at most the groups (a
+// grid-stride loop makes any grid exact; an empty one costs a few µs).
+constexpr long long kLiteGridMin = 2048;
 // Words of the fallback's per-workgroup cycle buffers (nslot x L, at most this).
 constexpr int64_t kCycSlotWords = (int64_t)1 << 25;  // 8,192 buffers at L = 4,096 (128 MiB)
 
@@ -59,6 +63,14 @@ struct mraft_engine {
   int64_t stage_cap = kDefaultStageWords;  // words of staged entries the deferred launch may use
   long long *dhint = nullptr;  // pinned host word: the last by-reference call's deferred count (device-written)
   long long *dhint_dev = nullptr;  // its device-side address
+  // MRAFT_TICK_LIGHT (mraft_set_tick_mode): the list of groups for the full
+  // tick (G words, shard s at its first group), a counter pair per shard (the
+  // light launch counts into one, the fallback zeroes the other for the next
+  // tick) and per shard the last fallback count, pinned (dhint + 1 + s)
+  int32_t tick_mode = MRAFT_TICK_FULL;
+  int32_t *lite_list = nullptr;
+  unsigned *lite_cnt = nullptr;
+  int lite_par[kMaxShards] = {};
   std::vector<void *> scratch_ptr;
   std::vector<size_t> scratch_cap;
 };
@@ -213,9 +225,47 @@ int32_t *off(int32_t *p, int64_t k) { return p ? p + k : nullptr; }
 // The tick launch(es): one launch on the engine stream, or with S tick shards
 // one launch per contiguous group range on its own queue, each queue first
 // waiting for the engine stream's prior work (one event, fork_ev).
+int alloc_async(mraft_engine *h, void **p, size_t bytes, const char *what);
+
+// The light tick's buffers (MRAFT_TICK_LIGHT), allocated on first use,
+// stream-ordered, counters zeroed.
+int ensure_lite(mraft_engine *h) {
+  if (h->lite_list) return MRAFT_OK;
+  void *l = nullptr, *c = nullptr;
+  TRY(alloc_async(h, &l, (size_t)h->G * sizeof(int32_t), "light tick list"));
+  h->lite_list = (int32_t *)l;
+  TRY(alloc_async(h, &c, 2 * kMaxShards * sizeof(unsigned), "light tick counters"));
+  h->lite_cnt = (unsigned *)c;
+  HIP_TRY(hipMemsetAsync(h->lite_cnt, 0, 2 * kMaxShards * sizeof(unsigned), h->stream));
+  for (int s = 0; s < kMaxShards; ++s) h->lite_par[s] = 0;
+  return MRAFT_OK;
+}
+
+// One tick launch over groups [g0, g0 + d.G) as shard s on stream st: the full
+// tick, or the light tick's pair of launches.
+void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const int32_t *lp, int32_t *gf,
+                int32_t *ec, int32_t *et, hipStream_t st) {
+  if (h->tick_mode != MRAFT_TICK_LIGHT || h->P < 2) {
+    mraft::launch_replicate_tick(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), st);
+    return;
+  }
+  mraft::LiteBufs lb;
+  const int par = h->lite_par[s];
+  h->lite_par[s] ^= 1;
+  lb.list = h->lite_list + g0;
+  lb.cnt = h->lite_cnt + 2 * s + par;
+  lb.cnt_next = h->lite_cnt + 2 * s + (par ^ 1);
+  lb.hint = h->dhint_dev + 1 + s;
+  const long long prev = ((volatile long long *)h->dhint)[1 + s];
+  const long long gr = prev < 0 ? (long long)d.G : std::max(kLiteGridMin, 2 * prev);
+  lb.grid = (int)std::max(1ll, std::min(gr, (long long)d.G));
+  mraft::launch_replicate_tick_light(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), lb, st);
+}
+
 int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, int32_t *et) {
+  if (h->tick_mode == MRAFT_TICK_LIGHT) TRY(ensure_lite(h));
   if (h->nshards <= 1) {
-    mraft::launch_replicate_tick(dev_of(h), lp, gf, ec, et, h->stream);
+    tick_range(h, dev_of(h), 0, 0, lp, gf, ec, et, h->stream);
     HIP_TRY(hipGetLastError());
     return MRAFT_OK;
   }
@@ -224,7 +274,7 @@ int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, in
   for (int s = 0; s < h->nshards; ++s) {
     const int32_t g0 = (int32_t)((int64_t)h->G * s / h->nshards), g1 = (int32_t)((int64_t)h->G * (s + 1) / h->nshards);
     if (g1 <= g0) continue;
-    mraft::launch_replicate_tick(dev_slice(h, g0, g1), lp + g0, off(gf, g0), off(ec, g0), off(et, g0), h->shard_q[s]);
+    tick_range(h, dev_slice(h, g0, g1), s, g0, lp, gf, ec, et, h->shard_q[s]);
   }
   h->shards_pending = true;
   HIP_TRY(hipGetLastError());
@@ -372,13 +422,14 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
   h->stream = h->own_stream;
   {
     void *hp = nullptr;
-    if (hipHostMalloc(&hp, sizeof(long long), hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc(&hp, sizeof(long long) * (1 + kMaxShards), hipHostMallocMapped) != hipSuccess) {
       (void)hipStreamDestroy(h->own_stream);
       delete h;
       return fail(MRAFT_E_NOMEM, "pinned host word allocation failed");
     }
     h->dhint = (long long *)hp;
     *(volatile long long *)h->dhint = 0;
+    for (int k = 1; k <= kMaxShards; ++k) ((volatile long long *)h->dhint)[k] = -1;  // no light tick yet
     void *dp = nullptr;
     if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
       (void)hipHostFree(hp);
@@ -428,7 +479,7 @@ int mraft_destroy(mraft_engine *h) {
   // stream-ordered buffers (alloc_async): freed on the engine stream, then waited for
   for (void *p : h->scratch_ptr)
     if (p) (void)hipFreeAsync(p, h->stream);
-  for (void *p : {(void *)h->claim, (void *)h->srcmark, (void *)h->ae_total})
+  for (void *p : {(void *)h->claim, (void *)h->srcmark, (void *)h->ae_total, (void *)h->lite_list, (void *)h->lite_cnt})
     if (p) (void)hipFreeAsync(p, h->stream);
   (void)hipStreamSynchronize(h->stream);
   if (h->fanin_own) (void)hipStreamSynchronize(h->fanin_own);
@@ -1235,6 +1286,26 @@ int mraft_set_tick_shards(mraft_engine *h, int32_t shards) {
 }
 
 int32_t mraft_get_tick_shards(const mraft_engine *h) { return h ? h->nshards : 0; }
+
+int mraft_set_tick_mode(mraft_engine *h, int32_t mode) {
+  if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
+  if (mode != MRAFT_TICK_FULL && mode != MRAFT_TICK_LIGHT) return fail(MRAFT_E_INVAL, "tick mode %d", mode);
+  h->tick_mode = mode;
+  return MRAFT_OK;
+}
+
+int32_t mraft_get_tick_mode(const mraft_engine *h) { return h ? h->tick_mode : -1; }
+
+int64_t mraft_tick_light_fallbacks(mraft_engine *h) {
+  if (!h) return -1;
+  long long t = 0;
+  for (int s = 0; s < std::max(1, (int)h->nshards); ++s) {
+    const long long v = ((volatile long long *)h->dhint)[1 + s];
+    if (v < 0) return -1;
+    t += v;
+  }
+  return t;
+}
 
 void *mraft_shard_stream(mraft_engine *h, int32_t shard) {
   if (!h || shard < 0 || shard >= h->nshards) return nullptr;

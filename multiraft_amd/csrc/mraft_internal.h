@@ -11,6 +11,19 @@ namespace mraft {
 
 void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
                            int32_t *exp_term_leader, hipStream_t st);
+// The light tick (MRAFT_TICK_LIGHT, mraft_tick.hip): k_tick_lite settles the
+// steady-state groups eight per wave and lists the others (list, cnt); the
+// fallback launch (grid workgroups, grid-stride) runs them through the full
+// tick, zeroes cnt_next (the next light tick's counter) and writes the count
+// to the pinned host word hint.
+struct LiteBufs {
+  int32_t *list;
+  unsigned *cnt, *cnt_next;
+  long long *hint;
+  int grid;
+};
+void launch_replicate_tick_light(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
+                                 int32_t *exp_term_leader, const LiteBufs &lb, hipStream_t st);
 void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,
                                  hipStream_t st);
 

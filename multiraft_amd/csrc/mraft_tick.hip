@@ -234,448 +234,9 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_group(Dev s, const
   // code is kept instruction-for-instruction)
   const int g = uni(gb + (int)(threadIdx.x >> 6));
   if (g >= s.G) return;
-  const int L = s.L;
-  TICK_STAMP(0);
-
-  // ------------------------------------------------------------ header
-  const int lp = uni(leader_peer[g]);
-  if (lp < 0 || lp >= P) {
-    if (!COUNT && lane == 0) {
-      if (gflags) gflags[g] = lp >= P ? MRAFT_G_ERROR : 0;
-      if (ex.commit) {
-        const long long s0 = (long long)g * P;  // mraft_export_group_status: replica 0
-        ex.put(g, s.commit[s0], s.term[s0], s.role[s0]);
-      }
-    }
-    return;
-  }
-  const long long ld = (long long)g * P + lp;
-  const long long lrow = ld * L;
-  // Every load that depends only on the leader index, issued together.
-  const int role = uni(s.role[ld]), T = uni(s.term[ld]), c0 = uni(s.commit[ld]),
-            last = uni(s.last[ld]), ldummy = uni(s.dummy[ld]), lhead = uni(s.head[ld]),
-            lsrt = uni(s.srt[ld]);
-  const int lb = lhead - ldummy;  // leader Index i at lrow + ring(i + lb): the log ring
-  int mm[P];
-#pragma unroll
-  for (int j = 0; j < P; ++j) mm[j] = uni(s.match[ld * P + j]);
-  const int p = lane < lp ? lane : lane + 1;
-  const long long f = (long long)g * P + p;
-  int nxt = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
-  if (lane < NI) {
-    nxt = s.next[ld * P + p];
-    fterm = s.term[f];
-    fdummy = s.dummy[f];
-    flast = s.last[f];
-    fcommit = s.commit[f];
-    fhead = s.head[f];
-  }
-  long long hR = 1;  // algorithmic words of the header (wave-uniform)
-  if (role != kLeader || c0 < ldummy) {
-    // not a leader: appendOneRound returns (:22-25); commit < dummy: outside
-    // the reachable states (include/mraft.h MRAFT_ITEM_BAD_STATE).
-    if (COUNT) {
-      if (lane == 0) atomicAdd(&counts[0], (unsigned long long)(role != kLeader ? 1 : 5));
-    } else if (lane == 0) {
-      if (gflags) gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
-      ex.put(g, c0, T, role);
-    }
-    return;
-  }
-  hR = 6 + NI;  // role, term, commit, last, dummy, terms_sorted, nextIndex[q]
-
-  // ------------------------------------------------------------ phase A
-  int icls = IC_NONE;
-  const int prev = nxt - 1;                                              // :26
-  if (lane < NI) icls = prev < ldummy ? IC_SNAP : (prev > last ? IC_PANIC : IC_GO);  // :27, :41
-  const int snap_m = (int)__ballot(icls == IC_SNAP);  // lanes >= NI never set a bit: 32 bits suffice
-  if (__ballot(icls == IC_PANIC)) {  // a3 would panic: the whole group is skipped
-    if (COUNT) {
-      if (lane == 0) atomicAdd(&counts[0], (unsigned long long)hR);
-    } else if (lane == 0) {
-      if (gflags) gflags[g] = MRAFT_G_ERROR | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-      ex.put(g, c0, T, role);
-    }
-    return;
-  }
-  int flags = MRAFT_G_ACTIVE | (snap_m ? MRAFT_G_NEED_SNAPSHOT : 0);
-  const int probe_last = uni(s.log[lrow + ring(last + lb, L)]);  // speculative a1 probe
-  int prev_term = 0, ft = 0;
-  if (icls == IC_GO) {
-    prev_term = s.log[lrow + ring(prev + lb, L)];                        // :49
-    if (prev >= fdummy && prev <= flast) ft = s.log[f * L + ring(prev - fdummy + fhead, L)];
-  }
-  const int n = last - prev;                                             // :50
-  int rterm = 0, rsucc = 0, rci = 0;
-  bool adopt = false;
-  // InstallSnapshot (raft_append_entry.go:27-34 -> raft_snapshot.go:15-54),
-  // LastIncludedIndex = leader dummyIndex, LastIncludedTerm = dummyTerm.
-  const int lit = snap_m ? uni(s.log[lrow + lhead]) : 0;
-  if (icls == IC_SNAP) {
-    if (T >= fterm && ldummy > fcommit && ldummy <= flast && ldummy < fdummy) {
-      icls = IC_IS_PANIC;                                                // sliceFrom panics
-    } else if (T < fterm) {                                              // :20-22
-      icls = IC_IS_STALE;
-      rterm = fterm;
-    } else {
-      adopt = T > fterm;                                                 // :23-26
-      rterm = T;
-      icls = ldummy <= fcommit ? IC_IS_OLD : IC_IS_INSTALL;              // :31-33
-    }
-  }
-  if (icls == IC_GO) {
-    if (T < fterm) {                                                     // :112-115
-      icls = IC_STALE;
-      rterm = fterm;
-    } else {
-      adopt = T > fterm;                                                 // :116-118
-      if (prev < fdummy) {                                               // :123-127
-        icls = IC_BELOW;
-        rci = fdummy + 1;
-      } else {
-        rterm = T;
-        if (prev > flast) {                                              // :131-133
-          icls = IC_BEYOND;
-          rci = flast + 1;
-        } else if (ft != prev_term) {                                    // :128
-          if (prev > fdummy + 1) icls = IC_SCAN;
-          else { icls = IC_MISMATCH; rci = prev; }
-        } else {
-          rsucc = 1;
-          icls = n > 0 ? IC_MERGE : IC_HB;
-        }
-      }
-    }
-  }
-
-  // ------------------------------------------------------------ phase B
-  int scan_extra = 0;
-  // ConflictIndex scans (:136-142): the first 64 terms below prev of every
-  // scanning follower in one round trip (most runs end there), then each
-  // longer run on its own, 64 * MRAFT_TICK_SCANU terms per round trip (64
-  // measured 1.4 % faster than 256: fewer lines fetched past the run's end
-  // outweigh the extra round trips). (Running them after the pass with their
-  // inputs parked in LDS measured no faster and moved no traffic: r4_v13.)
-  auto conflict_scans = [&](const int32_t *__restrict__ logp, unsigned long long m, int qdummy, int qhead, int qft) {
-    int pv[NI];
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      pv[q] = 0;
-      if ((m >> q) & 1) {
-        const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)),
-                  sh = uni(__shfl(qhead, q, 64));
-        const int32_t *pp = logp + sf * L + ring(max(sp - 1 - lane, sd + 2) - sd + sh, L);  // prev >= dummy + 2
-        pv[q] = *pp;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if ((m >> q) & 1) {
-        const long long sf = (long long)g * P + (q < lp ? q : q + 1);
-        const int sd = uni(__shfl(qdummy, q, 64)), sp = uni(__shfl(prev, q, 64)), sa = uni(__shfl(qft, q, 64)),
-                  sh = uni(__shfl(qhead, q, 64));
-        const int lo = sd + 2, hi = sp - 1;
-        const unsigned long long mm = __ballot(hi - lane >= lo && pv[q] != sa);
-        int ci;
-        if (mm) {
-          ci = hi - first_lane(mm);
-        } else if (hi - 64 < lo) {
-          ci = sd + 1;
-        } else {
-          const int r = wave_scan_down_ne<MRAFT_TICK_SCANU>(logp + sf * L, sd, sh, L, lo, hi - 64, sa);
-          ci = r < lo ? sd + 1 : r;
-        }
-        if (lane == q) {
-          rci = ci;
-          if (COUNT) scan_extra = sp - (ci > sd + 1 ? ci : sd + 2);
-        }
-      }
-    }
-  };
-  const unsigned long long scan_m = __ballot(icls == IC_SCAN);
-  if (scan_m) conflict_scans(s.log, scan_m, fdummy, fhead, ft);
-
-  // prev == the follower's dummy, for phase C's terms_sorted rule (a ballot:
-  // no per-lane word kept live across the pass)
-  const unsigned long long pd_m = __ballot(prev == fdummy);
-  // Per-follower pass parameters (wave-uniform).
-  const int merge_m = (int)__ballot(icls == IC_MERGE);
-  Fol<NI> fo;
-  fo.log = s.log;
-  fo.slot0 = (long long)g * P;
-  fo.skip = lp;
-  fo.L = L;
-  fo.cmp = merge_m;
-  fo.copy = 0;
-  fo.capok = 0;
-  fo.full = 0;
-  int mlo = last + 1, maybe_full = 0;
-  bool vec = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(s.log) & 15) == 0;
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {
-    const int sp = uni(__shfl(prev, q, 64)), sd = uni(__shfl(fdummy, q, 64)),
-              sl = uni(__shfl(flast, q, 64)), sh = uni(__shfl(fhead, q, 64));
-    fo.base[q] = sh - sd;
-    fo.start[q] = sp + 1;
-    fo.cend[q] = min(last, sl) + 1;  // compared while the follower has the slot
-    fo.cfrom[q] = 0;                 // 0: no mismatch (the pass's relative Indexes are > 0)
-    const bool capok = (long long)last - sd <= (long long)L - 1;
-    fo.capok |= capok ? 1 << q : 0;
-    if ((merge_m >> q) & 1) {
-      mlo = min(mlo, fo.start[q]);
-      vec = vec && (((fo.base[q] - lb) & 3) == 0);  // 4-entry groups aligned alike in both rings
-      maybe_full |= !capok;
-    }
-  }
-
-  // Fold before the pass when no follower can be rejected for capacity (then
-  // every merge replies success whatever its mismatch point), so the exact
-  // commit scan of a Figure-8 group rides along the same streaming pass.
-  Fold<P, COUNT> fd;
-  int commit = c0, top = 0, slo = 1, shi = 0;
-  int settled = 0;  // a1 decided by its top term alone (sorted terms, include/mraft.h)
-  const int is_m = (int)__ballot(icls >= IC_IS_STALE && icls <= IC_IS_INSTALL);
-  const int have0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
-  const int succ0 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
-  if (!maybe_full) {
-    fd.run(T, lp, mm, have0, succ0, is_m, ldummy, rterm, prev, n, rci, icls);
-    if (fd.any) {
-      top = min(fd.mstar, last);
-      if (top > c0) {
-        const int t = top == last ? probe_last : uni(s.log[lrow + ring(top + lb, L)]);  // :98
-        if (t == T) commit = top;
-        else if (lsrt && t < T) settled = 1;  // no lower entry carries currentTerm
-        else { slo = c0 + 1; shi = top - 1; }
-      }
-    }
-  }
-  int found = -1;
-  TICK_STAMP(1);
-  if (merge_m || slo <= shi) {
-    const int plo = min(mlo, slo <= shi ? slo : mlo);
-    const int phi = merge_m ? last : shi;
-    // The pass runs on Indexes relative to B = pass_bias(plo) (mraft_pass.h:
-    // no chunk end overflows int32 near 2^31); the rows absorb B.
-    const int B = pass_bias(plo);
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (!((merge_m >> q) & 1)) continue;  // (only merging followers are ever addressed)
-      fo.base[q] += B;
-      fo.start[q] -= B;
-      fo.cend[q] -= B;
-    }
-    const RingRow lsrc{s.log, lrow, lb + B, L};
-    const int pl = plo - B, ph = phi - B, nend = last + 1 - B;
-    const int sl = slo <= shi ? slo - B : 1, sh = slo <= shi ? shi - B : 0;
-    // Chunks start on a 128-B line of the leader's row (physical position of
-    // plo rounded down; the ring wraps at a multiple of 4 entries, so every
-    // lane's dwordx4 stays contiguous).
-    if (vec) {
-      int c = pl - (int)((lrow + ring(plo + lb, L)) & (MRAFT_TICK_ALIGN - 1));
-      if (c <= ph && fo.cmp) c = pass_pipe<COUNT, MRAFT_TICK_CMP_EPL>(lsrc, fo, nend, sl, sh, T, found, c, pl, ph);
-      copy_loop<true, COUNT>(lsrc, fo, c, nend, pl, ph, sl, sh, T, found);
-    } else {
-      int c = pl;
-      for (; c <= ph && fo.cmp; c += 256) pass_chunk<1, false, COUNT>(lsrc, fo, nend, sl, sh, T, found, c, pl, ph);
-      copy_loop<false, COUNT>(lsrc, fo, c, nend, pl, ph, sl, sh, T, found);
-    }
-    if (found >= 0) found += B;  // the a1 hit back in Raft Indexes
-  }
-  TICK_STAMP(2);
-  const Dev s2 = reload_dev();  // phase C/D re-read the state pointers (not held across the pass)
-  int mk = -1;  // this lane's follower: first mismatching entry of its merge
-#pragma unroll
-  for (int q = 0; q < NI; ++q) {
-    if (lane == q && icls == IC_MERGE) {
-      mk = (fo.cfrom[q] > 0 || ((fo.full >> q) & 1)) ? fo.cfrom[q] - fo.start[q] : -1;
-      if ((fo.full >> q) & 1) icls = IC_FULL;
-    }
-  }
-  if (!maybe_full) {
-    if (slo <= shi && found > c0) commit = found;
-  } else {
-    const int have1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB) | is_m;
-    const int succ1 = (int)__ballot(icls >= IC_STALE && icls <= IC_HB && rsucc);
-#pragma unroll
-    for (int j = 0; j < P; ++j) mm[j] = uni(s2.match[ld * P + j]);  // re-read: not kept live across the pass
-    fd.run(T, lp, mm, have1, succ1, is_m, ldummy, rterm, prev, n, rci, icls);
-    if (fd.any) {
-      top = min(fd.mstar, last);
-      if (top > c0) {
-        const int t = uni(s2.log[lrow + ring(top + lb, L)]);
-        if (t == T) {
-          commit = top;
-        } else if (uni(s2.srt[ld]) && t < T) {
-          settled = 1;
-        } else {
-          const int i = wave_scan_down_eq(s2.log + lrow, ldummy, lhead, L, c0 + 1, top - 1, T);
-          if (i > c0) commit = i;
-        }
-      }
-    }
-  }
-
-  // ------------------------------------------------------------ phase C
-  int fcadv = 0;
-  long long cR = 0, cW = 0;  // algorithmic words of this lane's follower item (COUNT)
-  if (icls >= IC_STALE && icls <= IC_HB) {
-    // deferred :111 (a load, OR and store: as a non-returning atomic OR it
-    // measured no faster here, r4_v7)
-    if (!COUNT) mark_persist(s2, f, MRAFT_PERSIST_STATE);
-    if (icls == IC_STALE) {
-      cR = 1;
-    } else {
-      if (!COUNT) {
-        if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
-        s2.role[f] = kFollower;                                           // :120
-      }
-      cR = 2;                                                            // term, dummy
-      cW = (adopt ? 2 : 0) + 1;                                          // role
-      if (icls != IC_BELOW) cR += 1;                                     // last
-      if (icls >= IC_MISMATCH) cR += 1;                                  // log[prev]
-      if (icls == IC_SCAN) cR += scan_extra;
-      if (icls == IC_MERGE || icls == IC_HB) {
-        int newlast = flast;
-        if (icls == IC_MERGE) {
-          const int kc = min(n, flast - prev);
-          cR += (mk < 0) ? n : (mk < kc ? mk + 1 : mk);                 // compared follower terms
-          if (mk >= 0) {
-            newlast = prev + n;
-            if (!COUNT) s2.last[f] = newlast;
-            cW += (n - mk) + 1;
-            // terms_sorted after appending from Index prev+1+mk: the args'
-            // flag (prevLogTerm, entries sorted: the leader's proof, with the
-            // dummy's term compared explicitly), or the new entries are the
-            // whole log when that Index is the dummy's successor
-            bool fl = lsrt != 0;
-            if (fl && prev == ldummy)
-              fl = s2.log[lrow + ring(prev + lb, L)] <= s2.log[lrow + ring(prev + 1 + lb, L)];
-            const bool at_dummy = ((pd_m >> lane) & 1) != 0;
-            const int sw = !fl ? 0 : (mk == 0 && at_dummy) ? 1 : -1;
-            if (sw >= 0) {
-              if (!COUNT) s2.srt[f] = sw;
-              cW += 1;
-            }
-          }
-        }
-        cR += 1;                                                         // :157-160
-        if (c0 > fcommit) {
-          fcadv = 1;
-          cW += 1;
-          if (!COUNT) s2.commit[f] = min(c0, newlast);
-        }
-      }
-    }
-  }
-  if (icls >= IC_IS_STALE && icls <= IC_IS_INSTALL) {
-    cR = 1;                                                              // term
-    if (!COUNT) {
-      const int bits = (adopt ? MRAFT_PERSIST_STATE : 0) |                 // raft_snapshot.go:26
-                       (icls == IC_IS_INSTALL ? MRAFT_PERSIST_STATE | MRAFT_PERSIST_SNAPSHOT : 0);  // :47
-      mark_persist(s2, f, bits);
-    }
-    if (icls != IC_IS_STALE) {
-      if (!COUNT) {
-        if (adopt) { s2.term[f] = T; s2.voted[f] = -1; }
-        s2.role[f] = kFollower;                                           // :28
-      }
-      cR += 1;                                                           // commit
-      cW = (adopt ? 2 : 0) + 1;
-      if (icls == IC_IS_INSTALL) {
-        const bool newlog = ldummy > flast;                              // :35-37
-        // sliceFrom(LastIncludedIndex) (:38-40) is an O(1) rebase of the
-        // ring: the head moves to the entry at LastIncludedIndex, no term
-        // moves; a new log ([dummy] only, :35-37) keeps its head.
-        // (head and dummy re-read here rather than kept live across the pass)
-        const int fh = s2.head[f], nh = newlog ? fh : ring(fh + (ldummy - s2.dummy[f]), L);
-        if (!COUNT) {
-          s2.log[f * L + nh] = lit;                                       // :44-45 dummy term
-          if (newlog) { s2.last[f] = ldummy; s2.srt[f] = 1; }           // [dummy] only: sorted
-          else s2.head[f] = nh;                                           // a suffix: unchanged
-          s2.hsnap[f] = 1;                                                // raft_snapshot.go:52 hasSnapshot
-          s2.dummy[f] = ldummy;
-          s2.commit[f] = ldummy;                                          // :42
-          s2.applied[f] = ldummy;                                         // :43
-        }
-        cR += 1;                                                         // last
-        cW += 3;
-        if (newlog) {
-          cW += 3;                                                       // dummy term, last, terms_sorted
-        } else {
-          cR += 1;                                                       // dummy
-          cW += 1;                                                       // dummy term
-        }
-      }
-    }
-  }
-  if (__ballot(icls == IC_IS_INSTALL)) flags |= MRAFT_G_SNAPSHOT_INSTALLED;
-  if (__ballot(icls == IC_IS_PANIC)) flags |= MRAFT_G_FOLLOWER_PANIC;
-  if (__ballot(icls == IC_FULL)) flags |= MRAFT_G_LOG_FULL;
-  if (__ballot(fcadv != 0)) flags |= MRAFT_G_FOLLOWER_COMMIT;
-
-  // ------------------------------------------------------------ phase D
-  if (commit != c0) flags |= MRAFT_G_COMMITTED;
-  if (fd.stepped) flags |= MRAFT_G_STEPPED_DOWN;
-  if (!COUNT) {
-    if (lane == 0) {
-      if (fd.stepped) {
-        s2.term[ld] = fd.term;
-        s2.voted[ld] = -1;
-        s2.role[ld] = kFollower;
-        mark_persist(s2, ld, MRAFT_PERSIST_STATE);                        // :72, snapshot :64
-      }
-      if (commit != c0) s2.commit[ld] = commit;
-      if (gflags) gflags[g] = flags;
-      ex.put(g, commit, fd.stepped ? fd.term : T, fd.stepped ? kFollower : kLeader);
-    }
-    TICK_STAMP(3);
-    // nextIndex / matchIndex of this lane's follower (:76-77, :82; snapshot
-    // :66-67): success -> prev + n (+1), failure -> ConflictIndex, snapshot
-    // -> LastIncludedIndex (+1).
-    if (lane < NI && ((fd.gate_m >> lane) & 1)) {
-      const bool isr = ((is_m >> lane) & 1) != 0, ok = ((fd.rs_m >> lane) & 1) != 0;
-      const int mv = isr ? ldummy : prev + n;
-      s2.next[ld * P + p] = ok ? mv + 1 : rci;
-      if (ok) s2.match[ld * P + p] = mv;
-    }
-  } else {
-    // Leader-side words, wave-uniform.
-    long long gR = hR + (fd.any ? NI : 0), gW = (fd.stepped ? 3 : 0) + (commit != c0 ? 1 : 0);
-#pragma unroll
-    for (int q = 0; q < NI; ++q) gW += ((fd.gate_m >> q) & 1) ? (((fd.rs_m >> q) & 1) ? 2 : 1) : 0;
-    // Leader log words: union of {prev_q} (PrevLogTerm), [prev_q+1, last]
-    // (entries consumed by merges) and the commit scan [stop, top].
-    long long A = (long long)last + 1;
-#pragma unroll
-    for (int q = 0; q < NI; ++q)
-      if (fd.ic[q] == IC_MERGE) A = min(A, (long long)fd.rp[q] + 1);
-    long long a1lo = 1, a1hi = 0;
-    if (fd.any && top > c0) {
-      a1hi = top;
-      a1lo = (commit != c0) ? commit : settled ? top : c0 + 1;
-    }
-    long long u = interval_len(A, last) + interval_len(a1lo, a1hi);
-    u -= interval_len(max(A, a1lo), min((long long)last, a1hi));
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      if (fd.ic[q] < IC_STALE) continue;  // log[prev] per gathered item, log[dummy] per snapshot
-      bool dup = false;
-#pragma unroll
-      for (int q2 = 0; q2 < q; ++q2) dup |= (fd.ic[q2] >= IC_STALE && fd.rp[q2] == fd.rp[q]);
-      const long long x = fd.rp[q];
-      const bool inside = (x >= A && x <= last) || (x >= a1lo && x <= a1hi);
-      if (!dup && !inside) u += 1;
-    }
-    gR += u;
-    const unsigned long long R = wave_sum((unsigned long long)cR) + (unsigned long long)gR;
-    const unsigned long long W = wave_sum((unsigned long long)cW) + (unsigned long long)gW;
-    if (lane == 0) {
-      atomicAdd(&counts[0], R);
-      atomicAdd(&counts[1], W);
-      atomicAdd(&counts[2], 1ull);
-    }
-  }
+#define TICK_EXIT return
+#include "mraft_tick_body.inc"
+#undef TICK_EXIT
 }
 
 // P == 1: no peers, so no AppendEntries and no reply ever reaches a1.
@@ -704,6 +265,204 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
     if (gflags) gflags[g] = fl;
     ex.put(g, s.commit[g], s.term[g], s.role[g]);
   }
+}
+
+// ------------------------------------------------------------ light tick
+// MRAFT_TICK_LIGHT (mraft_set_tick_mode). The tick of a running deployment —
+// every follower caught up to its nextIndex, a heartbeat or a few appended
+// entries — is a handful of dependent word loads per group and almost no
+// streaming, so a wave per group spends its life waiting on them
+// (secondary.steady_state_config3: 0.117 ms per 65,536-group tick, 285 GB/s).
+// k_tick_lite gives each group eight lanes (eight Raft groups per wave, lane j
+// = peer j), so eight groups' chains overlap in one wave. It settles a group
+// only when every follower's reply is a success that needs no compare:
+// prevLogTerm matches and either n = 0 (heartbeat, IC_HB) or the follower's
+// log ends at prev (a pure append: IC_MERGE with an empty compare range, so
+// the first mismatch is prev + 1), the append fits the ring, the leader's
+// entries to send span at most kLiteSpan Indexes, and a1 settles at its top:
+// with every follower at `last`, min(M*, last) = last (the order statistic of
+// the last evaluation is `last`), and log[last] is currentTerm, or below it
+// under the leader's terms_sorted proof. Every other group (stale or
+// adopting-with-conflict replies, snapshots, conflicts, merges that compare,
+// Figure-8 scans, capacity) is recognised before any store and appended to a
+// device list that k_tick_list runs through the full tick
+// (mraft_tick_body.inc). Per group the stores are the full tick's.
+constexpr int kLiteSpan = 64;
+
+template <int P>
+__global__ __launch_bounds__(64) void k_tick_lite(Dev s, const int32_t *__restrict__ leader_peer,
+                                                  int32_t *__restrict__ gflags, Export ex,
+                                                  int32_t *__restrict__ fb_list, unsigned *__restrict__ fb_count) {
+  const int lane = lane_id(), j = lane & 7, gbase = lane & ~7;
+  int wb = (int)blockIdx.x;  // XCD-contiguous wave ranges, as k_tick_group
+  {
+    const int nb = (int)gridDim.x, x = wb & 7, per = nb >> 3, rem = nb & 7;
+    wb = x * per + min(x, rem) + (wb >> 3);
+  }
+  const int g = wb * 8 + (lane >> 3);
+  const bool live = g < s.G;
+  const int L = s.L;
+  const int lpv = live ? leader_peer[g] : -1;
+  if (live && (lpv < 0 || lpv >= P) && j == 0) {
+    if (gflags) gflags[g] = lpv >= P ? MRAFT_G_ERROR : 0;
+    if (ex.commit) {
+      const long long s0 = (long long)g * P;  // mraft_export_group_status: replica 0
+      ex.put(g, s.commit[s0], s.term[s0], s.role[s0]);
+    }
+  }
+  bool go = live && lpv >= 0 && lpv < P;
+  const int lp = go ? lpv : 0;
+  const long long ld = (long long)g * P + lp, f = (long long)g * P + j;
+  // Every load that depends only on the leader index, one round trip: lanes
+  // 0-6 of the group the leader's scalars, lane j < P nextIndex[j] and, for a
+  // follower, its term, dummy, last, commit and ring head.
+  int vs = 0, nj = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
+  if (go) {
+    const int32_t *src = j == 0 ? s.role : j == 1 ? s.term : j == 2 ? s.commit : j == 3 ? s.last
+                         : j == 4 ? s.dummy : j == 5 ? s.head : j == 6 ? s.srt : nullptr;
+    if (src) vs = src[ld];
+    if (j < P) nj = s.next[ld * P + j];
+    if (j < P && j != lp) {
+      fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fcommit = s.commit[f]; fhead = s.head[f];
+    }
+  }
+  auto bc = [&](int v, int k) { return __shfl(v, gbase + k, 64); };
+  const int role = bc(vs, 0), T = bc(vs, 1), c0 = bc(vs, 2), last = bc(vs, 3), ldummy = bc(vs, 4),
+            lhead = bc(vs, 5), lsrt = bc(vs, 6);
+  if (go && (role != kLeader || c0 < ldummy)) {  // appendOneRound returns (:22-25) / MRAFT_ITEM_BAD_STATE
+    if (j == 0) {
+      if (gflags) gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
+      ex.put(g, c0, T, role);
+    }
+    go = false;
+  }
+  const long long lrow = ld * L;
+  const int lb = lhead - ldummy;
+  const bool isf = go && j < P && j != lp;
+  const int prev = nj - 1, n = last - prev;                              // :26, :50
+  // snapshot, panic, stale, below / beyond the follower's log: the full tick
+  bool fb = isf && (prev < ldummy || prev > last || T < fterm || prev < fdummy || prev > flast);
+  int pt = 0, ft = 0, probe = 0;
+  if (isf && !fb) {
+    pt = s.log[lrow + ring(prev + lb, L)];                               // :49
+    ft = s.log[f * L + ring(prev - fdummy + fhead, L)];                  // :128
+  }
+  if (go && j == lp) probe = s.log[lrow + ring(last + lb, L)];           // a1's probe (:98)
+  // a conflict, a merge that compares (the follower holds entries past prev),
+  // or an append past the ring's capacity: the full tick
+  if (isf && !fb && (ft != pt || (n > 0 && (flast != prev || (long long)last - fdummy > (long long)L - 1))))
+    fb = true;
+  const bool mrg = isf && !fb && n > 0;
+  int mlo = mrg ? prev + 1 : INT32_MAX;  // the leader's first entry any follower needs
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) mlo = min(mlo, __shfl_xor(mlo, o, 64));
+  const int t = bc(probe, lp);
+  int commit = c0;
+  bool gfb = ((__ballot(fb) >> gbase) & 0xffull) != 0;
+  if (go && !gfb) {
+    if (mlo != INT32_MAX && (long long)last - mlo + 1 > kLiteSpan) gfb = true;
+    if (last > c0) {                                                     // top = last (above)
+      if (t == T) commit = last;                                         // :98-100
+      else if (!(lsrt && t < T)) gfb = true;                             // a Figure-8 scan: the full tick
+    }
+  }
+  // the groups for the full tick, one atomic per wave
+  {
+    const bool push = go && gfb && j == 0;
+    const unsigned long long pm = __ballot(push);
+    if (pm) {
+      const int l0 = first_lane(pm);
+      unsigned base = 0;
+      if (lane == l0) base = atomicAdd(fb_count, (unsigned)__popcll(pm));
+      base = (unsigned)__shfl((int)base, l0, 64);
+      if (push) fb_list[base + (unsigned)__popcll(pm & ((1ull << lane) - 1))] = g;
+    }
+  }
+  const bool w = go && !gfb;
+  // The appended entries: leader Indexes [mlo, last], lane j of the group takes
+  // mlo + j, mlo + j + 8, ..., stored into every merging follower whose prev
+  // lies below (:149-155; the compare ranges are empty).
+  {
+    int fp[P], fd[P], fh[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) { fp[q] = bc(prev, q); fd[q] = bc(fdummy, q); fh[q] = bc(fhead, q); }
+    const unsigned mm = (unsigned)((__ballot(mrg) >> gbase) & 0xffull);
+    if (w && mm) {
+      for (int k = j; k <= last - mlo; k += 8) {  // (an Index loop could overflow near 2^31)
+        const int idx = mlo + k;
+        const int e = s.log[lrow + ring(idx + lb, L)];
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+          if (((mm >> q) & 1) && idx > fp[q]) s.log[((long long)g * P + q) * L + ring(idx - fd[q] + fh[q], L)] = e;
+      }
+    }
+  }
+  bool fcadv = false;
+  if (w && isf) {
+    mark_persist(s, f, MRAFT_PERSIST_STATE);                             // :111
+    if (T > fterm) { s.term[f] = T; s.voted[f] = -1; }                   // :116-118
+    s.role[f] = kFollower;                                               // :120
+    int newlast = flast;
+    if (n > 0) {
+      newlast = last;                                                    // prev + n
+      s.last[f] = newlast;
+      // terms_sorted after appending from prev + 1 (the tick's rule, mk = 0)
+      bool fl = lsrt != 0;
+      if (fl && prev == ldummy) fl = pt <= s.log[lrow + ring(prev + 1 + lb, L)];
+      const int sw = !fl ? 0 : prev == fdummy ? 1 : -1;
+      if (sw >= 0) s.srt[f] = sw;
+    }
+    if (c0 > fcommit) {                                                  // :157-160
+      s.commit[f] = min(c0, newlast);
+      fcadv = true;
+    }
+    s.next[ld * P + j] = last + 1;                                       // :76-77
+    s.match[ld * P + j] = last;
+  }
+  const bool anyadv = ((__ballot(fcadv) >> gbase) & 0xffull) != 0;
+  if (w && j == 0) {
+    if (commit != c0) s.commit[ld] = commit;
+    if (gflags)
+      gflags[g] = MRAFT_G_ACTIVE | (commit != c0 ? MRAFT_G_COMMITTED : 0) | (anyadv ? MRAFT_G_FOLLOWER_COMMIT : 0);
+    ex.put(g, commit, T, kLeader);
+  }
+}
+
+// The light tick's fallback: the groups k_tick_lite listed, each through the
+// full tick (one wave per group, grid-stride over the device count, so any
+// grid is exact; the host sizes it from the previous tick's count). The first
+// workgroup zeroes the counter the next light tick uses and publishes this
+// tick's count to the host's pinned word.
+template <int P>
+__global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_list(Dev s, const int32_t *__restrict__ leader_peer,
+                                                   int32_t *__restrict__ gflags,
+                                                   unsigned long long *__restrict__ counts, Export ex,
+                                                   const int32_t *__restrict__ list, const unsigned *__restrict__ cnt,
+                                                   unsigned *__restrict__ cnt_next, long long *__restrict__ hint) {
+  constexpr bool COUNT = false;
+  constexpr int NI = P - 1;
+  const int lane = lane_id();
+  const unsigned nl = (unsigned)uni((int)*cnt);
+  if (blockIdx.x == 0 && lane == 0) {
+    *cnt_next = 0;
+    if (hint) *hint = (long long)nl;
+  }
+  for (unsigned k = blockIdx.x; k < nl; k += gridDim.x) {
+    const int g = uni(list[k]);
+#define TICK_EXIT continue
+#include "mraft_tick_body.inc"
+#undef TICK_EXIT
+  }
+}
+
+template <int P>
+void launch_tick_light_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, Export ex, const LiteBufs &lb,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_tick_lite<P>, dim3((unsigned)((s.G + 7) / 8)), dim3(64), 0, st, s, lpeer, gflags, ex, lb.list,
+                     lb.cnt);
+  hipLaunchKernelGGL(k_tick_list<P>, dim3((unsigned)lb.grid), dim3(64), 0, st, s, lpeer, gflags,
+                     (unsigned long long *)nullptr, ex, (const int32_t *)lb.list, (const unsigned *)lb.cnt,
+                     lb.cnt_next, lb.hint);
 }
 
 template <int P, bool COUNT>
@@ -744,6 +503,21 @@ extern "C" int mraft_debug_tick_trace(void *dst, long long nbytes) {
 void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
                            int32_t *exp_term_leader, hipStream_t st) {
   launch_tick_c<false>(s, lpeer, gflags, nullptr, Export{exp_commit, exp_term_leader}, st);
+}
+
+void launch_replicate_tick_light(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
+                                 int32_t *exp_term_leader, const LiteBufs &lb, hipStream_t st) {
+  const Export ex{exp_commit, exp_term_leader};
+  switch (s.P) {
+    case 2: launch_tick_light_p<2>(s, lpeer, gflags, ex, lb, st); break;
+    case 3: launch_tick_light_p<3>(s, lpeer, gflags, ex, lb, st); break;
+    case 4: launch_tick_light_p<4>(s, lpeer, gflags, ex, lb, st); break;
+    case 5: launch_tick_light_p<5>(s, lpeer, gflags, ex, lb, st); break;
+    case 6: launch_tick_light_p<6>(s, lpeer, gflags, ex, lb, st); break;
+    case 7: launch_tick_light_p<7>(s, lpeer, gflags, ex, lb, st); break;
+    case 8: launch_tick_light_p<8>(s, lpeer, gflags, ex, lb, st); break;
+    default: launch_tick_c<false>(s, lpeer, gflags, nullptr, ex, st);  // P == 1: k_tick_p1 is a lane per group already
+  }
 }
 
 void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,

@@ -153,6 +153,19 @@ class Engine:
     def tick_shards(self) -> int:
         return int(self._lib.mraft_get_tick_shards(self._h))
 
+    def set_tick_mode(self, mode: int):
+        """TICK_FULL (default) or TICK_LIGHT (mraft_set_tick_mode): the light
+        tick settles steady-state groups eight per wave and runs the rest
+        through the full tick; outputs are identical."""
+        _ck(self._lib.mraft_set_tick_mode(self._h, mode), "mraft_set_tick_mode")
+
+    def tick_mode(self) -> int:
+        return int(self._lib.mraft_get_tick_mode(self._h))
+
+    def tick_light_fallbacks(self) -> int:
+        """Groups the last completed light tick sent to the full tick (-1: none yet)."""
+        return int(self._lib.mraft_tick_light_fallbacks(self._h))
+
     def set_stage_capacity(self, words: int):
         """Words of staged entries mraft_handle_append_entries may use for its
         deferred items (mraft_set_stage_capacity; 0 forces the ordered fallback)."""

@@ -30,3 +30,18 @@ _ensure_built()
 def gpu_available():
     import torch
     return torch.cuda.is_available()
+
+
+# MRAFT_TEST_TICK_MODE=light runs every engine the tests create in
+# MRAFT_TICK_LIGHT (mraft_set_tick_mode): the whole GPU suite then checks the
+# light tick against the oracle wherever it checks the full one.
+if os.environ.get("MRAFT_TEST_TICK_MODE") == "light":
+    from multiraft_amd import engine as _engine_mod
+
+    _engine_init = _engine_mod.Engine.__init__
+
+    def _light_init(self, *a, **k):
+        _engine_init(self, *a, **k)
+        self.set_tick_mode(1)
+
+    _engine_mod.Engine.__init__ = _light_init

@@ -34,7 +34,7 @@ def test_library_exports_every_symbol():
 
 def test_abi_version_and_struct_sizes():
     lib = _abi.lib()
-    assert lib.mraft_abi_version() == _abi.ABI_VERSION == 5
+    assert lib.mraft_abi_version() == _abi.ABI_VERSION == 6
     assert _abi.AE_ARGS.itemsize == 40
     assert _abi.AE_REPLY.itemsize == 16
     assert _abi.RV_RESULT.itemsize == 20

@@ -1,0 +1,171 @@
+"""The light tick (MRAFT_TICK_LIGHT, mraft_set_tick_mode in include/mraft.h):
+one launch settles, eight Raft groups per wave, every group whose followers all
+reply success without a compare (a heartbeat, or an append at the follower's
+last Index) and whose commitIndex settles at log[last]; a second launch runs
+every other group through the full tick. Both are the reference's
+appendOneRound -> HandleAppendEntries -> processAppendEntriesReply ->
+advanceCommitIndexForLeader (src/raft/raft_append_entry.go:20-162, with
+Start, src/raft/raft.go:90-104, between ticks).
+
+Every case compares the GPU with the CPU oracle bit for bit after every tick
+(group flags, the fused GetState words where exported, the whole state and
+its persist bits), and reads which path the groups took
+(mraft_tick_light_fallbacks): steady-state runs where most groups settle in
+the light launch, seeded random states where most do not, a batch past the
+light launch's 64-entry span after a steady tick (its fallback grid, sized
+from the previous count, is then far smaller than the list: the grid-stride
+loop), the top of the Index domain, shards, P = 1 and the mode calls."""
+import numpy as np
+import pytest
+
+from message_cases import shift_indices, top_offset
+from oracle_lib import Oracle, assert_states_equal, rotate_rings
+from random_states import random_tick_state
+
+from multiraft_amd import TICK_FULL, TICK_LIGHT, Engine, MraftError, synth_tick_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _active(gf):
+    return int((gf & 1).astype(bool).sum())
+
+
+def _step(e, o, lp, G, P, L, ctx, export):
+    if export:
+        gf, c, tl = e.replicate_tick_export(lp)
+        oc, otl = o.export_group_status(lp)
+        assert np.array_equal(c, oc) and np.array_equal(tl, otl), f"{ctx}: export words"
+    else:
+        gf = e.replicate_tick(lp)
+    ogf = o.replicate_tick(lp)
+    assert np.array_equal(gf, ogf), f"{ctx}: group flags"
+    assert_states_equal(e.store_state(), o.state(), G, P, L, ctx)
+    return gf
+
+
+def _start_all(e, o, lp, G, P, rng, cmax, frac=1.0):
+    g = np.flatnonzero(rng.random(G) < frac)
+    if len(g) == 0:
+        return
+    slots = (g * P + lp[g]).astype(np.int32)
+    counts = rng.integers(0, cmax + 1, size=len(slots)).astype(np.int32)
+    for a, b in zip(e.start(slots, counts), o.start(slots, counts)):
+        assert np.array_equal(a, b), "start"
+
+
+def _steady_run(G, P, L, seed, shards, steps, cmax=4, export=False, state=None, lp=None):
+    rng = np.random.default_rng(seed)
+    if state is None:
+        state, lp, _ = synth_tick_state(G, P, L, seed=seed)
+    o = Oracle(G, P, L, state)
+    fbs = []
+    with Engine(G, P, L) as e:
+        e.load_state(state)
+        e.set_tick_shards(min(shards, G))
+        e.set_tick_mode(TICK_LIGHT)
+        assert e.tick_mode() == TICK_LIGHT
+        for k in range(steps):
+            gf = _step(e, o, lp, G, P, L, f"seed {seed} step {k}", export)
+            fbs.append((e.tick_light_fallbacks(), _active(gf)))
+            _start_all(e, o, lp, G, P, rng, cmax)
+    return fbs
+
+
+@pytest.mark.parametrize("P,L,shards", [(3, 64, 1), (5, 256, 2), (8, 99, 1), (5, 128, 3), (2, 37, 1), (7, 512, 2)])
+def test_light_steady_state_gpu(P, L, shards):
+    """Ticks with Start() of 0-4 entries at every leader between them: after
+    the first ticks have repaired the seeded conflicts, most groups settle in
+    the light launch."""
+    G = 1024
+    fbs = _steady_run(G, P, L, 9100 + P * 7 + L, shards, steps=8, export=(shards == 2))
+    fb, act = fbs[-1]
+    assert 0 <= fb < act, fbs            # the light launch settled groups
+    assert fb <= act // 2, fbs           # ... most of the active ones, once steady
+
+
+@pytest.mark.parametrize("seed", list(range(16)))
+def test_light_fuzz_gpu(seed):
+    """Seeded random states (tests/random_states.py: diverging tails, snapshot
+    branches, bad-state leaders, rotated rings), 1-3 shards, Start() and leader
+    moves between ticks: every path of the full tick mixed with the light one."""
+    rng = np.random.default_rng(8800 + seed)
+    P = int(rng.choice([2, 3, 5, 7, 8]))
+    L = int(rng.choice([32, 37, 64, 99, 128, 256]))
+    G = int(rng.integers(150, 700))
+    st, lp = random_tick_state(rng, G, P, L, monotone=bool(rng.random() < 0.5), snap=bool(rng.random() < 0.3))
+    if rng.random() < 0.7:
+        st = rotate_rings(st, G, P, L, rng, frac=float(rng.uniform(0.3, 1.0)))
+    shards = int(rng.choice([1, 2, 3]))
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        e.set_tick_shards(min(shards, G))
+        e.set_tick_mode(TICK_LIGHT)
+        for step in range(6):
+            _step(e, o, lp, G, P, L, f"seed {seed} step {step} shards {shards}", export=bool(step & 1))
+            assert e.tick_light_fallbacks() >= 0
+            _start_all(e, o, lp, G, P, rng, 3, frac=0.5)
+            moved = rng.random(G) < 0.05
+            lp = np.where(moved, rng.integers(0, P, size=G), lp).astype(np.int32)
+
+
+def test_light_span_and_grid_stride_gpu():
+    """Steady ticks (small fallback counts: the next fallback grid is 2,048
+    workgroups), then Start() of 70 entries at every leader: every active group
+    exceeds the light launch's 64-entry span and goes to the full tick, 6,000
+    groups through a 2,048-workgroup grid-stride loop; then steady again."""
+    G, P, L = 6000, 5, 512
+    rng = np.random.default_rng(77)
+    st, lp, _ = synth_tick_state(G, P, L, seed=4242)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        e.set_tick_mode(TICK_LIGHT)
+        assert e.tick_light_fallbacks() == -1  # no light tick yet
+        for k in range(5):
+            _step(e, o, lp, G, P, L, f"steady {k}", False)
+            _start_all(e, o, lp, G, P, rng, 2)
+        fb0 = e.tick_light_fallbacks()
+        g = np.arange(G)
+        slots = (g * P + lp).astype(np.int32)
+        counts = np.full(G, 70, np.int32)
+        for a, b in zip(e.start(slots, counts), o.start(slots, counts)):
+            assert np.array_equal(a, b)
+        gf = _step(e, o, lp, G, P, L, "span 70", True)
+        fb1 = e.tick_light_fallbacks()
+        assert fb1 > 2 * 2048 and fb1 >= fb0, (fb0, fb1, _active(gf))
+        for k in range(3):
+            _step(e, o, lp, G, P, L, f"steady again {k}", False)
+            _start_all(e, o, lp, G, P, rng, 1)
+
+
+@pytest.mark.parametrize("j", [0, 5])
+def test_light_top_of_index_domain_gpu(j):
+    """Steady ticks whose Indexes end within j of 2^31 - 2 (include/mraft.h: the
+    Index domain): the light launch's entry loop and ring arithmetic there."""
+    G, P, L, steps, cmax = 512, 5, 256, 6, 3
+    st0, lp, _ = synth_tick_state(G, P, L, seed=5150 + j)
+    st = shift_indices(st0, top_offset(st0, j + steps * cmax))
+    fbs = _steady_run(G, P, L, 5150 + j, 2, steps, cmax=cmax, state=st, lp=lp)
+    assert fbs[-1][0] < fbs[-1][1], fbs
+
+
+def test_light_mode_calls_and_p1_gpu():
+    """The mode calls (bad modes rejected, the mode kept across shard changes)
+    and P = 1, where the one-lane-per-group tick already is the light form."""
+    G, P, L = 64, 1, 16
+    st, lp, _ = synth_tick_state(G, P, L, seed=3)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        assert e.tick_mode() == TICK_FULL
+        with pytest.raises(MraftError):
+            e.set_tick_mode(2)
+        e.set_tick_mode(TICK_LIGHT)
+        e.set_tick_shards(2)
+        assert e.tick_mode() == TICK_LIGHT
+        for k in range(2):
+            _step(e, o, lp, G, P, L, f"P=1 step {k}", bool(k))
+        e.set_tick_mode(TICK_FULL)
+        _step(e, o, lp, G, P, L, "P=1 full", False)

@@ -45,6 +45,16 @@ for st in ${DO:-tests bench}; do
       echo "== deferred"
       timeout -k 10 400 python3 tools/bench_deferred.py > "$OUT/deferred.json" 2> "$OUT/deferred.err" || { tail -5 "$OUT/deferred.err"; exit 1; }
       python3 -c "import json; d=json.loads(open('$OUT/deferred.json').read().strip().splitlines()[-1]); [print(k, round(v['ms_per_call'], 4), round(v['first_call_ms'], 3), round(v.get('vs_plain', 1.0), 3)) for k, v in d.items()]" ;;
+    steady)
+      # the steady-state ticks alone, full and light (tools/bench_steady.py)
+      echo "== steady"
+      timeout -k 10 400 python3 tools/bench_steady.py > "$OUT/steady.json" 2> "$OUT/steady.err" || { tail -5 "$OUT/steady.err"; exit 1; }
+      python3 -c "import json; e=json.loads(open('$OUT/steady.json').read().strip().splitlines()[-1]); li=e['light']; print('full', round(e['tick_ms_steady'],4), 'light', round(li['tick_ms_steady'],4), 'x', round(li['speedup_tick_steady'],2), 'same', li['state_equals_full'], 'fb', li['fallback_groups_steps'])" ;;
+    lighttests)
+      # the whole tick-related GPU suite with every engine in MRAFT_TICK_LIGHT (tests/conftest.py)
+      echo "== lighttests"
+      MRAFT_TEST_TICK_MODE=light timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${LTESTS:-tick or persist or ring or odd or index or snapshot or sim or multirank}" > "$OUT/pytest_light.log" 2>&1
+      rc=$?; tail -3 "$OUT/pytest_light.log"; [ $rc -eq 0 ] || { grep -E "FAIL|Error" "$OUT/pytest_light.log" | head -20; exit 1; } ;;
     abmsg)
       # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
       echo "== abmsg ${VARIANTS:-prebuilt}"

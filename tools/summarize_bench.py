@@ -28,3 +28,9 @@ if "config4_one_gpu" in s:
 cb = d.get("cpu_baseline")
 if cb:
     print("cpu baseline", f"{cb['value']:.4g}", cb["cores"])
+if "steady_state_config3" in s:
+    e = s["steady_state_config3"]
+    li = e.get("light", {})
+    print("steady state tick ms: full", round(e["tick_ms_steady"], 4), "light", round(li.get("tick_ms_steady", 0), 4),
+          "speedup", round(li.get("speedup_tick_steady", 0), 2), "same", li.get("state_equals_full"),
+          "fallbacks", li.get("fallback_groups_steps", [])[:6], "...", li.get("fallback_groups_steps", [])[-2:])
