@@ -285,9 +285,11 @@ def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
     #3 batches heavy in deferred items (deferred_batch_state), against the
     plain batch on the same copies: per call, and per message. Each variant on
     a fresh engine: its first call runs on the minimal deferred grid (no
-    earlier count: `first_call_ms`), then `steps` timed calls, each on a state
-    copy restored from that variant's master (one event before and one after
-    the handle call)."""
+    earlier count) and, past the stage, in the ordered fallback
+    (`first_call_ms`), then `steps` timed calls, each on a state copy restored
+    from that variant's master (one event before and one after the handle
+    call); under MRAFT_STAGE_AUTO (the default) the second call grows the stage
+    to the first call's need (`ms_calls` has every call)."""
     import torch
 
     from multiraft_amd import DEVICE, Engine, _abi
@@ -340,10 +342,12 @@ def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
                 src = np.where(ok & (ah["n_entries"] > 0), ah["entries_offset"] // L, -1)
                 ndef = int((ok & np.isin(ah["slot"], src[src >= 0])).sum())
                 assert ok.all(), f"{name}: gather errors"
+        cap_end = int(lib.mraft_get_stage_capacity(e._h))
         e.close()
         out[name] = {"messages": n, "deferred_items": ndef, "stage_capacity_words": cap if cap is not None else
-                     "default (4 Mi)", "first_call_ms": times[0], "ms_per_call": float(np.mean(times[1:])),
-                     "ns_per_message": float(np.mean(times[1:])) * 1e6 / n}
+                     "MRAFT_STAGE_AUTO (from 4 Mi)", "stage_capacity_words_end": cap_end,
+                     "first_call_ms": times[0], "ms_per_call": float(np.mean(times[1:])),
+                     "ms_calls": [round(t, 4) for t in times], "ns_per_message": float(np.mean(times[1:])) * 1e6 / n}
     base = out["plain"]
     for name in out:
         if name != "plain":

@@ -384,8 +384,8 @@ int mraft_gather_append_args(mraft_engine *h, const int32_t *slots,
  * a batch larger than any before grows the engine's buffers in stream order,
  * without waiting either). n <= 2^31 - 1.
  * Staged entries use the engine's stage (mraft_set_stage_capacity); a batch
- * that needs more runs its deferred items in an order that needs no stage (one
- * wave, slower), with the same results. */
+ * that needs more runs its deferred items in an order that needs no stage
+ * (slower), with the same results. */
 int mraft_handle_append_entries(mraft_engine *h, const mraft_ae_args *args,
                                 int64_t n, const int32_t *entry_terms,
                                 int64_t n_entry_terms, mraft_ae_reply *replies,
@@ -407,11 +407,16 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args,
                                    int32_t where);
 
 /* Capacity, in entry words, of the device stage mraft_handle_append_entries
- * copies the entries of deferred by-reference items into (default 4 Mi words,
- * 16 MiB; allocated on first use). A batch needing more is still handled
- * exactly, in the ordered fallback (as is every batch when the stage cannot
- * be allocated). words in [0, 2^31). Returns MRAFT_OK;
+ * copies the entries of deferred by-reference items into (allocated on first
+ * use). A batch needing more is still handled exactly, in the ordered
+ * fallback (as is every batch when the stage cannot be allocated).
+ * words in [0, 2^31): that fixed capacity. MRAFT_STAGE_AUTO (the default,
+ * from 4 Mi words = 16 MiB; ABI 6): after a batch that needed more, the calls
+ * after it get a stage of 5/4 of that need (stream-ordered growth, the device
+ * publishes the need to a pinned word: no host wait), up to 2^31 - 1 words;
+ * growth stops at the first allocation that fails. Returns MRAFT_OK;
  * mraft_get_stage_capacity returns the current capacity (-1: null handle). */
+enum { MRAFT_STAGE_AUTO = -1 };
 int mraft_set_stage_capacity(mraft_engine *h, int64_t words);
 int64_t mraft_get_stage_capacity(const mraft_engine *h);
 

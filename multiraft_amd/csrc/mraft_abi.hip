@@ -34,6 +34,16 @@ constexpr int kDeferGridMax = 1 << 16;
 // workgroups, twice the previous light tick's count, at most the groups (a
 // grid-stride loop makes any grid exact; an empty one costs a few µs).
 constexpr long long kLiteGridMin = 2048;
+constexpr long long kLiteGridUnknown = 8192;
+// The engine's pinned host words (device-written, read by the host when it
+// enqueues): [0] the last by-reference AppendEntries call's deferred count,
+// [1] the staged words of the last call that exceeded the stage (its need),
+// [kHintLite + s] the last light tick's fallback count of shard s.
+constexpr int kHintLite = 2;
+constexpr int kHintWords = kHintLite + kMaxShards;
+// MRAFT_STAGE_AUTO grows the stage to 5/4 of a batch's need, in 1 Mi-word
+// steps, up to 2^31 - 1 words (8 GiB).
+constexpr int64_t kStageStep = (int64_t)1 << 20;
 // Words of the fallback's per-workgroup cycle buffers (nslot x L, at most this).
 constexpr int64_t kCycSlotWords = (int64_t)1 << 25;  // 8,192 buffers at L = 4,096 (128 MiB)
 
@@ -61,12 +71,13 @@ struct mraft_engine {
   uint32_t epoch = 0;
   unsigned long long *ae_total = nullptr;  // AppendEntries by reference: staged words, deferred items << 32
   int64_t stage_cap = kDefaultStageWords;  // words of staged entries the deferred launch may use
+  bool stage_auto = true;                  // MRAFT_STAGE_AUTO: grow stage_cap to the last overflow's need
   long long *dhint = nullptr;  // pinned host word: the last by-reference call's deferred count (device-written)
   long long *dhint_dev = nullptr;  // its device-side address
-  // MRAFT_TICK_LIGHT (mraft_set_tick_mode): the list of groups for the full
-  // tick (G words, shard s at its first group), a counter pair per shard (the
-  // light launch counts into one, the fallback zeroes the other for the next
-  // tick) and per shard the last fallback count, pinned (dhint + 1 + s)
+  // MRAFT_TICK_LIGHT (mraft_set_tick_mode): the lists of groups for the full
+  // tick (shard s at its first group + 512 s), a pair of counter sets per shard (the light
+  // launch counts into one, the fallback zeroes the other for the next tick)
+  // and per shard the last fallback count, pinned (dhint + kHintLite + s)
   int32_t tick_mode = MRAFT_TICK_FULL;
   int32_t *lite_list = nullptr;
   unsigned *lite_cnt = nullptr;
@@ -232,11 +243,13 @@ int alloc_async(mraft_engine *h, void **p, size_t bytes, const char *what);
 int ensure_lite(mraft_engine *h) {
   if (h->lite_list) return MRAFT_OK;
   void *l = nullptr, *c = nullptr;
-  TRY(alloc_async(h, &l, (size_t)h->G * sizeof(int32_t), "light tick list"));
+  // a shard of G_s groups needs lite_list_words(G_s) <= G_s + 512 words
+  TRY(alloc_async(h, &l, ((size_t)h->G + 512 * kMaxShards) * sizeof(int32_t), "light tick list"));
   h->lite_list = (int32_t *)l;
-  TRY(alloc_async(h, &c, 2 * kMaxShards * sizeof(unsigned), "light tick counters"));
+  const size_t cb = (size_t)2 * kMaxShards * mraft::kLiteCntWords * sizeof(unsigned);
+  TRY(alloc_async(h, &c, cb, "light tick counters"));
   h->lite_cnt = (unsigned *)c;
-  HIP_TRY(hipMemsetAsync(h->lite_cnt, 0, 2 * kMaxShards * sizeof(unsigned), h->stream));
+  HIP_TRY(hipMemsetAsync(h->lite_cnt, 0, cb, h->stream));
   for (int s = 0; s < kMaxShards; ++s) h->lite_par[s] = 0;
   return MRAFT_OK;
 }
@@ -252,12 +265,14 @@ void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const i
   mraft::LiteBufs lb;
   const int par = h->lite_par[s];
   h->lite_par[s] ^= 1;
-  lb.list = h->lite_list + g0;
-  lb.cnt = h->lite_cnt + 2 * s + par;
-  lb.cnt_next = h->lite_cnt + 2 * s + (par ^ 1);
-  lb.hint = h->dhint_dev + 1 + s;
-  const long long prev = ((volatile long long *)h->dhint)[1 + s];
-  const long long gr = prev < 0 ? (long long)d.G : std::max(kLiteGridMin, 2 * prev);
+  lb.list = h->lite_list + g0 + 512 * s;
+  lb.cnt = h->lite_cnt + (2 * s + par) * mraft::kLiteCntWords;
+  lb.cnt_next = h->lite_cnt + (2 * s + (par ^ 1)) * mraft::kLiteCntWords;
+  lb.hint = h->dhint_dev + kHintLite + s;
+  const long long prev = ((volatile long long *)h->dhint)[kHintLite + s];
+  // no completed light tick yet (e.g. the first ticks enqueued back to back):
+  // one wave per SIMD slot, grid-stride
+  const long long gr = prev < 0 ? kLiteGridUnknown : std::max(kLiteGridMin, 2 * prev);
   lb.grid = (int)std::max(1ll, std::min(gr, (long long)d.G));
   mraft::launch_replicate_tick_light(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), lb, st);
 }
@@ -422,14 +437,15 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
   h->stream = h->own_stream;
   {
     void *hp = nullptr;
-    if (hipHostMalloc(&hp, sizeof(long long) * (1 + kMaxShards), hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc(&hp, sizeof(long long) * kHintWords, hipHostMallocMapped) != hipSuccess) {
       (void)hipStreamDestroy(h->own_stream);
       delete h;
       return fail(MRAFT_E_NOMEM, "pinned host word allocation failed");
     }
     h->dhint = (long long *)hp;
     *(volatile long long *)h->dhint = 0;
-    for (int k = 1; k <= kMaxShards; ++k) ((volatile long long *)h->dhint)[k] = -1;  // no light tick yet
+    ((volatile long long *)h->dhint)[1] = 0;
+    for (int k = 0; k < kMaxShards; ++k) ((volatile long long *)h->dhint)[kHintLite + k] = -1;  // no light tick yet
     void *dp = nullptr;
     if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
       (void)hipHostFree(hp);
@@ -735,9 +751,22 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   db.cyc = (int32_t *)(db.fb + nn);
   db.cslot = db.cyc + L;
   db.hint = h->dhint_dev;
+  // MRAFT_STAGE_AUTO: a batch that exceeded the stage (its need published by
+  // the device, dhint[1]) grows it for the calls after it (stream-ordered)
+  if (h->stage_auto) {
+    const long long need = ((volatile long long *)h->dhint)[1];
+    if (need > h->stage_cap) {
+      const int64_t want = std::min<int64_t>((int64_t)INT32_MAX, (need + need / 4 + kStageStep - 1) / kStageStep * kStageStep);
+      h->stage_cap = want;
+    }
+  }
   // the stage: when it cannot be allocated the batch runs with none (every
-  // staged item then takes the ordered fallback: the same results, slower)
-  if (h->stage_cap > 0 && scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage) != MRAFT_OK) stage = nullptr;
+  // staged item then takes the ordered fallback: the same results, slower);
+  // an automatic stage stops growing there
+  if (h->stage_cap > 0 && scratch(h, 16, sizeof(int32_t) * (size_t)h->stage_cap, &stage) != MRAFT_OK) {
+    stage = nullptr;
+    h->stage_auto = false;
+  }
   const int ni = h->P - 1 < 1 ? 1 : h->P - 1 > 7 ? 7 : h->P - 1;
   const int64_t n_log = gp_of(h) * h->L;
   mraft::launch_claim_ae((const mraft_ae_args *)a, n, n_log, h->L, gp_of(h), ni, h->claim, h->srcmark, h->epoch,
@@ -751,8 +780,13 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
 
 int mraft_set_stage_capacity(mraft_engine *h, int64_t words) {
   TRY(enter(h));
+  if (words == MRAFT_STAGE_AUTO) {
+    h->stage_auto = true;
+    return MRAFT_OK;
+  }
   if (words < 0 || words > INT32_MAX) return fail(MRAFT_E_INVAL, "stage capacity %lld out of [0, 2^31)", (long long)words);
   h->stage_cap = words;
+  h->stage_auto = false;
   return MRAFT_OK;
 }
 
@@ -1300,7 +1334,7 @@ int64_t mraft_tick_light_fallbacks(mraft_engine *h) {
   if (!h) return -1;
   long long t = 0;
   for (int s = 0; s < std::max(1, (int)h->nshards); ++s) {
-    const long long v = ((volatile long long *)h->dhint)[1 + s];
+    const long long v = ((volatile long long *)h->dhint)[kHintLite + s];
     if (v < 0) return -1;
     t += v;
   }

@@ -12,10 +12,16 @@ namespace mraft {
 void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
                            int32_t *exp_term_leader, hipStream_t st);
 // The light tick (MRAFT_TICK_LIGHT, mraft_tick.hip): k_tick_lite settles the
-// steady-state groups eight per wave and lists the others (list, cnt); the
-// fallback launch (grid workgroups, grid-stride) runs them through the full
-// tick, zeroes cnt_next (the next light tick's counter) and writes the count
-// to the pinned host word hint.
+// steady-state groups eight per wave (32 per workgroup) and lists the others,
+// per XCD: list region x = [x * lite_cap(G), ...), its count at cnt[32 x]
+// (eight counters, one 128-B line each); the fallback launch (grid
+// workgroups, grid-stride) runs them through the full tick, zeroes cnt_next
+// (the next light tick's counters) and writes the total to the pinned host
+// word hint. A list of G groups needs at most lite_list_words(G) words.
+inline int lite_blocks(int G) { return (G + 31) / 32; }
+inline int lite_cap(int G) { return (lite_blocks(G) + 7) / 8 * 32; }
+inline int64_t lite_list_words(int G) { return 8 * (int64_t)lite_cap(G); }
+constexpr int kLiteCntWords = 8 * 32;  // one light tick's counters
 struct LiteBufs {
   int32_t *list;
   unsigned *cnt, *cnt_next;

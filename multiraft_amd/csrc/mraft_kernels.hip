@@ -357,7 +357,8 @@ struct HsArgs {
   int32_t *cslot;            // per-workgroup cycle buffers, nslot x L words
   int nslot;
   int32_t *cyc;              // the last workgroup's cycle buffer (L words)
-  long long *hint;           // pinned host word: the last deferred count (the next call's grid)
+  long long *hint;           // pinned host words: [0] the last deferred count (the next call's grid),
+                             // [1] staged words of the last batch that exceeded the stage
   mraft_ae_reply *rep;
   int32_t *err;
   mraft_ae_result *res;  // optional: each item's reply as its co-resident leader folds it
@@ -990,6 +991,10 @@ __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_deferred(HsArgs ka
     ka.total[2] = (unsigned long long)nd;
     __hip_atomic_store(ka.hint, (long long)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // a batch whose staged words exceed the stage: the need, for the host's
+  // next call (the stage grows to it under MRAFT_STAGE_AUTO, mraft_abi.hip)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ka.hint && (long long)staged > ka.stage_cap)
+    __hip_atomic_store(ka.hint + 1, (long long)staged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (nd == 0) return;
   if ((long long)staged <= ka.stage_cap) {
     for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) handle_one<1, HM_DEFER>(ka, ka.defer[j], 1);

@@ -288,47 +288,54 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
 // device list that k_tick_list runs through the full tick
 // (mraft_tick_body.inc). Per group the stores are the full tick's.
 constexpr int kLiteSpan = 64;
+constexpr int kLiteWaves = 4;  // waves per light workgroup: 32 groups, one list reservation
 
 template <int P>
-__global__ __launch_bounds__(64) void k_tick_lite(Dev s, const int32_t *__restrict__ leader_peer,
-                                                  int32_t *__restrict__ gflags, Export ex,
-                                                  int32_t *__restrict__ fb_list, unsigned *__restrict__ fb_count) {
-  const int lane = lane_id(), j = lane & 7, gbase = lane & ~7;
-  int wb = (int)blockIdx.x;  // XCD-contiguous wave ranges, as k_tick_group
+__global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const int32_t *__restrict__ leader_peer,
+                                                               int32_t *__restrict__ gflags, Export ex,
+                                                               int32_t *__restrict__ fb_list,
+                                                               unsigned *__restrict__ fb_count, int cap) {
+  __shared__ unsigned sh_cnt, sh_base;
+  const int lane = lane_id(), j = lane & 7, gbase = lane & ~7, wv = (int)(threadIdx.x >> 6);
+  const int xcd = (int)(blockIdx.x & 7);
+  int wb = (int)blockIdx.x;  // XCD-contiguous workgroup ranges, as k_tick_group
   {
     const int nb = (int)gridDim.x, x = wb & 7, per = nb >> 3, rem = nb & 7;
     wb = x * per + min(x, rem) + (wb >> 3);
   }
-  const int g = wb * 8 + (lane >> 3);
+  if (threadIdx.x == 0) sh_cnt = 0;
+  const int g = (wb * kLiteWaves + wv) * 8 + (lane >> 3);
   const bool live = g < s.G;
   const int L = s.L;
-  const int lpv = live ? leader_peer[g] : -1;
-  if (live && (lpv < 0 || lpv >= P) && j == 0) {
-    if (gflags) gflags[g] = lpv >= P ? MRAFT_G_ERROR : 0;
-    if (ex.commit) {
-      const long long s0 = (long long)g * P;  // mraft_export_group_status: replica 0
-      ex.put(g, s.commit[s0], s.term[s0], s.role[s0]);
+  // Round trip 1: everything that does not depend on which peer leads. Lane
+  // j < P of the group: replica j's scalars, its persist bits and column j of
+  // the group's P x P nextIndex block (every candidate leader's view of j).
+  const long long r = (long long)g * P + j;
+  const bool rl = live && j < P;
+  int lpv = -1, rrole = 0, rterm = 0, rcommit = 0, rlast = 0, rdummy = 0, rhead = 0, rsrt = 0, rpd = 0;
+  int nx[P];
+#pragma unroll
+  for (int x = 0; x < P; ++x) nx[x] = 0;
+  if (live) lpv = leader_peer[g];
+  if (rl) {
+    rrole = s.role[r]; rterm = s.term[r]; rcommit = s.commit[r]; rlast = s.last[r];
+    rdummy = s.dummy[r]; rhead = s.head[r]; rsrt = s.srt[r];
+    if (s.pdirty) rpd = s.pdirty[r];
+#pragma unroll
+    for (int x = 0; x < P; ++x) nx[x] = s.next[((long long)g * P + x) * P + j];
+  }
+  auto bc = [&](int v, int k) { return __shfl(v, gbase + k, 64); };
+  {
+    const int c_0 = bc(rcommit, 0), t_0 = bc(rterm, 0), r_0 = bc(rrole, 0);
+    if (live && (lpv < 0 || lpv >= P) && j == 0) {
+      if (gflags) gflags[g] = lpv >= P ? MRAFT_G_ERROR : 0;
+      ex.put(g, c_0, t_0, r_0);  // mraft_export_group_status: replica 0
     }
   }
   bool go = live && lpv >= 0 && lpv < P;
   const int lp = go ? lpv : 0;
-  const long long ld = (long long)g * P + lp, f = (long long)g * P + j;
-  // Every load that depends only on the leader index, one round trip: lanes
-  // 0-6 of the group the leader's scalars, lane j < P nextIndex[j] and, for a
-  // follower, its term, dummy, last, commit and ring head.
-  int vs = 0, nj = 0, fterm = 0, fdummy = 0, flast = 0, fcommit = 0, fhead = 0;
-  if (go) {
-    const int32_t *src = j == 0 ? s.role : j == 1 ? s.term : j == 2 ? s.commit : j == 3 ? s.last
-                         : j == 4 ? s.dummy : j == 5 ? s.head : j == 6 ? s.srt : nullptr;
-    if (src) vs = src[ld];
-    if (j < P) nj = s.next[ld * P + j];
-    if (j < P && j != lp) {
-      fterm = s.term[f]; fdummy = s.dummy[f]; flast = s.last[f]; fcommit = s.commit[f]; fhead = s.head[f];
-    }
-  }
-  auto bc = [&](int v, int k) { return __shfl(v, gbase + k, 64); };
-  const int role = bc(vs, 0), T = bc(vs, 1), c0 = bc(vs, 2), last = bc(vs, 3), ldummy = bc(vs, 4),
-            lhead = bc(vs, 5), lsrt = bc(vs, 6);
+  const int role = bc(rrole, lp), T = bc(rterm, lp), c0 = bc(rcommit, lp), last = bc(rlast, lp),
+            ldummy = bc(rdummy, lp), lhead = bc(rhead, lp), lsrt = bc(rsrt, lp);
   if (go && (role != kLeader || c0 < ldummy)) {  // appendOneRound returns (:22-25) / MRAFT_ITEM_BAD_STATE
     if (j == 0) {
       if (gflags) gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
@@ -336,79 +343,87 @@ __global__ __launch_bounds__(64) void k_tick_lite(Dev s, const int32_t *__restri
     }
     go = false;
   }
-  const long long lrow = ld * L;
+  int nj = 0;
+#pragma unroll
+  for (int x = 0; x < P; ++x) if (x == lp) nj = nx[x];
+  const long long lrow = ((long long)g * P + lp) * L, f = r;
   const int lb = lhead - ldummy;
   const bool isf = go && j < P && j != lp;
+  const int fterm = rterm, fdummy = rdummy, flast = rlast, fcommit = rcommit, fhead = rhead;
   const int prev = nj - 1, n = last - prev;                              // :26, :50
-  // snapshot, panic, stale, below / beyond the follower's log: the full tick
-  bool fb = isf && (prev < ldummy || prev > last || T < fterm || prev < fdummy || prev > flast);
+  // decided by round trip 1: snapshot, panic, stale, below / beyond the
+  // follower's log, a merge that would compare (the follower holds entries
+  // past prev) or run past the ring's capacity -> the full tick
+  // IC_BELOW (prev below the follower's dummy, :123-127): Go returns before
+  // setting reply.Term, so with currentTerm > 0 the leader's gate (:73-74)
+  // drops the reply — the follower's own words only (role, term adoption,
+  // persist), settled here too
+  const bool bel = isf && prev >= ldummy && prev <= last && T >= fterm && prev < fdummy && T > 0;
+  bool fb = isf && !bel && (prev < ldummy || prev > last || T < fterm || prev < fdummy || prev > flast ||
+                            (n > 0 && (flast != prev || n > kLiteSpan || (long long)last - fdummy > (long long)L - 1)));
+  const bool mrg = isf && !fb && !bel && n > 0;
+  // successful replies: with at least P/2 of them the last evaluation of a1's
+  // order statistic is `last` (so top = min(M*, last) = last); with none, a1
+  // never runs; in between the full tick decides
+  const int nsucc = __popcll(__ballot(isf && !fb && !bel) >> gbase & 0xffull);
+  bool gfb = ((__ballot(fb) >> gbase) & 0xffull) != 0 || (nsucc > 0 && nsucc < P / 2);
+  // Round trip 2 (groups still settling here): prevLogTerm at leader and
+  // follower, a1's probe log[last] and each merging follower's first four
+  // entries to append (its own lane loads the leader's words).
+  const bool t2 = go && !gfb;
   int pt = 0, ft = 0, probe = 0;
-  if (isf && !fb) {
-    pt = s.log[lrow + ring(prev + lb, L)];                               // :49
-    ft = s.log[f * L + ring(prev - fdummy + fhead, L)];                  // :128
-  }
-  if (go && j == lp) probe = s.log[lrow + ring(last + lb, L)];           // a1's probe (:98)
-  // a conflict, a merge that compares (the follower holds entries past prev),
-  // or an append past the ring's capacity: the full tick
-  if (isf && !fb && (ft != pt || (n > 0 && (flast != prev || (long long)last - fdummy > (long long)L - 1))))
-    fb = true;
-  const bool mrg = isf && !fb && n > 0;
-  int mlo = mrg ? prev + 1 : INT32_MAX;  // the leader's first entry any follower needs
+  int e4[4] = {0, 0, 0, 0};
+  if (t2) {
+    if (isf && !bel) {
+      pt = s.log[lrow + ring(prev + lb, L)];                             // :49
+      ft = s.log[f * L + ring(prev - fdummy + fhead, L)];                // :128
+    }
+    if (mrg) {
 #pragma unroll
-  for (int o = 1; o < 8; o <<= 1) mlo = min(mlo, __shfl_xor(mlo, o, 64));
+      for (int u = 0; u < 4; ++u)
+        if (u < n) e4[u] = s.log[lrow + ring(prev + 1 + u + lb, L)];
+    }
+    if (j == lp) probe = s.log[lrow + ring(last + lb, L)];               // a1's probe (:98)
+  }
+  if (t2 && isf && !bel && ft != pt) fb = true;                          // a conflict: the full tick
   const int t = bc(probe, lp);
   int commit = c0;
-  bool gfb = ((__ballot(fb) >> gbase) & 0xffull) != 0;
-  if (go && !gfb) {
-    if (mlo != INT32_MAX && (long long)last - mlo + 1 > kLiteSpan) gfb = true;
-    if (last > c0) {                                                     // top = last (above)
-      if (t == T) commit = last;                                         // :98-100
-      else if (!(lsrt && t < T)) gfb = true;                             // a Figure-8 scan: the full tick
-    }
-  }
-  // the groups for the full tick, one atomic per wave
-  {
-    const bool push = go && gfb && j == 0;
-    const unsigned long long pm = __ballot(push);
-    if (pm) {
-      const int l0 = first_lane(pm);
-      unsigned base = 0;
-      if (lane == l0) base = atomicAdd(fb_count, (unsigned)__popcll(pm));
-      base = (unsigned)__shfl((int)base, l0, 64);
-      if (push) fb_list[base + (unsigned)__popcll(pm & ((1ull << lane) - 1))] = g;
-    }
+  gfb = gfb || ((__ballot(fb) >> gbase) & 0xffull) != 0;
+  if (go && !gfb && nsucc > 0 && last > c0) {                             // top = last (above)
+    if (t == T) commit = last;                                           // :98-100
+    else if (!(lsrt && t < T)) gfb = true;                               // a Figure-8 scan: the full tick
   }
   const bool w = go && !gfb;
-  // The appended entries: leader Indexes [mlo, last], lane j of the group takes
-  // mlo + j, mlo + j + 8, ..., stored into every merging follower whose prev
-  // lies below (:149-155; the compare ranges are empty).
-  {
-    int fp[P], fd[P], fh[P];
+  // the appended entries, Indexes prev + 1 .. last, by the follower's own lane
+  // (:149-155; the compare range is empty); past the first four, four at a time
+  if (w && mrg) {
+    const long long frow = f * L;
+    const int fb0 = prev + 1 - fdummy + fhead;  // ring position of Index prev + 1, before the wrap
 #pragma unroll
-    for (int q = 0; q < P; ++q) { fp[q] = bc(prev, q); fd[q] = bc(fdummy, q); fh[q] = bc(fhead, q); }
-    const unsigned mm = (unsigned)((__ballot(mrg) >> gbase) & 0xffull);
-    if (w && mm) {
-      for (int k = j; k <= last - mlo; k += 8) {  // (an Index loop could overflow near 2^31)
-        const int idx = mlo + k;
-        const int e = s.log[lrow + ring(idx + lb, L)];
+    for (int u = 0; u < 4; ++u)
+      if (u < n) s.log[frow + ring(fb0 + u, L)] = e4[u];
+    for (int c = 4; c < n; c += 4) {
+      int x[4];
 #pragma unroll
-        for (int q = 0; q < P; ++q)
-          if (((mm >> q) & 1) && idx > fp[q]) s.log[((long long)g * P + q) * L + ring(idx - fd[q] + fh[q], L)] = e;
-      }
+      for (int u = 0; u < 4; ++u) x[u] = c + u < n ? s.log[lrow + ring(prev + 1 + c + u + lb, L)] : 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (c + u < n) s.log[frow + ring(fb0 + c + u, L)] = x[u];
     }
   }
   bool fcadv = false;
   if (w && isf) {
-    mark_persist(s, f, MRAFT_PERSIST_STATE);                             // :111
+    if (s.pdirty) s.pdirty[f] = rpd | MRAFT_PERSIST_STATE;              // :111 (mark_persist)
     if (T > fterm) { s.term[f] = T; s.voted[f] = -1; }                   // :116-118
     s.role[f] = kFollower;                                               // :120
+  }
+  if (w && isf && !bel) {
     int newlast = flast;
     if (n > 0) {
       newlast = last;                                                    // prev + n
       s.last[f] = newlast;
       // terms_sorted after appending from prev + 1 (the tick's rule, mk = 0)
-      bool fl = lsrt != 0;
-      if (fl && prev == ldummy) fl = pt <= s.log[lrow + ring(prev + 1 + lb, L)];
+      const bool fl = lsrt != 0 && (prev != ldummy || pt <= e4[0]);  // e4[0]: the entry at prev + 1
       const int sw = !fl ? 0 : prev == fdummy ? 1 : -1;
       if (sw >= 0) s.srt[f] = sw;
     }
@@ -416,39 +431,64 @@ __global__ __launch_bounds__(64) void k_tick_lite(Dev s, const int32_t *__restri
       s.commit[f] = min(c0, newlast);
       fcadv = true;
     }
-    s.next[ld * P + j] = last + 1;                                       // :76-77
-    s.match[ld * P + j] = last;
+    s.next[((long long)g * P + lp) * P + j] = last + 1;                  // :76-77
+    s.match[((long long)g * P + lp) * P + j] = last;
   }
   const bool anyadv = ((__ballot(fcadv) >> gbase) & 0xffull) != 0;
   if (w && j == 0) {
-    if (commit != c0) s.commit[ld] = commit;
+    if (commit != c0) s.commit[(long long)g * P + lp] = commit;
     if (gflags)
       gflags[g] = MRAFT_G_ACTIVE | (commit != c0 ? MRAFT_G_COMMITTED : 0) | (anyadv ? MRAFT_G_FOLLOWER_COMMIT : 0);
     ex.put(g, commit, T, kLeader);
   }
+  // The groups for the full tick: one LDS count per wave, one global atomic
+  // per workgroup on its XCD's counter (one device-wide counter hit by every
+  // wave serialised the launch: 72 us for 65,536 groups, profiles/r6_l4), the
+  // list entries in the XCD's region of cap groups.
+  const bool push = go && gfb && j == 0;
+  const unsigned long long pmask = __ballot(push);
+  unsigned woff = 0;
+  if (pmask && lane == first_lane(pmask)) woff = atomicAdd(&sh_cnt, (unsigned)__popcll(pmask));
+  woff = (unsigned)__shfl((int)woff, pmask ? first_lane(pmask) : 0, 64);
+  __syncthreads();
+  if (threadIdx.x == 0) sh_base = sh_cnt ? atomicAdd(&fb_count[xcd * 32], sh_cnt) : 0u;
+  __syncthreads();
+  if (push) fb_list[(long long)xcd * cap + sh_base + woff + (unsigned)__popcll(pmask & ((1ull << lane) - 1))] = g;
 }
 
-// The light tick's fallback: the groups k_tick_lite listed, each through the
-// full tick (one wave per group, grid-stride over the device count, so any
-// grid is exact; the host sizes it from the previous tick's count). The first
-// workgroup zeroes the counter the next light tick uses and publishes this
+// The light tick's fallback: the groups k_tick_lite listed (eight XCD lists
+// of cap entries, their counts 32 words apart), each through the full tick
+// (one wave per group, grid-stride over the device counts, so any grid is
+// exact; the host sizes it from the previous tick's count). The first
+// workgroup zeroes the counters the next light tick uses and publishes this
 // tick's count to the host's pinned word.
 template <int P>
 __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_list(Dev s, const int32_t *__restrict__ leader_peer,
                                                    int32_t *__restrict__ gflags,
                                                    unsigned long long *__restrict__ counts, Export ex,
                                                    const int32_t *__restrict__ list, const unsigned *__restrict__ cnt,
-                                                   unsigned *__restrict__ cnt_next, long long *__restrict__ hint) {
+                                                   unsigned *__restrict__ cnt_next, long long *__restrict__ hint,
+                                                   int cap) {
   constexpr bool COUNT = false;
   constexpr int NI = P - 1;
   const int lane = lane_id();
-  const unsigned nl = (unsigned)uni((int)*cnt);
-  if (blockIdx.x == 0 && lane == 0) {
-    *cnt_next = 0;
-    if (hint) *hint = (long long)nl;
+  unsigned c8[8], nl = 0;
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    c8[x] = (unsigned)uni((int)cnt[x * 32]);
+    nl += c8[x];
+  }
+  if (blockIdx.x == 0) {
+    if (lane < 8) cnt_next[lane * 32] = 0;
+    if (lane == 0 && hint) __hip_atomic_store(hint, (long long)nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   for (unsigned k = blockIdx.x; k < nl; k += gridDim.x) {
-    const int g = uni(list[k]);
+    unsigned base = 0;
+    int x = 0;
+#pragma unroll
+    for (int y = 0; y < 7; ++y)
+      if (x == y && k >= base + c8[y]) { base += c8[y]; x = y + 1; }
+    const int g = uni(list[(long long)x * cap + (k - base)]);
 #define TICK_EXIT continue
 #include "mraft_tick_body.inc"
 #undef TICK_EXIT
@@ -458,11 +498,11 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_list(Dev s, const 
 template <int P>
 void launch_tick_light_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, Export ex, const LiteBufs &lb,
                          hipStream_t st) {
-  hipLaunchKernelGGL(k_tick_lite<P>, dim3((unsigned)((s.G + 7) / 8)), dim3(64), 0, st, s, lpeer, gflags, ex, lb.list,
-                     lb.cnt);
+  hipLaunchKernelGGL(k_tick_lite<P>, dim3((unsigned)lite_blocks(s.G)), dim3(64 * kLiteWaves), 0, st, s, lpeer, gflags,
+                     ex, lb.list, lb.cnt, lite_cap(s.G));
   hipLaunchKernelGGL(k_tick_list<P>, dim3((unsigned)lb.grid), dim3(64), 0, st, s, lpeer, gflags,
                      (unsigned long long *)nullptr, ex, (const int32_t *)lb.list, (const unsigned *)lb.cnt,
-                     lb.cnt_next, lb.hint);
+                     lb.cnt_next, lb.hint, lite_cap(s.G));
 }
 
 template <int P, bool COUNT>

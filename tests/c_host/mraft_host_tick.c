@@ -7,7 +7,7 @@
  * tests/golden/make_golden.py from tick_vectors.npz: inputs from the seeded
  * generator, expected outputs from the pure-Python restatement of
  * src/raft/raft_append_entry.go:20-162) it runs one replication round of the
- * reference three ways through the boundary, each on a fresh engine
+ * reference four ways through the boundary, each on a fresh engine
  * (mraft_create = Make, src/raft/raft.go:51-87; mraft_load_state =
  * readPersist, raft.go:217-235; mraft_destroy = Kill, src/raft/utility.go:9-19):
  *
@@ -21,7 +21,10 @@
  *             leader (processAppendEntriesReply + advanceCommitIndexForLeader,
  *             :66-105) -> mraft_export_group_status (GetState);
  *   by value  the same with the entries copied into a caller buffer, as a
- *             host that received the args over the network holds them.
+ *             host that received the args over the network holds them;
+ *   light     the tick again with mraft_set_tick_mode(MRAFT_TICK_LIGHT): the
+ *             steady-state groups settled eight per wave, the rest through
+ *             the full tick (ABI 6).
  *
  * Each path is compared with the same fixture: the group flags (on the message
  * paths rebuilt from the gather errors, the per-item fold flags and the
@@ -56,8 +59,8 @@ typedef struct {
   int32_t *in[N_ARR], *want[N_ARR];
 } vec_t;
 
-enum { PATH_TICK, PATH_MESSAGES, PATH_BY_VALUE };
-static const char *const k_path[3] = {"tick", "messages", "by value"};
+enum { PATH_TICK, PATH_MESSAGES, PATH_BY_VALUE, PATH_LIGHT };
+static const char *const k_path[4] = {"tick", "messages", "by value", "light tick"};
 
 static int64_t arr_len(int i, int64_t gp, int64_t P, int64_t L) {
   return i == A_LOG ? gp * L : (i == 9 || i == 10) ? gp * P : gp;
@@ -204,7 +207,7 @@ static int check_engine(const vec_t *t, int v, int path, mraft_engine *h, const 
   return 0;
 }
 
-static int run_tick(const vec_t *t, int v, int device) {
+static int run_tick(const vec_t *t, int v, int device, int light) {
   const int32_t G = t->G;
   int32_t *flags = (int32_t *)zalloc(G, sizeof(int32_t)), *commit = (int32_t *)zalloc(G, sizeof(int32_t)),
           *tl = (int32_t *)zalloc(G, sizeof(int32_t));
@@ -218,8 +221,20 @@ static int run_tick(const vec_t *t, int v, int device) {
     fprintf(stderr, "vector %d: mraft_get_tick_shards = %d, want %d\n", v, mraft_get_tick_shards(h), shards);
     return 2;
   }
+  if (light) {
+    ABI(mraft_set_tick_mode(h, MRAFT_TICK_LIGHT));
+    if (mraft_get_tick_mode(h) != MRAFT_TICK_LIGHT || mraft_tick_light_fallbacks(h) != -1) {
+      fprintf(stderr, "vector %d: tick mode %d, fallbacks %lld before the first light tick\n", v,
+              mraft_get_tick_mode(h), (long long)mraft_tick_light_fallbacks(h));
+      return 2;
+    }
+  }
   ABI(mraft_replicate_tick_export(h, t->lp, flags, commit, tl, MRAFT_HOST));
-  rc = check_engine(t, v, PATH_TICK, h, flags, commit, tl);
+  if (light && mraft_tick_light_fallbacks(h) < 0) {
+    fprintf(stderr, "vector %d: no fallback count after a light tick\n", v);
+    return 2;
+  }
+  rc = check_engine(t, v, light ? PATH_LIGHT : PATH_TICK, h, flags, commit, tl);
   free(flags);
   free(commit);
   free(tl);
@@ -330,13 +345,14 @@ static int run_vector(FILE *f, int v, int device) {
   vec_t t;
   memset(&t, 0, sizeof t);
   int rc = read_vector(f, &t);
-  if (!rc) rc = run_tick(&t, v, device);
+  if (!rc) rc = run_tick(&t, v, device, 0);
+  if (!rc) rc = run_tick(&t, v, device, 1);
   if (!rc) rc = run_messages(&t, v, device, 0);
   if (!rc) rc = run_messages(&t, v, device, 1);
   if (!rc) {
     int committed = 0;
     for (int32_t g = 0; g < t.G; ++g) committed += (t.want_flags[g] & MRAFT_G_COMMITTED) != 0;
-    printf("vector %d: %d x %d x %d: tick (2 shards), messages and by value: flags, GetState words and "
+    printf("vector %d: %d x %d x %d: tick and light tick (2 shards), messages and by value: flags, GetState words and "
            "state bit-exact (%d groups committed)\n",
            v, (int)t.G, (int)t.P, (int)t.L, committed);
   }

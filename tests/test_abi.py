@@ -99,9 +99,11 @@ def test_message_calls_reject_bad_arguments_gpu():
         assert b"n_entry_terms" in lib.mraft_last_error_string()
         assert lib.mraft_process_append_replies(h, ptr(res), 2, ptr(seg), -1, ptr(fl), ptr(err), HOST) == _abi.E_INVAL
         assert lib.mraft_process_append_replies(h, ptr(res), -2, None, 0, ptr(fl), ptr(err), HOST) == _abi.E_INVAL
-        assert lib.mraft_set_stage_capacity(h, -1) == _abi.E_INVAL
+        assert lib.mraft_set_stage_capacity(h, -2) == _abi.E_INVAL
         assert lib.mraft_set_stage_capacity(h, 1 << 31) == _abi.E_INVAL
         assert lib.mraft_get_stage_capacity(h) == 4 << 20  # unchanged default
+        assert lib.mraft_set_stage_capacity(h, -1) == 0  # MRAFT_STAGE_AUTO (the default mode)
+        assert lib.mraft_get_stage_capacity(h) == 4 << 20
         gf = e.replicate_tick(lp)
         o = Oracle(G, P, L, st)
         assert np.array_equal(gf, o.replicate_tick(lp))

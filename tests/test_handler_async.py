@@ -208,7 +208,7 @@ def _self_reference(st, lp, G, P, L, rng):
 CASES = ["stale_leader", "ring2", "ring3", "self"]
 
 
-@pytest.mark.parametrize("cap", ["default", "small", "zero"])
+@pytest.mark.parametrize("cap", ["default", "small", "zero", "auto"])
 @pytest.mark.parametrize("case", CASES)
 def test_deferred_items_gpu(case, cap):
     G, P, L = 256, 5, 128
@@ -224,11 +224,13 @@ def test_deferred_items_gpu(case, cap):
     o = Oracle(G, P, L, st)
     with Engine(G, P, L) as e:
         e.load_state(st)
-        if cap == "small":
+        if cap in ("small", "auto"):
             e.set_stage_capacity(64)
         elif cap == "zero":
             e.set_stage_capacity(0)
-        assert e.stage_capacity() == {"default": 1 << 22, "small": 64, "zero": 0}[cap]
+        if cap == "auto":  # MRAFT_STAGE_AUTO from 64 words: the first call's need grows it for the second
+            e.set_stage_capacity(-1)
+        assert e.stage_capacity() == {"default": 1 << 22, "small": 64, "zero": 0, "auto": 64}[cap]
         args, gerr = e.gather_append_args(slots, peers)
         oargs, ogerr = o.gather_append_args(slots, peers)
         assert np.array_equal(args, oargs) and np.array_equal(gerr, ogerr)
@@ -254,6 +256,8 @@ def test_deferred_items_gpu(case, cap):
         orep2, oherr2 = o.handle_append_entries(oargs2[ogerr2 == 0], None)
         assert np.array_equal(herr2, oherr2) and np.array_equal(rep2, orep2)
         assert_states_equal(e.store_state(), o.state(), G, P, L, f"{case}, stage {cap}, second call")
+        if cap == "auto" and case.startswith("ring"):
+            assert e.stage_capacity() >= 1 << 20, e.stage_capacity()  # grown (1 Mi-word steps)
 
 
 @pytest.mark.parametrize("fold", ["append", "vote", "install"])

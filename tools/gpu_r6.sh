@@ -53,8 +53,27 @@ for st in ${DO:-tests bench}; do
     lighttests)
       # the whole tick-related GPU suite with every engine in MRAFT_TICK_LIGHT (tests/conftest.py)
       echo "== lighttests"
-      MRAFT_TEST_TICK_MODE=light timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${LTESTS:-tick or persist or ring or odd or index or snapshot or sim or multirank}" > "$OUT/pytest_light.log" 2>&1
+      MRAFT_TEST_TICK_MODE=light timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${LTESTS:-(tick or persist or ring or odd or index or snapshot or sim or multirank) and not mode_calls}" > "$OUT/pytest_light.log" 2>&1
       rc=$?; tail -3 "$OUT/pytest_light.log"; [ $rc -eq 0 ] || { grep -E "FAIL|Error" "$OUT/pytest_light.log" | head -20; exit 1; } ;;
+    ktrace)
+      # kernel trace + stats of a tool (KT_CMD, e.g. tools/bench_steady.py) -> $OUT/kt_<name>, per-kernel summary
+      name=$(basename "${KT_CMD%% *}" .py)
+      echo "== ktrace $KT_CMD"
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_$name" -o kt -- python3 $KT_CMD \
+        > "$OUT/kt_$name.json" 2> "$OUT/kt_$name.err" || { tail -5 "$OUT/kt_$name.err"; exit 1; }
+      f=$(find "$OUT/kt_$name" -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && head -25 "$f" | cut -d, -f1-8 ;;
+    pmcsteady)
+      # counters of the steady-state ticks (tools/bench_steady.py), one pass per group -> $OUT/steady_counters.json
+      echo "== pmcsteady"
+      i=0
+      for grp in "FETCH_SIZE" "WRITE_SIZE" \
+                 "SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU" \
+                 "TCC_HIT TCC_MISS TCC_EA0_RDREQ TCC_EA0_WRREQ TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pst$i" -o p -- python3 tools/bench_steady.py \
+          > "$OUT/pst$i.json" 2> "$OUT/pst$i.err" || { tail -5 "$OUT/pst$i.err"; exit 1; }
+      done
+      python3 tools/pmc_kernels.py "$OUT/steady_counters.json" "$OUT"/pst[0-9]* --kernels "k_tick_lite<5>;k_tick_list<5>;k_tick_group<5, false>" | head -60 ;;
     abmsg)
       # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
       echo "== abmsg ${VARIANTS:-prebuilt}"
