@@ -486,8 +486,12 @@ void *mraft_shard_stream(mraft_engine *h, int32_t shard);
  * pair of launches); mraft_replicate_tick_count always counts the full tick.
  * The second launch's grid follows the previous light tick's count (a pinned
  * word the device writes): a jump from few to many non-settling groups costs
- * one slow tick, never a wrong one. */
-enum { MRAFT_TICK_FULL = 0, MRAFT_TICK_LIGHT = 1 };
+ * one slow tick, never a wrong one. MRAFT_TICK_AUTO: per shard, the light
+ * tick while the last completed light tick sent at most a quarter of the
+ * groups to the full tick (or before any has completed), otherwise the full
+ * tick with a light tick every 32nd to measure again (the counts reach the
+ * host asynchronously: a choice may follow a count a few ticks old). */
+enum { MRAFT_TICK_FULL = 0, MRAFT_TICK_LIGHT = 1, MRAFT_TICK_AUTO = 2 };
 int mraft_set_tick_mode(mraft_engine *h, int32_t mode);
 int32_t mraft_get_tick_mode(const mraft_engine *h);  /* -1: null handle */
 /* Groups the most recent completed MRAFT_TICK_LIGHT tick sent to the full

@@ -10,11 +10,11 @@ ABI in include/mraft.h); this package is its host-side mirror:
   * `router`         — the shard router's view of the all-gathered GetState
     words (one RCCL all-gather per tick on multi-GPU).
 """
-from ._abi import (CANDIDATE, DEVICE, FOLLOWER, HOST, LEADER, TICK_FULL, TICK_LIGHT, synth_seed)  # noqa: F401
+from ._abi import (CANDIDATE, DEVICE, FOLLOWER, HOST, LEADER, TICK_AUTO, TICK_FULL, TICK_LIGHT, synth_seed)  # noqa: F401
 from .engine import (Engine, MraftError, copy_state, decode_persistent, entry_positions,  # noqa: F401
                      encode_persistent, new_state, state_sizes, synth_election_state,
                      synth_fold_batch, synth_tick_state)
 
 __all__ = ["Engine", "MraftError", "new_state", "copy_state", "state_sizes", "synth_tick_state",
            "synth_fold_batch", "synth_election_state", "encode_persistent", "decode_persistent", "synth_seed", "LEADER", "CANDIDATE", "FOLLOWER", "HOST", "DEVICE",
-           "TICK_FULL", "TICK_LIGHT"]
+           "TICK_FULL", "TICK_LIGHT", "TICK_AUTO"]

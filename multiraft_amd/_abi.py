@@ -18,7 +18,7 @@ SYNTH_PATH = os.path.join(_HERE, "libmraft_synth.so")
 # ---- constants (include/mraft.h) -------------------------------------------
 LEADER, CANDIDATE, FOLLOWER = 1, 2, 3
 HOST, DEVICE = 0, 1
-TICK_FULL, TICK_LIGHT = 0, 1  # mraft_set_tick_mode
+TICK_FULL, TICK_LIGHT, TICK_AUTO = 0, 1, 2  # mraft_set_tick_mode
 CREATE_NO_ALLOC = 1
 CREATE_DEDICATED_QUEUE = 2
 OK, E_INVAL, E_NOMEM, E_HIP, E_NOSTATE = 0, -1, -2, -3, -4

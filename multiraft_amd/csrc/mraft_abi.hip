@@ -35,6 +35,7 @@ constexpr int kDeferGridMax = 1 << 16;
 // grid-stride loop makes any grid exact; an empty one costs a few µs).
 constexpr long long kLiteGridMin = 2048;
 constexpr long long kLiteGridUnknown = 8192;
+constexpr int kAutoProbe = 32;  // MRAFT_TICK_AUTO: a light tick at least every 32 ticks
 // The engine's pinned host words (device-written, read by the host when it
 // enqueues): [0] the last by-reference AppendEntries call's deferred count,
 // [1] the staged words of the last call that exceeded the stage (its need),
@@ -82,6 +83,7 @@ struct mraft_engine {
   int32_t *lite_list = nullptr;
   unsigned *lite_cnt = nullptr;
   int lite_par[kMaxShards] = {};
+  int auto_since[kMaxShards] = {};  // MRAFT_TICK_AUTO: full ticks since the last light one
   std::vector<void *> scratch_ptr;
   std::vector<size_t> scratch_cap;
 };
@@ -256,9 +258,28 @@ int ensure_lite(mraft_engine *h) {
 
 // One tick launch over groups [g0, g0 + d.G) as shard s on stream st: the full
 // tick, or the light tick's pair of launches.
+// MRAFT_TICK_AUTO's choice for shard s of G_s groups: the light tick while
+// the last completed light tick sent at most a quarter of the groups to the
+// full tick (or none has completed yet); otherwise the full tick, with a
+// light tick every kAutoProbe-th tick to measure again.
+bool auto_light(mraft_engine *h, int s, int32_t gs) {
+  const long long last = ((volatile long long *)h->dhint)[kHintLite + s];
+  if (last < 0 || 4 * last <= (long long)gs) {
+    h->auto_since[s] = 0;
+    return true;
+  }
+  if (++h->auto_since[s] >= kAutoProbe) {
+    h->auto_since[s] = 0;
+    return true;
+  }
+  return false;
+}
+
 void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const int32_t *lp, int32_t *gf,
                 int32_t *ec, int32_t *et, hipStream_t st) {
-  if (h->tick_mode != MRAFT_TICK_LIGHT || h->P < 2) {
+  const bool light = h->P >= 2 && (h->tick_mode == MRAFT_TICK_LIGHT ||
+                                   (h->tick_mode == MRAFT_TICK_AUTO && auto_light(h, s, d.G)));
+  if (!light) {
     mraft::launch_replicate_tick(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), st);
     return;
   }
@@ -278,7 +299,7 @@ void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const i
 }
 
 int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, int32_t *et) {
-  if (h->tick_mode == MRAFT_TICK_LIGHT) TRY(ensure_lite(h));
+  if (h->tick_mode != MRAFT_TICK_FULL) TRY(ensure_lite(h));
   if (h->nshards <= 1) {
     tick_range(h, dev_of(h), 0, 0, lp, gf, ec, et, h->stream);
     HIP_TRY(hipGetLastError());
@@ -837,10 +858,8 @@ int mraft_start(mraft_engine *h, const int32_t *slots, const int32_t *counts, in
   TRY(sg.map(out_term, sizeof(int32_t) * n, false, true, &ot));
   TRY(sg.map(out_is_leader, sizeof(int32_t) * n, false, true, &ol));
   TRY(sg.map(item_err, sizeof(int32_t) * n, false, true, &e));
-  mraft::launch_claim(s, n, sizeof(int32_t), 0, nullptr, gp_of(h), h->P, h->claim, h->epoch,
-                      (int32_t *)e, h->stream);
   mraft::launch_start(dev_of(h), (const int32_t *)s, (const int32_t *)c, n, (int32_t *)oi,
-                      (int32_t *)ot, (int32_t *)ol, (int32_t *)e, h->stream);
+                      (int32_t *)ot, (int32_t *)ol, (int32_t *)e, h->claim, h->epoch, h->stream);
   return sg.finish();
 }
 
@@ -1323,7 +1342,8 @@ int32_t mraft_get_tick_shards(const mraft_engine *h) { return h ? h->nshards : 0
 
 int mraft_set_tick_mode(mraft_engine *h, int32_t mode) {
   if (!h) return fail(MRAFT_E_INVAL, "null engine handle");
-  if (mode != MRAFT_TICK_FULL && mode != MRAFT_TICK_LIGHT) return fail(MRAFT_E_INVAL, "tick mode %d", mode);
+  if (mode != MRAFT_TICK_FULL && mode != MRAFT_TICK_LIGHT && mode != MRAFT_TICK_AUTO)
+    return fail(MRAFT_E_INVAL, "tick mode %d", mode);
   h->tick_mode = mode;
   return MRAFT_OK;
 }

@@ -76,8 +76,10 @@ void launch_fold(const Dev &s, const mraft_ae_result *items, int64_t n, const in
                  int64_t n_seg, int64_t gp, unsigned long long *claim, uint32_t epoch, int32_t *seg_err,
                  int32_t *flags, int32_t *item_err, void *scan_buf, hipStream_t st);
 size_t fold_scan_bytes(int64_t n, int64_t n_seg);  // scratch launch_fold needs (a1 scan list, long segments)
+// Start: the slot claims (k_claim) and k_start, which checks them itself.
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
-                  int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st);
+                  int32_t *ot, int32_t *ol, int32_t *err, const unsigned long long *claim, uint32_t epoch,
+                  hipStream_t st);
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,
                           hipStream_t st);
 void launch_collect_apply_compact(const Dev &s, int32_t *scratch_bcnt, int64_t cap, int32_t *oslot,

@@ -1522,15 +1522,20 @@ __global__ __launch_bounds__(64, 8) void k_fold_tail(Dev s, const mraft_ae_resul
 }
 
 // ---------------------------------------------------------------- Start
+// The duplicate-slot check (k_claim_check's) is done here, on the claim word
+// k_claim left: one launch fewer per Start call.
 __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t *__restrict__ counts,
                         int64_t n, int32_t *__restrict__ oi, int32_t *__restrict__ ot,
-                        int32_t *__restrict__ ol, int32_t *__restrict__ err) {
+                        int32_t *__restrict__ ol, int32_t *__restrict__ err,
+                        const unsigned long long *__restrict__ claim, uint32_t epoch) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   int idx = -1, term = -1, isl = 0;
   if (!err[i]) {
     const int sl = slots[i], k = counts ? counts[i] : 1;
-    if (k < 1) {
+    if (claim[sl] != (((unsigned long long)epoch << 32) | (0xFFFFFFFFull - (uint64_t)i))) {
+      err[i] = MRAFT_ITEM_DUP_SLOT;
+    } else if (k < 1) {
       err[i] = MRAFT_ITEM_BAD_SLOT;
     } else if (s.role[sl] == kLeader) {                                // raft.go:93-95
       const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl], h = s.head[sl];
@@ -2123,10 +2128,14 @@ size_t fold_scan_bytes(int64_t n, int64_t n_seg) {
 }
 
 void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int64_t n, int32_t *oi,
-                  int32_t *ot, int32_t *ol, int32_t *err, hipStream_t st) {
+                  int32_t *ot, int32_t *ol, int32_t *err, const unsigned long long *claim, uint32_t epoch,
+                  hipStream_t st) {
   if (n <= 0) return;
+  hipLaunchKernelGGL(k_claim, dim3(blocks_for(n)), dim3(kBlock), 0, st, (const char *)slots, n, (int)sizeof(int32_t),
+                     0, (const int64_t *)nullptr, (int64_t)s.G * s.P, s.P, const_cast<unsigned long long *>(claim),
+                     epoch, err);
   hipLaunchKernelGGL(k_start, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, counts, n, oi, ot,
-                     ol, err);
+                     ol, err, claim, epoch);
 }
 
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,

@@ -22,7 +22,7 @@ from message_cases import shift_indices, top_offset
 from oracle_lib import Oracle, assert_states_equal, rotate_rings
 from random_states import random_tick_state
 
-from multiraft_amd import TICK_FULL, TICK_LIGHT, Engine, MraftError, synth_tick_state
+from multiraft_amd import TICK_AUTO, TICK_FULL, TICK_LIGHT, Engine, MraftError, synth_tick_state
 
 pytestmark = pytest.mark.gpu
 
@@ -164,7 +164,7 @@ def test_light_mode_calls_and_p1_gpu():
         e.load_state(st)
         assert e.tick_mode() == TICK_FULL
         with pytest.raises(MraftError):
-            e.set_tick_mode(2)
+            e.set_tick_mode(3)
         e.set_tick_mode(TICK_LIGHT)
         e.set_tick_shards(2)
         assert e.tick_mode() == TICK_LIGHT
@@ -172,3 +172,26 @@ def test_light_mode_calls_and_p1_gpu():
             _step(e, o, lp, G, P, L, f"P=1 step {k}", bool(k))
         e.set_tick_mode(TICK_FULL)
         _step(e, o, lp, G, P, L, "P=1 full", False)
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_auto_mode_gpu(shards):
+    """MRAFT_TICK_AUTO: a heavy first tick (every group of the seeded state
+    falls back) turns the engine to the full tick, a light tick every 32nd
+    re-measures, and the steady state brings the light tick back — the oracle
+    equal after every one of 40 ticks with Start() between them."""
+    G, P, L = 512, 5, 256
+    rng = np.random.default_rng(31 + shards)
+    st, lp, _ = synth_tick_state(G, P, L, seed=2024 + shards)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        e.set_tick_shards(shards)
+        e.set_tick_mode(TICK_AUTO)
+        assert e.tick_mode() == TICK_AUTO
+        seen = set()
+        for k in range(40):
+            _step(e, o, lp, G, P, L, f"auto step {k}", bool(k % 3 == 0))
+            seen.add(e.tick_light_fallbacks())
+            _start_all(e, o, lp, G, P, rng, 2)
+        assert len(seen) > 1 and min(seen) >= 0, seen  # light ticks ran and were counted again
