@@ -408,11 +408,14 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args,
 
 /* Capacity, in entry words, of the device stage mraft_handle_append_entries
  * copies the entries of deferred by-reference items into (allocated on first
- * use). A batch needing more is still handled exactly, in the ordered
- * fallback (as is every batch when the stage cannot be allocated).
+ * use), in eight equal stripes that the batch's deferred items fill by the
+ * XCD their set ran on. A batch whose stripe needs more is still handled
+ * exactly, in the ordered fallback (as is every batch when the stage cannot
+ * be allocated).
  * words in [0, 2^31): that fixed capacity. MRAFT_STAGE_AUTO (the default,
  * from 4 Mi words = 16 MiB; ABI 6): after a batch that needed more, the calls
- * after it get a stage of 5/4 of that need (stream-ordered growth, the device
+ * after it get a stage of 5/4 of that need — eight times its fullest
+ * stripe's words — (stream-ordered growth, the device
  * publishes the need to a pinned word: no host wait), up to 2^31 - 1 words;
  * growth stops at the first allocation that fails. Returns MRAFT_OK;
  * mraft_get_stage_capacity returns the current capacity (-1: null handle). */

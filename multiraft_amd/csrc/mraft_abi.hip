@@ -70,7 +70,7 @@ struct mraft_engine {
   unsigned long long *claim = nullptr;
   uint32_t *srcmark = nullptr;             // per slot: epoch of the last call that read its row
   uint32_t epoch = 0;
-  unsigned long long *ae_total = nullptr;  // AppendEntries by reference: staged words, deferred items << 32
+  unsigned long long *ae_total = nullptr;  // AppendEntries by reference: the deferred launch's counters (mraft_kernels.hip)
   int64_t stage_cap = kDefaultStageWords;  // words of staged entries the deferred launch may use
   bool stage_auto = true;                  // MRAFT_STAGE_AUTO: grow stage_cap to the last overflow's need
   long long *dhint = nullptr;  // pinned host word: the last by-reference call's deferred count (device-written)
@@ -747,14 +747,14 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   // "a4" for the rules).
   if (!h->ae_total) {
     void *t = nullptr;
-    TRY(alloc_async(h, &t, 4 * sizeof(unsigned long long), "AppendEntries counters"));
+    TRY(alloc_async(h, &t, mraft::kAeTotalWords * sizeof(unsigned long long), "AppendEntries counters"));
     h->ae_total = (unsigned long long *)t;
-    HIP_TRY(hipMemsetAsync(h->ae_total, 0, 4 * sizeof(unsigned long long), h->stream));
+    HIP_TRY(hipMemsetAsync(h->ae_total, 0, mraft::kAeTotalWords * sizeof(unsigned long long), h->stream));
   }
   void *sethd, *soff, *defer, *order, *stage = nullptr;
   TRY(scratch(h, 14, sizeof(int64_t) * (size_t)n, &soff));
   TRY(scratch(h, 15, (size_t)n, &sethd));
-  TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n, &defer));
+  TRY(scratch(h, 18, sizeof(int64_t) * (size_t)n * mraft::kAeStripes, &defer));  // a list of n per stripe
   // the deferred launch's grid: the last call's deferred count (a pinned word
   // the device writes; a stale value only changes the grid, never a result)
   const long long last_nd = *(volatile long long *)h->dhint;

@@ -16,7 +16,9 @@
 // wave-round), fewer instructions per candidate alone changed nothing, and
 // taking the per-candidate LDS round trip out of the delivery loop's
 // dependent chain (candidates ranked once per round, held in registers) took
-// the storm 9 % down.
+// the storm 9 % down; the loop's conditions as bitwise ops (no exec-mask
+// region per candidate: 126 -> 77 SALU per round body) 1.5 % more
+// (profiles/r6_d1).
 #include "mraft_device.h"
 #include "mraft_internal.h"
 
@@ -121,13 +123,15 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
         const bool valid = k < ncand;
         const int c = (int)((rcs >> (8 * k)) & 0xffull);
         const int cat = rt[k];
-        pmx = (valid && c <= p) ? max(pmx, cat) : pmx;
-        const bool h = act && valid && c != p;                         // this voter handles c's RV
-        const bool gt = h && cat > term;                               // :63-66
-        const bool ge = h && cat >= term;                              // :59-62 (stale: no change)
+        // conditions as bitwise (non-short-circuit) ops: no exec-mask region per
+        // candidate (round 6: 126 -> 77 SALU per round body, storm -1.5 %)
+        pmx = (valid & (c <= p)) ? max(pmx, cat) : pmx;
+        const bool h = act & valid & (c != p);                         // this voter handles c's RV
+        const bool gt = h & (cat > term);                              // :63-66
+        const bool ge = h & (cat >= term);                             // :59-62 (stale: no change)
         term = gt ? cat : term;
         voted = gt ? -1 : voted;
-        const bool grant = ge && (voted == -1 || voted == c) && ((upm >> c) & 1);  // :69-74
+        const bool grant = ge & ((voted == -1) | (voted == c)) & (((upm >> c) & 1) != 0);  // :69-74
         voted = grant ? c : voted;
         gm |= grant ? (1 << c) : 0;
       }

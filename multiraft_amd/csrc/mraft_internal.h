@@ -51,6 +51,14 @@ void launch_gather_args(const Dev &s, const int32_t *slots, const int32_t *peers
 void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L, int64_t gp, int ni,
                      unsigned long long *claim, uint32_t *srcmark, uint32_t epoch, int32_t *err, uint8_t *sethd,
                      unsigned long long *total, hipStream_t st);
+// The by-reference handler's counter buffer (u64 words: [2] the published
+// deferred count, [3] the fallback's finished workgroups, then per stripe —
+// the main launch workgroup's XCD — its deferred items and its staged words,
+// one 128-B line each) and its stripes: stripe x lists its deferred items at
+// defer[x * n] (the list buffer holds kAeStripes * n) and stages at
+// stage[x * capacity / kAeStripes].
+constexpr int kAeStripes = 8;
+constexpr int kAeTotalWords = 16 + 2 * kAeStripes * 16;
 // The deferred launch's buffers and grid (mraft_kernels.hip "deferred
 // launch's fallback"): per item a 16-B record (writer, arrivals, run flag,
 // cycle counter) and a reader count, nslot cycle buffers of L words, the last

@@ -11,6 +11,17 @@ namespace mraft {
 namespace {
 
 constexpr int kBlock = 256;
+// The main launch's deferred list and stage offsets are counted per stripe
+// (the workgroup's XCD, blockIdx % 8), each counter on its own 128-B line of
+// the counter buffer (mraft_abi.hip ae_total, kAeTotalWords u64): one
+// same-address counter took an atomic round trip per deferred item and per
+// staged item, serialised — 1.3 ms of a 2-cycle-heavy batch (r6_l7). Stripe x
+// lists its items at defer[x * n ...] and stages at stage[x * cap / 8 ...].
+constexpr int kStripes = kAeStripes;
+static_assert(16 + 2 * kStripes * 16 == kAeTotalWords, "the counter buffer's layout (mraft_internal.h)");
+constexpr int kStripeWords = 16;                            // 128 B
+constexpr int kStripeDef = 16;                              // total[16 + 16 x]: deferred items of stripe x
+constexpr int kStripeStg = kStripeDef + kStripes * kStripeWords;  // total[144 + 16 x]: its staged words
 #ifndef MRAFT_MSG_BLOCK
 #define MRAFT_MSG_BLOCK 64  // workgroup size of the message path's lane-per-item kernels (gather, claims; r4_v26: 64 pipelines -3 %)
 #endif
@@ -232,9 +243,10 @@ __device__ __forceinline__ bool same_key(const AeKey &x, const AeKey &y) {
 // the slot check and the claim (atomicMax: the lowest item wins), srcmark of
 // the row it reads, and sethd[i] = the size of the set item i heads, else 0
 // (keys of the neighbours within kAeHalo from LDS, the halo loaded by the
-// wave's edge lanes). Its first thread also arms the counters the main launch
-// adds into (total[0]: staged words, total[1]: deferred items << 32); the
-// previous call's deferred launch has read them (stream order).
+// wave's edge lanes). Its first threads also arm the counters the main launch
+// adds into (per stripe: deferred items and staged words, kStripeDef /
+// kStripeStg); the previous call's deferred launch has read them (stream
+// order).
 constexpr int kAeHalo = 7;
 
 __global__ __launch_bounds__(64) void k_claim_ae(const mraft_ae_args *__restrict__ args, int64_t n, int64_t n_log,
@@ -246,10 +258,10 @@ __global__ __launch_bounds__(64) void k_claim_ae(const mraft_ae_args *__restrict
   __shared__ int kb[64 + 2 * kAeHalo], ke[64 + 2 * kAeHalo];
   const int t = (int)threadIdx.x;
   const int64_t i = blockIdx.x * (int64_t)64 + t;
-  if (i == 0) {
-    total[0] = 0;  // staged words
-    total[1] = 0;  // deferred items << 32
-    total[3] = 0;  // workgroups of the deferred launch's fallback done (total[2]: the published count)
+  if (i == 0) total[3] = 0;  // workgroups of the deferred launch's fallback done (total[2]: the published count)
+  if (i < kStripes) {
+    total[kStripeDef + kStripeWords * i] = 0;  // deferred items of stripe i
+    total[kStripeStg + kStripeWords * i] = 0;  // staged words of stripe i
   }
   AeKey k{-1, 0, 0};
   if (i < n) {
@@ -451,12 +463,13 @@ __device__ __forceinline__ void defer_lanes(const HsArgs &k0, bool dfr, bool stg
                                             int head, int from, int L, int wraw) {
   const unsigned long long m = __ballot(dfr);
   const int lane = lane_id(), q0 = first_lane(m);
+  const int x = (int)(blockIdx.x & (kStripes - 1));  // this workgroup's stripe
   unsigned long long b = 0;
-  if (lane == q0) b = atomicAdd(&k0.total[1], (unsigned long long)__popcll(m) << 32) >> 32;
+  if (lane == q0) b = atomicAdd(&k0.total[kStripeDef + kStripeWords * x], (unsigned long long)__popcll(m));
   b = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), q0) << 32) |
       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, q0);
   if (dfr) {
-    k0.defer[b + lanes_below(m)] = i;
+    k0.defer[x * k0.n + (int64_t)b + lanes_below(m)] = i;
     int64_t in_place = -2;  // made here (as a hoisted constant pair it was spilled across the pass)
     asm volatile("" : "+v"(in_place));
     if (!stg) k0.soff[i] = in_place;
@@ -467,17 +480,31 @@ __device__ __forceinline__ void defer_lanes(const HsArgs &k0, bool dfr, bool stg
     k0.fb[i] = make_int4(wraw, 0, 0, 0);  // one store (four separate arrays spilled the main launch)
     if (wraw >= 0) tag_inc(&k0.kin[wraw], k0.epoch);
   }
-  for (unsigned long long sm = __ballot(stg); sm; sm &= sm - 1) {
+  // the staged lanes' offsets: one atomic per wave on the stripe's counter
+  // (an exclusive scan of their sizes), the copies one by one on the wave
+  const unsigned long long smask = __ballot(stg);
+  if (!smask) return;
+  const int64_t cap8 = k0.stage_cap / kStripes;  // stripe x stages in [x cap8, (x + 1) cap8)
+  int64_t pre = stg ? (int64_t)n : 0;  // inclusive scan of the staged sizes over the lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(pre, o, 64);
+    if (lane >= o) pre += v;
+  }
+  const int64_t tot = __shfl(pre, 63, 64);
+  unsigned long long sb = 0;
+  if (lane == first_lane(smask)) sb = atomicAdd(&k0.total[kStripeStg + kStripeWords * x], (unsigned long long)tot);
+  sb = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(sb >> 32), first_lane(smask)) << 32) |
+       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sb, first_lane(smask));
+  const int64_t my = (int64_t)sb + pre - (stg ? (int64_t)n : 0);  // this lane's offset within the stripe
+  if (stg) k0.soff[i] = x * cap8 + my;
+  for (unsigned long long sm = smask; sm; sm &= sm - 1) {
     const int q = first_lane(sm);
     const int nq = __builtin_amdgcn_readlane(n, q);
-    unsigned long long o = 0;
-    if (lane == q) {
-      o = atomicAdd(&k0.total[0], (unsigned long long)nq);
-      k0.soff[i] = (int64_t)o;
-    }
-    o = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(o >> 32), q) << 32) |
-        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)o, q);
-    if ((long long)o + nq <= k0.stage_cap) {  // past the capacity the deferred launch takes the ordered fallback
+    const int64_t oq = ((int64_t)__builtin_amdgcn_readlane((int)((uint64_t)my >> 32), q) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)my, q);
+    const long long o = x * cap8 + oq;
+    if (oq + nq <= cap8) {  // past the stripe's capacity the deferred launch takes the ordered fallback
       const uint64_t ra = (uint64_t)(uintptr_t)row;
       const int32_t *rq = (const int32_t *)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(ra >> 32), q) << 32) |
                                                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ra, q));
@@ -916,15 +943,28 @@ __device__ __forceinline__ void fb_chain(const HsArgs &k, int64_t x) {
   }
 }
 
+// The deferred items as one sequence j = 0 .. nd - 1 over the stripes' lists
+// (stripe x's count d[x], its list at defer[x * n]); wave-uniform counts.
+struct DeferSeq {
+  int64_t d[kStripes];
+  __device__ __forceinline__ int64_t at(const HsArgs &k, int64_t j) const {
+    int x = 0;
+#pragma unroll
+    for (int y = 0; y < kStripes - 1; ++y)
+      if (x == y && j >= d[y]) { j -= d[y]; x = y + 1; }
+    return k.defer[x * k.n + j];
+  }
+};
+
 // The last workgroup: every item not yet run lies on a cycle whose feeding
 // trees have run; each such cycle runs from one member x through the L-word
 // buffer.
-__device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd) {
+__device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd, const DeferSeq &ds) {
   const int lane = lane_id();
   const int L = k.s.L;
   for (int64_t j0 = 0; j0 < nd; j0 += 64) {
     const int64_t j = j0 + lane;
-    const int64_t y = j < nd ? k.defer[j] : -1;
+    const int64_t y = j < nd ? ds.at(k, j) : -1;
     for (unsigned long long m = __ballot(y >= 0 && at_load(&fb_dn(k, y)) == 0); m; m &= m - 1) {
       const int q = first_lane(m);
       const int64_t x = ((int64_t)__builtin_amdgcn_readlane((int)(y >> 32), q) << 32) |
@@ -945,13 +985,13 @@ __device__ __forceinline__ void fb_leftover(const HsArgs &k, int64_t nd) {
   }
 }
 
-__device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd) {
+__device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd, const DeferSeq &ds) {
   // only workgroups with a cycle buffer take items (any of them may complete
   // a cycle and must run it: r6_v6 ran 28k of 32k 2-cycles on the last
   // workgroup when the grid was 16x the buffers); the others only count out
   const int64_t nb = min((int64_t)gridDim.x, (int64_t)max(k.nslot, 1));
   for (int64_t j = blockIdx.x; (int64_t)blockIdx.x < nb && j < nd; j += nb) {
-    const int64_t x = k.defer[j];
+    const int64_t x = ds.at(k, j);
     if (tag_count(&k.kin[x], k.epoch) == 0) {
       fb_chain(k, x);  // no deferred item reads x's row: a chain starts here
     } else {
@@ -976,7 +1016,7 @@ __device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd) {
   if (lane_id() == 0) last = atomicAdd(&k.total[3], 1ull) == (unsigned long long)gridDim.x - 1;
   if (!__builtin_amdgcn_readfirstlane(last)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  fb_leftover(k, nd);
+  fb_leftover(k, nd, ds);
 }
 
 // The deferred launch: every deferred item (a set of one), grid-stride; the
@@ -985,21 +1025,31 @@ __device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd) {
 // from the last call's deferred count, which workgroup 0 publishes to a pinned
 // host word when it changes (total[2] keeps the published value).
 __global__ __launch_bounds__(64, MRAFT_AE_MINW) void k_handle_deferred(HsArgs ka) {
-  const unsigned long long staged = ka.total[0];
-  const int64_t nd = (int64_t)(ka.total[1] >> 32);
+  DeferSeq ds;
+  int64_t nd = 0;
+  long long smax = 0;  // the largest stripe's staged words
+#pragma unroll
+  for (int x = 0; x < kStripes; ++x) {
+    ds.d[x] = (int64_t)ka.total[kStripeDef + kStripeWords * x];
+    nd += ds.d[x];
+    smax = max(smax, (long long)ka.total[kStripeStg + kStripeWords * x]);
+  }
+  const long long cap8 = ka.stage_cap / kStripes;
+  // the need, as a stage whose every stripe holds the largest one's words
+  const long long staged = smax > cap8 ? smax * kStripes : 0;
   if (blockIdx.x == 0 && threadIdx.x == 0 && ka.hint && ka.total[2] != (unsigned long long)nd) {
     ka.total[2] = (unsigned long long)nd;
     __hip_atomic_store(ka.hint, (long long)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // a batch whose staged words exceed the stage: the need, for the host's
   // next call (the stage grows to it under MRAFT_STAGE_AUTO, mraft_abi.hip)
-  if (blockIdx.x == 0 && threadIdx.x == 0 && ka.hint && (long long)staged > ka.stage_cap)
-    __hip_atomic_store(ka.hint + 1, (long long)staged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ka.hint && smax > cap8)
+    __hip_atomic_store(ka.hint + 1, staged, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (nd == 0) return;
-  if ((long long)staged <= ka.stage_cap) {
-    for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) handle_one<1, HM_DEFER>(ka, ka.defer[j], 1);
+  if (smax <= cap8) {
+    for (int64_t j = blockIdx.x; j < nd; j += gridDim.x) handle_one<1, HM_DEFER>(ka, ds.at(ka, j), 1);
   } else {
-    defer_fallback(ka, nd);
+    defer_fallback(ka, nd, ds);
   }
 }
 
