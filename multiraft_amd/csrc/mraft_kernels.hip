@@ -261,6 +261,7 @@ __global__ __launch_bounds__(64) void k_claim_ae(const mraft_ae_args *__restrict
   if (i == 0) total[3] = 0;  // workgroups of the deferred launch's fallback done (total[2]: the published count)
   if (i < kStripes) {
     total[kStripeDef + kStripeWords * i] = 0;  // deferred items of stripe i
+    total[kStripeDef + kStripeWords * i + 1] = 0;  // the fallback's finished workgroups of stripe i
     total[kStripeStg + kStripeWords * i] = 0;  // staged words of stripe i
   }
   AeKey k{-1, 0, 0};
@@ -990,7 +991,8 @@ __device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd, cons
   // a cycle and must run it: r6_v6 ran 28k of 32k 2-cycles on the last
   // workgroup when the grid was 16x the buffers); the others only count out
   const int64_t nb = min((int64_t)gridDim.x, (int64_t)max(k.nslot, 1));
-  for (int64_t j = blockIdx.x; (int64_t)blockIdx.x < nb && j < nd; j += nb) {
+  if ((int64_t)blockIdx.x >= nb) return;  // (not counted below either)
+  for (int64_t j = blockIdx.x; j < nd; j += nb) {
     const int64_t x = ds.at(k, j);
     if (tag_count(&k.kin[x], k.epoch) == 0) {
       fb_chain(k, x);  // no deferred item reads x's row: a chain starts here
@@ -1010,10 +1012,20 @@ __device__ __forceinline__ void defer_fallback(const HsArgs &k, int64_t nd, cons
     }
   }
   // the last workgroup to finish runs what is left (it sees every other
-  // workgroup's runs: release before the count, acquire after it)
+  // workgroup's runs: release before each count, acquire after it). Counted
+  // in two levels, per stripe (blockIdx % 8, its own line) and then the
+  // stripes: one counter taking every workgroup's atomic serialised them
+  // (the 2-cycle-heavy batch's fallback, r6_d1)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   int last = 0;
-  if (lane_id() == 0) last = atomicAdd(&k.total[3], 1ull) == (unsigned long long)gridDim.x - 1;
+  if (lane_id() == 0) {
+    const int64_t x = blockIdx.x & (kStripes - 1);
+    const unsigned long long in_x = (unsigned long long)((nb - 1 - x) / kStripes + 1);  // workgroups b < nb, b % 8 == x
+    if (atomicAdd(&k.total[kStripeDef + kStripeWords * x + 1], 1ull) == in_x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+      last = atomicAdd(&k.total[3], 1ull) == (unsigned long long)min(nb, (int64_t)kStripes) - 1;
+    }
+  }
   if (!__builtin_amdgcn_readfirstlane(last)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   fb_leftover(k, nd, ds);
