@@ -39,7 +39,7 @@ HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
 def kernel_src_sha() -> str:
     import hashlib
     h = hashlib.sha1()
-    for f in ("mraft_tick.hip", "mraft_device.h", "mraft_pass.h"):
+    for f in ("mraft_tick.hip", "mraft_tick_body.inc", "mraft_device.h", "mraft_pass.h"):
         h.update(open(os.path.join(ROOT, "multiraft_amd", "csrc", f), "rb").read())
     return h.hexdigest()[:12]
 

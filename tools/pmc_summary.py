@@ -27,7 +27,7 @@ TICK = "k_tick_group<5, false>"
 
 def kernel_src_sha() -> str:
     h = hashlib.sha1()
-    for f in ("mraft_tick.hip", "mraft_device.h", "mraft_pass.h"):
+    for f in ("mraft_tick.hip", "mraft_tick_body.inc", "mraft_device.h", "mraft_pass.h"):
         h.update(open(os.path.join(ROOT, "multiraft_amd", "csrc", f), "rb").read())
     return h.hexdigest()[:12]
 
