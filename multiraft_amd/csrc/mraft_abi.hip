@@ -677,15 +677,20 @@ int mraft_replicate_tick_count(mraft_engine *h, const int32_t *leader_peer, int6
   Stage sg(h, where);
   void *lp, *cnt;
   TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
-  TRY(scratch(h, 0, 3 * sizeof(unsigned long long), &cnt));
-  HIP_TRY(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), h->stream));
+  constexpr size_t cw = (size_t)mraft::kCountStripes * mraft::kCountWords;
+  TRY(scratch(h, 0, cw * sizeof(unsigned long long), &cnt));
+  HIP_TRY(hipMemsetAsync(cnt, 0, cw * sizeof(unsigned long long), h->stream));
   mraft::launch_replicate_tick_count(dev_of(h), (const int32_t *)lp, (unsigned long long *)cnt,
                                      h->stream);
   HIP_TRY(hipGetLastError());
-  unsigned long long hc[3];
-  HIP_TRY(hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, h->stream));
+  std::vector<unsigned long long> hc(cw);
+  HIP_TRY(hipMemcpyAsync(hc.data(), cnt, cw * sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  for (int i = 0; i < 3; ++i) out_words[i] = (int64_t)hc[i];
+  for (int i = 0; i < 3; ++i) {
+    unsigned long long t = 0;
+    for (int x = 0; x < mraft::kCountStripes; ++x) t += hc[(size_t)x * mraft::kCountWords + i];
+    out_words[i] = (int64_t)t;
+  }
   return MRAFT_OK;
 }
 

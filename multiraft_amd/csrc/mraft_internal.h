@@ -30,6 +30,12 @@ struct LiteBufs {
 };
 void launch_replicate_tick_light(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
                                  int32_t *exp_term_leader, const LiteBufs &lb, hipStream_t st);
+// The algorithmic count's buffer (mraft_replicate_tick_count): kCountStripes
+// stripes of {reads, writes, active groups}, one 128-B line each, by
+// workgroup (one counter word per buffer took every wave's atomic in turn:
+// 1.8 ms per config-#3 count); the host sums the stripes.
+constexpr int kCountStripes = 64;
+constexpr int kCountWords = 16;
 void launch_replicate_tick_count(const Dev &s, const int32_t *lpeer, unsigned long long *counts,
                                  hipStream_t st);
 

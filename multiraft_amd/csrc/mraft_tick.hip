@@ -259,8 +259,8 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
     }
   }
   if (count) {
-    atomicAdd(&counts[0], R);
-    atomicAdd(&counts[2], A);
+    atomicAdd(&counts[kCountWords * (blockIdx.x & (kCountStripes - 1)) + 0], R);
+    atomicAdd(&counts[kCountWords * (blockIdx.x & (kCountStripes - 1)) + 2], A);
   } else {
     if (gflags) gflags[g] = fl;
     ex.put(g, s.commit[g], s.term[g], s.role[g]);
