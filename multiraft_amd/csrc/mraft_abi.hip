@@ -28,7 +28,10 @@ constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
 // blind launch finds wave slots beside another queue's kernels at once:
 // profiles/r5_g1); a deferred-heavy batch gets a workgroup per item from the
 // next call on (round 5's fixed 8 ran such batches on 0.4 % of the chip).
-constexpr int kDeferGridMin = 8;
+#ifndef MRAFT_DEFER_GRID_MIN
+#define MRAFT_DEFER_GRID_MIN 8
+#endif
+constexpr int kDeferGridMin = MRAFT_DEFER_GRID_MIN;
 constexpr int kDeferGridMax = 1 << 16;
 // The light tick's fallback launch (MRAFT_TICK_LIGHT): at least this many
 // workgroups, twice the previous light tick's count, at most the groups (a

@@ -74,6 +74,15 @@ for st in ${DO:-tests bench}; do
           > "$OUT/pst$i.json" 2> "$OUT/pst$i.err" || { tail -5 "$OUT/pst$i.err"; exit 1; }
       done
       python3 tools/pmc_kernels.py "$OUT/steady_counters.json" "$OUT"/pst[0-9]* --kernels "k_tick_lite<5>;k_tick_list<5>;k_tick_group<5, false>" | head -60 ;;
+    abdeferred)
+      # the deferred-heavy handle measurement per library variant (ABDEF_LIBS tags + in-tree)
+      echo "== abdeferred ${ABDEF_LIBS:-}"
+      for t in ${ABDEF_LIBS:-} in-tree; do
+        if [ "$t" = in-tree ]; then unset MRAFT_LIB; else export MRAFT_LIB=$PWD/tools/variants/libmraft_hip_$t.so; fi
+        timeout -k 10 400 python3 tools/bench_deferred.py > "$OUT/abdef_$t.json" 2> "$OUT/abdef_$t.err" || { tail -5 "$OUT/abdef_$t.err"; exit 1; }
+        python3 -c "import json; d=json.loads(open('$OUT/abdef_$t.json').read().strip().splitlines()[-1]); print('$t', {k: (round(v['first_call_ms'], 2), round(v['ms_per_call'], 4)) for k, v in d.items()})"
+      done
+      unset MRAFT_LIB ;;
     abmsg)
       # message path A/B of library variants (tools/build_variants.sh, VARIANTS="tag=DEFINES ...")
       echo "== abmsg ${VARIANTS:-prebuilt}"
