@@ -24,12 +24,15 @@ constexpr int64_t kDefaultStageWords = (int64_t)1 << 22;
 // The deferred launch's grid (mraft_handle_append_entries by reference): the
 // last call's deferred count, read from a pinned word the device writes, in
 // [kDeferGridMin, kDeferGridMax] workgroups (grid-stride beyond). With no
-// deferred item the launch exits at once on kDeferGridMin workgroups (a small
-// blind launch finds wave slots beside another queue's kernels at once:
-// profiles/r5_g1); a deferred-heavy batch gets a workgroup per item from the
-// next call on (round 5's fixed 8 ran such batches on 0.4 % of the chip).
+// deferred item the launch exits at once on kDeferGridMin workgroups; a
+// deferred-heavy batch gets a workgroup per item from the next call on. The
+// minimum bounds the first deferred-heavy call after calls without any (a
+// partition healing): 512 workgroups take it 30.6 -> 1.07 ms (stale second
+// leaders) and 96.9 -> 3.7 ms (2-cycles) against 8, with the message path's
+// pipelines within noise (profiles/r6_g1; round 5 had chosen 8 for ~2 %
+// there, r5_g1).
 #ifndef MRAFT_DEFER_GRID_MIN
-#define MRAFT_DEFER_GRID_MIN 8
+#define MRAFT_DEFER_GRID_MIN 512
 #endif
 constexpr int kDeferGridMin = MRAFT_DEFER_GRID_MIN;
 constexpr int kDeferGridMax = 1 << 16;
