@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -81,6 +82,9 @@ struct mraft_engine {
   bool stage_auto = true;                  // MRAFT_STAGE_AUTO: grow stage_cap to the last overflow's need
   long long *dhint = nullptr;  // pinned host word: the last by-reference call's deferred count (device-written)
   long long *dhint_dev = nullptr;  // its device-side address
+  // the deferred launch's minimum grid: kDeferGridMin, or the environment's
+  // MRAFT_DEFER_GRID_MIN at mraft_create (tests run the small-grid paths with it)
+  long long defer_grid_min = kDeferGridMin;
   // MRAFT_TICK_LIGHT (mraft_set_tick_mode): the lists of groups for the full
   // tick (shard s at its first group + 512 s), a pair of counter sets per shard (the light
   // launch counts into one, the fallback zeroes the other for the next tick)
@@ -451,6 +455,10 @@ int mraft_create(int32_t groups, int32_t peers, int32_t log_capacity, int32_t de
   HIP_TRY(hipSetDevice(device));
   mraft_engine *h = new mraft_engine();
   h->G = groups; h->P = peers; h->L = log_capacity; h->device = device;
+  if (const char *e = getenv("MRAFT_DEFER_GRID_MIN")) {
+    const long long v = atoll(e);
+    if (v >= 1 && v <= kDeferGridMax) h->defer_grid_min = v;
+  }
   if (flags & MRAFT_CREATE_DEDICATED_QUEUE) {
     const int rc = make_queue(h, true, &h->own_stream);
     if (rc) {
@@ -770,7 +778,8 @@ int mraft_handle_append_entries_ex(mraft_engine *h, const mraft_ae_args *args, i
   // the device writes; a stale value only changes the grid, never a result)
   const long long last_nd = *(volatile long long *)h->dhint;
   mraft::AeDeferBufs db{};
-  db.grid = (int)(last_nd < kDeferGridMin ? kDeferGridMin : last_nd > kDeferGridMax ? kDeferGridMax : last_nd);
+  const long long gmin = h->defer_grid_min;
+  db.grid = (int)(last_nd < gmin ? gmin : last_nd > kDeferGridMax ? kDeferGridMax : last_nd);
   db.nslot = (int)std::min<int64_t>(db.grid, std::max<int64_t>(1, kCycSlotWords / h->L));
   // the fallback's per-item records and reader counts, its L-word buffer and
   // nslot cycle buffers

@@ -4,8 +4,9 @@ feeding cycles, cycles longer than the fallback's walk, self-references —
 through mraft_handle_append_entries at the default stage, a stage too small
 (64 words) and none (the fallback: chains hand-off, short cycles on one wave
 each, the rest on the last workgroup), each twice on one engine: the first
-call on the minimal deferred grid (no earlier count), the second on the grid
-the first call's count asked for. GPU == oracle (which copies every item's
+call on the minimal deferred grid (no earlier count: 512 workgroups, and 8
+through MRAFT_DEFER_GRID_MIN), the second on the grid the first call's count
+asked for. GPU == oracle (which copies every item's
 entries before the call, as the reference's gather does,
 src/raft/raft_append_entry.go:50-54) on replies, errors and state."""
 import numpy as np
@@ -19,9 +20,15 @@ from multiraft_amd import Engine
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("gmin", [None, 8])
 @pytest.mark.parametrize("cap", [None, 64, 0])
 @pytest.mark.parametrize("shape", ["random", "long_cycle", "dense"])
-def test_deferred_graphs_gpu(shape, cap):
+def test_deferred_graphs_gpu(shape, cap, gmin, monkeypatch):
+    # gmin 8: the deferred launch's minimum grid far below the item count
+    # (MRAFT_DEFER_GRID_MIN, read at mraft_create): the grid-stride loops and,
+    # in the fallback, workgroups without a cycle buffer
+    if gmin is not None:
+        monkeypatch.setenv("MRAFT_DEFER_GRID_MIN", str(gmin))
     G, P, L = 64, 5, 64
     rng = np.random.default_rng({"random": 700, "long_cycle": 701, "dense": 702}[shape])
     st, c = deferred_graph_state(G, P, L, rng)
