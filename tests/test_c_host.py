@@ -2,8 +2,9 @@
 mraft_host_tick.c includes only include/mraft.h (C11, -Wall -Wextra -Werror
 -pedantic, no C++, no HIP header) and links libmraft_hip.so as a cgo binding
 does. On each seeded tick vector it runs one replication
-round three ways, each on a fresh engine: the fused tick
-(set_tick_shards(2) -> replicate_tick_export), the per-message sequence a Go
+round four ways, each on a fresh engine: the fused tick
+(set_tick_shards(2) -> replicate_tick_export), the same with
+set_tick_mode(MRAFT_TICK_LIGHT) (ABI 6), the per-message sequence a Go
 host drives (gather_append_args -> handle_append_entries_ex by reference ->
 process_append_replies -> export_group_status), and the same with the entries
 passed by value; every path's flags, GetState words and state are compared
