@@ -505,7 +505,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     memory populations, like the headline's)."""
     import torch
 
-    from multiraft_amd import DEVICE, Engine, synth_election_state, synth_seed, synth_tick_state
+    from multiraft_amd import DEVICE, TICK_FULL, Engine, synth_election_state, synth_seed, synth_tick_state
 
     out = {}
 
@@ -612,6 +612,7 @@ def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):
     c2 = {k: v.clone() for k, v in m2.items()}
     lp2_d = torch.from_numpy(lp2).to(dev)
     e2 = Engine(G2, P2, L2, device=dev.index or 0, alloc=False)
+    e2.set_tick_mode(TICK_FULL)  # the fused tick (MRAFT_TICK_AUTO would settle here after one light probe)
     e2.set_stream(stream.cuda_stream)
     gf2 = torch.zeros(G2, dtype=torch.int32, device=dev)
     t2 = []
@@ -683,7 +684,7 @@ def config4_one_gpu(dev, stream, steps=10, shards=(1, 2)):
     may use."""
     import torch
 
-    from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
+    from multiraft_amd import DEVICE, TICK_FULL, Engine, synth_seed, synth_tick_state
     G4, P, L = 262144, 5, 4096
     t = time.perf_counter()
     st, lp, _ = synth_tick_state(G4, P, L, seed=synth_seed(3), nthreads=cpu_share()["threads"])
@@ -698,6 +699,7 @@ def config4_one_gpu(dev, stream, steps=10, shards=(1, 2)):
     lp_d = torch.from_numpy(lp).to(dev)
     gf = torch.zeros(G4, dtype=torch.int32, device=dev)
     eng = Engine(G4, P, L, device=dev.index or 0, alloc=False)
+    eng.set_tick_mode(TICK_FULL)
     eng.set_stream(stream.cuda_stream)
     eng.bind(master)
     rd, wr, active = eng.replicate_tick_count(lp_d, where=DEVICE)
@@ -1096,7 +1098,7 @@ def main():
         # the host; the data path (the fan-in) is the library's RCCL gather
         dist.init_process_group("gloo")
 
-    from multiraft_amd import DEVICE, Engine, synth_seed, synth_tick_state
+    from multiraft_amd import DEVICE, TICK_FULL, Engine, synth_seed, synth_tick_state
     from multiraft_amd.router import RcclFanIn, allgather_status_packed
 
     if args.config == 2:
@@ -1173,6 +1175,10 @@ def main():
     # (mraft_set_tick_shards); shard s's tick i+1 follows only its own tick i.
     S = args.shards if (args.shards > 1 and not restore and G >= args.shards) else 1
     eng = Engine(G, P, L, device=local_dev, alloc=False)
+    # The measured path is the fused tick (k_tick_group): on a fresh config-#3
+    # copy every group needs it, and MRAFT_TICK_AUTO (the engine default)
+    # chooses it after one light probe; set here so no warmup setting changes it.
+    eng.set_tick_mode(TICK_FULL)
     eng.set_tick_shards(S)
     if rccl and args.fanin_cus:
         # the tick's queues are masked off the fan-in's reserved CUs (include/mraft.h)
@@ -1310,6 +1316,7 @@ def main():
         for k in ck:
             ck[k].copy_(master[k])
         one = Engine(G, P, L, device=local_dev, alloc=False)  # one launch, on torch's stream
+        one.set_tick_mode(TICK_FULL)
         one.set_stream(stream.cuda_stream)
         one.bind(ck)
         gf1 = torch.zeros_like(gf_d)
@@ -1386,7 +1393,7 @@ def main():
                    "tick_stream_marks_per_step": (1 if chain else 2) + args.extra_marks
                    + (1 if fan is not None and not chain else 0),
                    "step_minus_kernel_ms": dt / K * 1e3 - float(np.mean(ker_ms)),
-                   "shards_per_gpu": S,
+                   "shards_per_gpu": S, "tick_mode": "MRAFT_TICK_FULL (the fused tick; MRAFT_TICK_AUTO, the default, chooses it on this workload)",
                    "shard_pipelining": (None if S == 1 else
                                         f"mraft_set_tick_shards({S}): one engine, {S} contiguous group "
                                         f"ranges of ~{G // S} on {S} hardware queues the engine owns; each "

@@ -476,8 +476,8 @@ int32_t mraft_get_tick_shards(const mraft_engine *h);
  * NULL when out of range): for events that time or order against a shard. */
 void *mraft_shard_stream(mraft_engine *h, int32_t shard);
 
-/* Tick path (ABI 6). MRAFT_TICK_FULL (the default): one wave per group, the
- * streaming pass of the fused tick. MRAFT_TICK_LIGHT: for a running
+/* Tick path (ABI 6). MRAFT_TICK_FULL: one wave per group, the streaming pass
+ * of the fused tick. MRAFT_TICK_LIGHT: for a running
  * deployment's ticks (heartbeats and a few appended entries per leader): a
  * first launch settles, eight groups per wave, every group whose followers all
  * reply success without a compare (prevLogTerm matches; a heartbeat, or an
@@ -493,7 +493,8 @@ void *mraft_shard_stream(mraft_engine *h, int32_t shard);
  * tick while the last completed light tick sent at most a quarter of the
  * groups to the full tick (or before any has completed), otherwise the full
  * tick with a light tick every 32nd to measure again (the counts reach the
- * host asynchronously: a choice may follow a count a few ticks old). */
+ * host asynchronously: a choice may follow a count a few ticks old).
+ * MRAFT_TICK_AUTO is the default. */
 enum { MRAFT_TICK_FULL = 0, MRAFT_TICK_LIGHT = 1, MRAFT_TICK_AUTO = 2 };
 int mraft_set_tick_mode(mraft_engine *h, int32_t mode);
 int32_t mraft_get_tick_mode(const mraft_engine *h);  /* -1: null handle */

@@ -89,7 +89,7 @@ struct mraft_engine {
   // tick (shard s at its first group + 512 s), a pair of counter sets per shard (the light
   // launch counts into one, the fallback zeroes the other for the next tick)
   // and per shard the last fallback count, pinned (dhint + kHintLite + s)
-  int32_t tick_mode = MRAFT_TICK_FULL;
+  int32_t tick_mode = MRAFT_TICK_AUTO;
   int32_t *lite_list = nullptr;
   unsigned *lite_cnt = nullptr;
   int lite_par[kMaxShards] = {};

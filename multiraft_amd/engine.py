@@ -154,7 +154,7 @@ class Engine:
         return int(self._lib.mraft_get_tick_shards(self._h))
 
     def set_tick_mode(self, mode: int):
-        """TICK_FULL (default), TICK_LIGHT or TICK_AUTO (mraft_set_tick_mode):
+        """TICK_FULL, TICK_LIGHT or TICK_AUTO (the default; mraft_set_tick_mode):
         the light tick settles steady-state groups eight per wave and runs the
         rest through the full tick; AUTO picks per shard from the last light
         tick's fallback share. Outputs are identical in every mode."""

@@ -155,14 +155,15 @@ def test_light_top_of_index_domain_gpu(j):
 
 
 def test_light_mode_calls_and_p1_gpu():
-    """The mode calls (bad modes rejected, the mode kept across shard changes)
-    and P = 1, where the one-lane-per-group tick already is the light form."""
+    """The mode calls (MRAFT_TICK_AUTO by default, bad modes rejected, the mode
+    kept across shard changes) and P = 1, where the one-lane-per-group tick
+    already is the light form."""
     G, P, L = 64, 1, 16
     st, lp, _ = synth_tick_state(G, P, L, seed=3)
     o = Oracle(G, P, L, st)
     with Engine(G, P, L) as e:
         e.load_state(st)
-        assert e.tick_mode() == TICK_FULL
+        assert e.tick_mode() == TICK_AUTO  # the default
         with pytest.raises(MraftError):
             e.set_tick_mode(3)
         e.set_tick_mode(TICK_LIGHT)
