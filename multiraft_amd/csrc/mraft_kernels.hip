@@ -410,22 +410,6 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// The source row's writer of a deferred item: the item that owns the row it
-// reads (claim winner) when that row is claimed in this call and the owner is
-// itself a deferred item (a well-formed reference; its slot is read, so it
-// was deferred); else -1.
-__device__ __forceinline__ int64_t ae_writer(const HsArgs &k, int64_t x) {
-  const mraft_ae_args a = k.args[x];
-  const int L = k.s.L;
-  const int64_t gp = (int64_t)k.s.G * k.s.P;
-  if (a.n_entries <= 0 || !ae_ref_ok(a, gp * L, L) || !ae_index_ok(a)) return -1;
-  const unsigned long long c = __hip_atomic_load(&k.claim[a.entries_offset / L], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  if ((uint32_t)(c >> 32) != k.epoch) return -1;
-  const int64_t w = (int64_t)(0xFFFFFFFFull - (c & 0xFFFFFFFFull));
-  return ae_ref_ok(k.args[w], gp * L, L) ? w : -1;
-}
-
 __device__ __forceinline__ int at_load(int32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
