@@ -380,7 +380,14 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     lq = np.where(lp >= 0)[0]
     ldr = torch.from_numpy((lq * P + lp[lq]).astype(np.int32)).to(dev)
     nl = len(lq)
-    cnts = [torch.from_numpy(rng.integers(1, 5, size=nl).astype(np.int32)).to(dev) for _ in range(steps)]
+    cnts_h = [rng.integers(1, 5, size=nl).astype(np.int32) for _ in range(steps)]
+    cnts = [torch.from_numpy(c).to(dev) for c in cnts_h]
+    # the same Starts per group, for mraft_start_and_tick (0 where no leader)
+    gcnts = []
+    for c in cnts_h:
+        gc = np.zeros(G, np.int32)
+        gc[lq] = c
+        gcnts.append(torch.from_numpy(gc).to(dev))
     oi, ot, ol, oe = (torch.zeros(nl, dtype=torch.int32, device=dev) for _ in range(4))
     lp_d = torch.from_numpy(lp.astype(np.int32)).to(dev)
     gf = torch.zeros(G, dtype=torch.int32, device=dev)
@@ -416,6 +423,19 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     log_full = int((oe.cpu().numpy() == 3).sum())
     lstart_ms, ltick_ms, lspan_ss, lflags = timed(TICK_LIGHT, copies[1])
     same = bool(np.array_equal(flags, lflags)) and all(torch.equal(copies[0][k], copies[1][k]) for k in master)
+    # the same sequence as one call per step (mraft_start_and_tick, light
+    # tick: Start inside its first launch), on a third copy
+    restore(copies[2])
+    e.set_tick_mode(TICK_LIGHT)
+    fmarks = [ev() for _ in range(steps + 1)]
+    fmarks[0].record(st)
+    for k in range(steps):
+        e.start_and_tick(lp_d, gcnts[k], gf, where=DEVICE)
+        fmarks[k + 1].record(st)
+    e.synchronize()
+    fstep_ms = [fmarks[k].elapsed_time(fmarks[k + 1]) for k in range(steps)]
+    fflags = gf.cpu().numpy()
+    fsame = bool(np.array_equal(flags, fflags)) and all(torch.equal(copies[0][k], copies[2][k]) for k in master)
     # count pass (same sequence, the count before each tick)
     restore(copies[0])
     e.set_tick_mode(TICK_FULL)
@@ -487,7 +507,16 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
                       "tick_hbm_frac_steady": bytes_ss / (ltick_ss / 1e3) / HBM_PEAK,
                       "speedup_tick_steady": tick_ss / ltick_ss,
                       "fallback_groups_steps": fallbacks,
-                      "state_equals_full": same}}
+                      "state_equals_full": same},
+            "fused": {"what": "mraft_start_and_tick with MRAFT_TICK_LIGHT: the Start of every step inside the light "
+                              "tick's first launch, one call and one event per step (the same Starts and ticks as "
+                              "above, on a third copy)",
+                      "step_ms_steps": [round(x, 4) for x in fstep_ms],
+                      "device_ms_per_step_steady": float(np.mean(fstep_ms[2:])),
+                      "decisions_per_s_steady": G / (float(np.mean(fstep_ms[2:])) / 1e3),
+                      "vs_full_start_then_tick": span_ss / float(np.mean(fstep_ms[2:])),
+                      "vs_light_start_then_tick": lspan_ss / float(np.mean(fstep_ms[2:])),
+                      "state_equals_full": fsame}}
 
 
 def secondary(master, copies, lp, G, P, L, stream, dev, headline_ms, steps=8):

@@ -503,6 +503,24 @@ int32_t mraft_get_tick_mode(const mraft_engine *h);  /* -1: null handle */
  * first light tick or for a null handle. */
 int64_t mraft_tick_light_fallbacks(mraft_engine *h);
 
+/* Start (raft.go:90-104) at every group's leader replica, then the tick, in
+ * one call (ABI 6): for each group g with leader_peer[g] in [0, P),
+ * counts[g] >= 1 entries are appended at replica g*P + leader_peer[g]
+ * exactly as mraft_start would append them (counts[g] == 0: no Start;
+ * counts[g] < 0: MRAFT_ITEM_BAD_SLOT), then mraft_replicate_tick runs on the
+ * result. out_index / out_term / out_is_leader / item_err are per group (G
+ * each), mraft_start's per-item outputs; a group whose leader_peer is out of
+ * range starts nothing (-1, -1, 0; MRAFT_ITEM_BAD_SLOT when leader_peer >= P
+ * and counts[g] != 0). Equivalent to mraft_start over those slots followed by
+ * mraft_replicate_tick; when the light tick runs (MRAFT_TICK_LIGHT, or AUTO
+ * choosing it) Start is done inside its first launch, otherwise as its own
+ * launch before the full tick. group_flags optional. */
+int mraft_start_and_tick(mraft_engine *h, const int32_t *leader_peer,
+                         const int32_t *counts, int32_t *out_index,
+                         int32_t *out_term, int32_t *out_is_leader,
+                         int32_t *item_err, int32_t *group_flags,
+                         int32_t where);
+
 /* mraft_replicate_tick followed by mraft_export_group_status for the same
  * leader_peer, fused into the one launch (the words the shard router
  * all-gathers come out of the tick itself): commit[g] / term_leader[g] are

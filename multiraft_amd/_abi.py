@@ -100,7 +100,7 @@ ABI_SYMBOLS = (
     "mraft_fanin_synchronize", "mraft_fanin_stream", "mraft_fanin_reserve_cus",
     "mraft_set_tick_shards", "mraft_get_tick_shards", "mraft_shard_stream", "mraft_handle_append_entries_ex",
     "mraft_set_stage_capacity", "mraft_get_stage_capacity",
-    "mraft_set_tick_mode", "mraft_get_tick_mode", "mraft_tick_light_fallbacks",
+    "mraft_set_tick_mode", "mraft_get_tick_mode", "mraft_tick_light_fallbacks", "mraft_start_and_tick",
 )
 SYNTH_SYMBOLS = ("mraft_synth_tick_state", "mraft_synth_fold_batch", "mraft_synth_election_state")
 
@@ -159,6 +159,7 @@ _SIGS = {
     "mraft_set_tick_mode": (ctypes.c_int, [_vp, _i32]),
     "mraft_get_tick_mode": (_i32, [_vp]),
     "mraft_tick_light_fallbacks": (_i64, [_vp]),
+    "mraft_start_and_tick": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32]),
 }
 _SYNTH_SIGS = {
     "mraft_synth_tick_state": (ctypes.c_int, [ctypes.c_uint64, _i32, _i32, _i32, _i32, _i32,

@@ -285,11 +285,16 @@ bool auto_light(mraft_engine *h, int s, int32_t gs) {
   return false;
 }
 
+// sio (mraft_start_and_tick): Start at the range's leaders first — inside the
+// light launch, or as its own launch before the full tick.
 void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const int32_t *lp, int32_t *gf,
-                int32_t *ec, int32_t *et, hipStream_t st) {
+                int32_t *ec, int32_t *et, hipStream_t st, const mraft::StartIO *sio = nullptr) {
   const bool light = h->P >= 2 && (h->tick_mode == MRAFT_TICK_LIGHT ||
                                    (h->tick_mode == MRAFT_TICK_AUTO && auto_light(h, s, d.G)));
+  mraft::StartIO so{};
+  if (sio) so = {sio->counts + g0, sio->oi + g0, sio->ot + g0, sio->ol + g0, sio->err + g0};
   if (!light) {
+    if (sio) mraft::launch_start_groups(d, lp + g0, so, st);
     mraft::launch_replicate_tick(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), st);
     return;
   }
@@ -305,13 +310,14 @@ void tick_range(mraft_engine *h, const mraft::Dev &d, int s, int32_t g0, const i
   // one wave per SIMD slot, grid-stride
   const long long gr = prev < 0 ? kLiteGridUnknown : std::max(kLiteGridMin, 2 * prev);
   lb.grid = (int)std::max(1ll, std::min(gr, (long long)d.G));
-  mraft::launch_replicate_tick_light(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), lb, st);
+  mraft::launch_replicate_tick_light(d, lp + g0, off(gf, g0), off(ec, g0), off(et, g0), lb, sio ? &so : nullptr, st);
 }
 
-int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, int32_t *et) {
+int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, int32_t *et,
+                const mraft::StartIO *sio = nullptr) {
   if (h->tick_mode != MRAFT_TICK_FULL) TRY(ensure_lite(h));
   if (h->nshards <= 1) {
-    tick_range(h, dev_of(h), 0, 0, lp, gf, ec, et, h->stream);
+    tick_range(h, dev_of(h), 0, 0, lp, gf, ec, et, h->stream, sio);
     HIP_TRY(hipGetLastError());
     return MRAFT_OK;
   }
@@ -320,7 +326,7 @@ int launch_tick(mraft_engine *h, const int32_t *lp, int32_t *gf, int32_t *ec, in
   for (int s = 0; s < h->nshards; ++s) {
     const int32_t g0 = (int32_t)((int64_t)h->G * s / h->nshards), g1 = (int32_t)((int64_t)h->G * (s + 1) / h->nshards);
     if (g1 <= g0) continue;
-    tick_range(h, dev_slice(h, g0, g1), s, g0, lp, gf, ec, et, h->shard_q[s]);
+    tick_range(h, dev_slice(h, g0, g1), s, g0, lp, gf, ec, et, h->shard_q[s], sio);
   }
   h->shards_pending = true;
   HIP_TRY(hipGetLastError());
@@ -663,6 +669,29 @@ int mraft_replicate_tick(mraft_engine *h, const int32_t *leader_peer, int32_t *g
   TRY(sg.map(leader_peer, sizeof(int32_t) * h->G, true, false, &lp));
   TRY(sg.map(group_flags, sizeof(int32_t) * h->G, false, true, &gf));
   TRY(launch_tick(h, (const int32_t *)lp, (int32_t *)gf, nullptr, nullptr));
+  if (where == MRAFT_HOST) TRY(join_shards(h));
+  return sg.finish();
+}
+
+int mraft_start_and_tick(mraft_engine *h, const int32_t *leader_peer, const int32_t *counts, int32_t *out_index,
+                         int32_t *out_term, int32_t *out_is_leader, int32_t *item_err, int32_t *group_flags,
+                         int32_t where) {
+  TRY(check(h));
+  if (!leader_peer || !counts || !out_index || !out_term || !out_is_leader || !item_err)
+    return fail(MRAFT_E_INVAL, "null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  Stage sg(h, where);
+  void *lp, *c, *oi, *ot, *ol, *e, *gf;
+  const size_t gb = sizeof(int32_t) * h->G;
+  TRY(sg.map(leader_peer, gb, true, false, &lp));
+  TRY(sg.map(counts, gb, true, false, &c));
+  TRY(sg.map(out_index, gb, false, true, &oi));
+  TRY(sg.map(out_term, gb, false, true, &ot));
+  TRY(sg.map(out_is_leader, gb, false, true, &ol));
+  TRY(sg.map(item_err, gb, false, true, &e));
+  TRY(sg.map(group_flags, gb, false, true, &gf));
+  const mraft::StartIO sio{(const int32_t *)c, (int32_t *)oi, (int32_t *)ot, (int32_t *)ol, (int32_t *)e};
+  TRY(launch_tick(h, (const int32_t *)lp, (int32_t *)gf, nullptr, nullptr, &sio));
   if (where == MRAFT_HOST) TRY(join_shards(h));
   return sg.finish();
 }

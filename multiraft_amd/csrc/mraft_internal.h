@@ -28,8 +28,17 @@ struct LiteBufs {
   long long *hint;
   int grid;
 };
+// mraft_start_and_tick: per group, counts[g] entries to Start at replica
+// leader_peer[g] (0: none), and Start's outputs per group.
+struct StartIO {
+  const int32_t *counts;
+  int32_t *oi, *ot, *ol, *err;
+};
 void launch_replicate_tick_light(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
-                                 int32_t *exp_term_leader, const LiteBufs &lb, hipStream_t st);
+                                 int32_t *exp_term_leader, const LiteBufs &lb, const StartIO *sio, hipStream_t st);
+// Start at every group's leader replica (k_start per group; mraft_start_and_tick
+// on the full tick's path).
+void launch_start_groups(const Dev &s, const int32_t *lpeer, const StartIO &sio, hipStream_t st);
 // The algorithmic count's buffer (mraft_replicate_tick_count): kCountStripes
 // stripes of {reads, writes, active groups}, one 128-B line each, by
 // workgroup (one counter word per buffer took every wave's atomic in turn:

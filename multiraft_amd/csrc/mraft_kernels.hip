@@ -1600,6 +1600,37 @@ __global__ void k_start(Dev s, const int32_t *__restrict__ slots, const int32_t 
   oi[i] = idx; ot[i] = term; ol[i] = isl;
 }
 
+// Start at every group's leader replica (mraft_start_and_tick on the full
+// tick's path): slot g * P + leader_peer[g], counts[g] entries (0: none), the
+// rules of k_start; a group whose leader_peer is out of range starts nothing
+// (MRAFT_ITEM_BAD_SLOT when it asked for entries with leader_peer >= P).
+__global__ void k_start_groups(Dev s, const int32_t *__restrict__ lpeer, StartIO sio) {
+  const int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (g >= s.G) return;
+  const int lp = lpeer[g], k = sio.counts[g];
+  int idx = -1, term = -1, isl = 0, e = 0;
+  if (lp >= 0 && lp < s.P) {
+    const int64_t sl = g * s.P + lp;
+    if (k < 0) {
+      e = MRAFT_ITEM_BAD_SLOT;
+    } else if (k > 0 && s.role[sl] == kLeader) {                        // raft.go:93-95
+      const int last = s.last[sl], dummy = s.dummy[sl], t = s.term[sl], h = s.head[sl];
+      if ((int64_t)last + k - dummy > (int64_t)s.L - 1 || (int64_t)last + k > (int64_t)INT32_MAX - 1) {
+        e = MRAFT_ITEM_LOG_FULL;
+      } else {
+        if (last > dummy && s.log[sl * s.L + ring(last - dummy + h, s.L)] > t) s.srt[sl] = 0;
+        for (int j = 1; j <= k; ++j) s.log[sl * s.L + ring(last + j - dummy + h, s.L)] = t;  // :96-100
+        s.last[sl] = last + k;
+        mark_persist(s, sl, MRAFT_PERSIST_STATE);                        // :101
+        idx = last + 1; term = t; isl = 1;                               // :103
+      }
+    }
+  } else if (lp >= s.P && k != 0) {
+    e = MRAFT_ITEM_BAD_SLOT;
+  }
+  sio.oi[g] = idx; sio.ot[g] = term; sio.ol[g] = isl; sio.err[g] = e;
+}
+
 // ---------------------------------------------------------------- applier
 __global__ void k_collect_apply(Dev s, int32_t *__restrict__ from, int32_t *__restrict__ to,
                                 int32_t *__restrict__ snap_index, int32_t *__restrict__ snap_term) {
@@ -2182,6 +2213,11 @@ void launch_start(const Dev &s, const int32_t *slots, const int32_t *counts, int
                      epoch, err);
   hipLaunchKernelGGL(k_start, dim3(blocks_for(n)), dim3(kBlock), 0, st, s, slots, counts, n, oi, ot,
                      ol, err, claim, epoch);
+}
+
+void launch_start_groups(const Dev &s, const int32_t *lpeer, const StartIO &sio, hipStream_t st) {
+  if (s.G <= 0) return;
+  hipLaunchKernelGGL(k_start_groups, dim3(blocks_for(s.G)), dim3(kBlock), 0, st, s, lpeer, sio);
 }
 
 void launch_collect_apply(const Dev &s, int32_t *from, int32_t *to, int32_t *snap_index, int32_t *snap_term,

@@ -290,11 +290,18 @@ __global__ void k_tick_p1(Dev s, const int32_t *__restrict__ leader_peer,
 constexpr int kLiteSpan = 64;
 constexpr int kLiteWaves = 4;  // waves per light workgroup: 32 groups, one list reservation
 
-template <int P>
+// START (mraft_start_and_tick): Start (raft.go:90-104) of counts[g] entries at
+// the group's leader replica first, inside this launch: the leader lane
+// appends them (terms_sorted, lastIndex, persist bit, as k_start) and the
+// tick runs on the result — the new entries' terms are currentTerm, known
+// without a load (the followers' copies and a1's probe of the new last).
+// Groups that fall back carry their Start's stores into the full tick.
+template <int P, bool START>
 __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const int32_t *__restrict__ leader_peer,
                                                                int32_t *__restrict__ gflags, Export ex,
                                                                int32_t *__restrict__ fb_list,
-                                                               unsigned *__restrict__ fb_count, int cap) {
+                                                               unsigned *__restrict__ fb_count, int cap,
+                                                               StartIO sio) {
   __shared__ unsigned sh_cnt, sh_base;
   const int lane = lane_id(), j = lane & 7, gbase = lane & ~7, wv = (int)(threadIdx.x >> 6);
   const int xcd = (int)(blockIdx.x & 7);
@@ -316,7 +323,9 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
   int nx[P];
 #pragma unroll
   for (int x = 0; x < P; ++x) nx[x] = 0;
+  int kcnt = 0;  // START: entries to append at the leader
   if (live) lpv = leader_peer[g];
+  if (START && live) kcnt = sio.counts[g];
   if (rl) {
     rrole = s.role[r]; rterm = s.term[r]; rcommit = s.commit[r]; rlast = s.last[r];
     rdummy = s.dummy[r]; rhead = s.head[r]; rsrt = s.srt[r];
@@ -334,8 +343,32 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
   }
   bool go = live && lpv >= 0 && lpv < P;
   const int lp = go ? lpv : 0;
-  const int role = bc(rrole, lp), T = bc(rterm, lp), c0 = bc(rcommit, lp), last = bc(rlast, lp),
-            ldummy = bc(rdummy, lp), lhead = bc(rhead, lp), lsrt = bc(rsrt, lp);
+  const int role = bc(rrole, lp), T = bc(rterm, lp), c0 = bc(rcommit, lp), last0 = bc(rlast, lp),
+            ldummy = bc(rdummy, lp), lhead = bc(rhead, lp), lsrt0 = bc(rsrt, lp);
+  // START: mraft_start's decision (k_start) for the group's leader replica
+  bool started = false;
+  int serr = 0;
+  if (START && live) {
+    if (lpv >= 0 && lpv < P) {
+      if (kcnt < 0) {
+        serr = MRAFT_ITEM_BAD_SLOT;
+      } else if (kcnt > 0 && role == kLeader) {                          // raft.go:93-95
+        if ((int64_t)last0 + kcnt - ldummy > (int64_t)L - 1 || (int64_t)last0 + kcnt > (int64_t)INT32_MAX - 1)
+          serr = MRAFT_ITEM_LOG_FULL;
+        else
+          started = true;
+      }
+    } else if (lpv >= P && kcnt != 0) {
+      serr = MRAFT_ITEM_BAD_SLOT;
+    }
+    if (j == 0) {
+      sio.oi[g] = started ? last0 + 1 : -1;                              // :103
+      sio.ot[g] = started ? T : -1;
+      sio.ol[g] = started ? 1 : 0;
+      sio.err[g] = serr;
+    }
+  }
+  const int last = started ? last0 + kcnt : last0;                       // :96-100
   if (go && (role != kLeader || c0 < ldummy)) {  // appendOneRound returns (:22-25) / MRAFT_ITEM_BAD_STATE
     if (j == 0) {
       if (gflags) gflags[g] = role != kLeader ? 0 : MRAFT_G_ERROR;
@@ -373,20 +406,35 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
   const bool t2 = go && !gfb;
   int pt = 0, ft = 0, probe = 0;
   int e4[4] = {0, 0, 0, 0};
+  // (START: Indexes above last0 are the entries Start appends, currentTerm)
   if (t2) {
     if (isf && !bel) {
-      pt = s.log[lrow + ring(prev + lb, L)];                             // :49
+      pt = (START && prev > last0) ? T : s.log[lrow + ring(prev + lb, L)];  // :49
       ft = s.log[f * L + ring(prev - fdummy + fhead, L)];                // :128
     }
     if (mrg) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (u < n) e4[u] = s.log[lrow + ring(prev + 1 + u + lb, L)];
+        if (u < n) e4[u] = (START && prev + 1 + u > last0) ? T : s.log[lrow + ring(prev + 1 + u + lb, L)];
     }
-    if (j == lp) probe = s.log[lrow + ring(last + lb, L)];               // a1's probe (:98)
   }
+  // a1's probe (:98) of the pre-Start last: the tick's top when nothing was
+  // appended, and Start's terms_sorted rule (k_start) when something was
+  if ((t2 || started) && j == lp) probe = s.log[lrow + ring(last0 + lb, L)];
   if (t2 && isf && !bel && ft != pt) fb = true;                          // a conflict: the full tick
-  const int t = bc(probe, lp);
+  const int pr0 = bc(probe, lp);
+  const int t = started ? T : pr0;  // log[last]: an appended entry's term when Start appended
+  // the leader's terms_sorted after Start: cleared when an older entry above
+  // the dummy carries a term above currentTerm
+  const bool sclr = started && last0 > ldummy && pr0 > T;
+  const int lsrt = sclr ? 0 : lsrt0;
+  if (START && started && j == lp) {
+    const long long sl = (long long)g * P + lp;
+    if (sclr) s.srt[sl] = 0;
+    for (int u = 1; u <= kcnt; ++u) s.log[lrow + ring(last0 + u + lb, L)] = T;
+    s.last[sl] = last;
+    if (s.pdirty) s.pdirty[sl] = rpd | MRAFT_PERSIST_STATE;             // :101
+  }
   int commit = c0;
   gfb = gfb || ((__ballot(fb) >> gbase) & 0xffull) != 0;
   if (go && !gfb && nsucc > 0 && last > c0) {                             // top = last (above)
@@ -405,7 +453,8 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
     for (int c = 4; c < n; c += 4) {
       int x[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = c + u < n ? s.log[lrow + ring(prev + 1 + c + u + lb, L)] : 0;
+      for (int u = 0; u < 4; ++u)
+        x[u] = c + u >= n ? 0 : (START && prev + 1 + c + u > last0) ? T : s.log[lrow + ring(prev + 1 + c + u + lb, L)];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (c + u < n) s.log[frow + ring(fb0 + c + u, L)] = x[u];
@@ -497,9 +546,13 @@ __global__ __launch_bounds__(64, MRAFT_TICK_MINW) void k_tick_list(Dev s, const 
 
 template <int P>
 void launch_tick_light_p(const Dev &s, const int32_t *lpeer, int32_t *gflags, Export ex, const LiteBufs &lb,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(k_tick_lite<P>, dim3((unsigned)lite_blocks(s.G)), dim3(64 * kLiteWaves), 0, st, s, lpeer, gflags,
-                     ex, lb.list, lb.cnt, lite_cap(s.G));
+                         const StartIO *sio, hipStream_t st) {
+  if (sio)
+    hipLaunchKernelGGL((k_tick_lite<P, true>), dim3((unsigned)lite_blocks(s.G)), dim3(64 * kLiteWaves), 0, st, s,
+                       lpeer, gflags, ex, lb.list, lb.cnt, lite_cap(s.G), *sio);
+  else
+    hipLaunchKernelGGL((k_tick_lite<P, false>), dim3((unsigned)lite_blocks(s.G)), dim3(64 * kLiteWaves), 0, st, s,
+                       lpeer, gflags, ex, lb.list, lb.cnt, lite_cap(s.G), StartIO{});
   hipLaunchKernelGGL(k_tick_list<P>, dim3((unsigned)lb.grid), dim3(64), 0, st, s, lpeer, gflags,
                      (unsigned long long *)nullptr, ex, (const int32_t *)lb.list, (const unsigned *)lb.cnt,
                      lb.cnt_next, lb.hint, lite_cap(s.G));
@@ -546,17 +599,19 @@ void launch_replicate_tick(const Dev &s, const int32_t *lpeer, int32_t *gflags, 
 }
 
 void launch_replicate_tick_light(const Dev &s, const int32_t *lpeer, int32_t *gflags, int32_t *exp_commit,
-                                 int32_t *exp_term_leader, const LiteBufs &lb, hipStream_t st) {
+                                 int32_t *exp_term_leader, const LiteBufs &lb, const StartIO *sio, hipStream_t st) {
   const Export ex{exp_commit, exp_term_leader};
   switch (s.P) {
-    case 2: launch_tick_light_p<2>(s, lpeer, gflags, ex, lb, st); break;
-    case 3: launch_tick_light_p<3>(s, lpeer, gflags, ex, lb, st); break;
-    case 4: launch_tick_light_p<4>(s, lpeer, gflags, ex, lb, st); break;
-    case 5: launch_tick_light_p<5>(s, lpeer, gflags, ex, lb, st); break;
-    case 6: launch_tick_light_p<6>(s, lpeer, gflags, ex, lb, st); break;
-    case 7: launch_tick_light_p<7>(s, lpeer, gflags, ex, lb, st); break;
-    case 8: launch_tick_light_p<8>(s, lpeer, gflags, ex, lb, st); break;
-    default: launch_tick_c<false>(s, lpeer, gflags, nullptr, ex, st);  // P == 1: k_tick_p1 is a lane per group already
+    case 2: launch_tick_light_p<2>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 3: launch_tick_light_p<3>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 4: launch_tick_light_p<4>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 5: launch_tick_light_p<5>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 6: launch_tick_light_p<6>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 7: launch_tick_light_p<7>(s, lpeer, gflags, ex, lb, sio, st); break;
+    case 8: launch_tick_light_p<8>(s, lpeer, gflags, ex, lb, sio, st); break;
+    default:  // P == 1: k_tick_p1 is a lane per group already
+      if (sio) launch_start_groups(s, lpeer, *sio, st);
+      launch_tick_c<false>(s, lpeer, gflags, nullptr, ex, st);
   }
 }
 

@@ -222,6 +222,25 @@ class Engine:
             "mraft_replicate_tick")
         return group_flags
 
+    def start_and_tick(self, leader_peer, counts, group_flags=None, where: int = HOST):
+        """Start (raft.go:90-104) of counts[g] entries at every group's leader
+        replica, then the tick (mraft_start_and_tick). Host arrays: returns
+        (group_flags, (index, term, is_leader, err)), Start's outputs per group."""
+        G = self.G
+        if where == HOST:
+            leader_peer = np.ascontiguousarray(leader_peer, dtype=np.int32)
+            counts = np.ascontiguousarray(counts, dtype=np.int32)
+            if group_flags is None:
+                group_flags = np.zeros(G, dtype=np.int32)
+            outs = tuple(np.zeros(G, np.int32) for _ in range(4))
+        else:
+            import torch
+            outs = tuple(torch.empty(G, dtype=torch.int32, device=leader_peer.device) for _ in range(4))
+        _ck(self._lib.mraft_start_and_tick(self._h, ptr(leader_peer), ptr(counts), ptr(outs[0]), ptr(outs[1]),
+                                           ptr(outs[2]), ptr(outs[3]), ptr(group_flags), where),
+            "mraft_start_and_tick")
+        return group_flags, outs
+
     def replicate_tick_export(self, leader_peer, group_flags=None, commit=None, term_leader=None,
                               where: int = HOST):
         """The tick with the GetState export fused in: (flags, commit, term<<1|leader)."""

@@ -196,3 +196,51 @@ def test_auto_mode_gpu(shards):
             seen.add(e.tick_light_fallbacks())
             _start_all(e, o, lp, G, P, rng, 2)
         assert len(seen) > 1 and min(seen) >= 0, seen  # light ticks ran and were counted again
+
+
+def _oracle_start_and_tick(o, lp, counts, G, P):
+    """mraft_start over the groups' leader slots (counts != 0, leader_peer in
+    range), then the tick: the composition mraft_start_and_tick must equal."""
+    idx, term = np.full(G, -1, np.int32), np.full(G, -1, np.int32)
+    isl, err = np.zeros(G, np.int32), np.zeros(G, np.int32)
+    sel = np.flatnonzero((lp >= 0) & (lp < P) & (counts != 0))
+    if len(sel):
+        oi, ot, ol, oe = o.start((sel * P + lp[sel]).astype(np.int32), counts[sel].astype(np.int32))
+        idx[sel], term[sel], isl[sel], err[sel] = oi, ot, ol, oe
+    err[(lp >= P) & (counts != 0)] = 6  # MRAFT_ITEM_BAD_SLOT
+    return o.replicate_tick(lp), (idx, term, isl, err)
+
+
+@pytest.mark.parametrize("mode,P,shards", [(TICK_LIGHT, 5, 1), (TICK_LIGHT, 8, 2), (TICK_FULL, 5, 1),
+                                           (TICK_AUTO, 3, 2), (TICK_LIGHT, 2, 3), (TICK_AUTO, 1, 1)])
+def test_start_and_tick_gpu(mode, P, shards):
+    """mraft_start_and_tick (raft.go:90-104 at every group's leader, then the
+    tick) == mraft_start over those slots followed by mraft_replicate_tick on
+    the oracle, over ten steps: counts 0-4 with some negative (MRAFT_ITEM_BAD_SLOT)
+    and some past the ring's capacity (MRAFT_ITEM_LOG_FULL), leader moves,
+    idle and out-of-range leader_peer; Start inside the light launch (the
+    followers' copies of the new entries and a1's probe from currentTerm),
+    and as its own launch on the full tick's path."""
+    G, L = 700, 128
+    rng = np.random.default_rng(4400 + 10 * P + shards + mode)
+    st, lp, _ = synth_tick_state(G, P, L, seed=4400 + P)
+    o = Oracle(G, P, L, st)
+    with Engine(G, P, L) as e:
+        e.load_state(st)
+        e.set_tick_shards(min(shards, G))
+        e.set_tick_mode(mode)
+        for k in range(10):
+            counts = rng.integers(0, 5, size=G).astype(np.int32)
+            counts[rng.random(G) < 0.03] = -1
+            counts[rng.random(G) < 0.02] = L  # past any ring's capacity
+            lpk = lp.copy()
+            lpk[rng.random(G) < 0.03] = -1
+            lpk[rng.random(G) < 0.01] = P
+            gf, outs = e.start_and_tick(lpk, counts)
+            ogf, oouts = _oracle_start_and_tick(o, lpk, counts, G, P)
+            for a, b, name in zip(outs, oouts, ("index", "term", "is_leader", "err")):
+                assert np.array_equal(a, b), (k, name)
+            assert np.array_equal(gf, ogf), (k, "group flags")
+            assert_states_equal(e.store_state(), o.state(), G, P, L, f"start_and_tick step {k}")
+            moved = rng.random(G) < 0.05
+            lp = np.where(moved, rng.integers(0, P, size=G), lp).astype(np.int32)

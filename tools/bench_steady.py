@@ -20,7 +20,7 @@ def main():
     dev = torch.device("cuda", 0)
     st, lp, _ = synth_tick_state(G, P, L, seed=synth_seed(3), nthreads=16)
     master = {k: torch.from_numpy(v).to(dev) for k, v in st.items()}
-    copies = [{k: v.clone() for k, v in master.items()} for _ in range(2)]
+    copies = [{k: v.clone() for k, v in master.items()} for _ in range(3)]
     out = bench.steady_state(master, copies, np.asarray(lp), G, P, L, dev)
     print(json.dumps(out))
 

@@ -49,7 +49,7 @@ for st in ${DO:-tests bench}; do
       # the steady-state ticks alone, full and light (tools/bench_steady.py)
       echo "== steady"
       timeout -k 10 400 python3 tools/bench_steady.py > "$OUT/steady.json" 2> "$OUT/steady.err" || { tail -5 "$OUT/steady.err"; exit 1; }
-      python3 -c "import json; e=json.loads(open('$OUT/steady.json').read().strip().splitlines()[-1]); li=e['light']; print('full', round(e['tick_ms_steady'],4), 'light', round(li['tick_ms_steady'],4), 'x', round(li['speedup_tick_steady'],2), 'same', li['state_equals_full'], 'fb', li['fallback_groups_steps'])" ;;
+      python3 -c "import json; e=json.loads(open('$OUT/steady.json').read().strip().splitlines()[-1]); li=e['light']; print('full', round(e['tick_ms_steady'],4), 'light', round(li['tick_ms_steady'],4), 'x', round(li['speedup_tick_steady'],2), 'same', li['state_equals_full'], 'fb', li['fallback_groups_steps']); fu=e['fused']; print('per step: full start+tick', round(e['device_ms_per_step_steady'],4), 'light start+tick', round(li['device_ms_per_step_steady'],4), 'fused', round(fu['device_ms_per_step_steady'],4), 'same', fu['state_equals_full'])" ;;
     lighttests)
       # the whole tick-related GPU suite with every engine in MRAFT_TICK_LIGHT (tests/conftest.py)
       echo "== lighttests"

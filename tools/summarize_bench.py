@@ -34,3 +34,8 @@ if "steady_state_config3" in s:
     print("steady state tick ms: full", round(e["tick_ms_steady"], 4), "light", round(li.get("tick_ms_steady", 0), 4),
           "speedup", round(li.get("speedup_tick_steady", 0), 2), "same", li.get("state_equals_full"),
           "fallbacks", li.get("fallback_groups_steps", [])[:6], "...", li.get("fallback_groups_steps", [])[-2:])
+    fu = e.get("fused")
+    if fu:
+        print("steady state per step: start_and_tick (light)", round(fu["device_ms_per_step_steady"], 4),
+              "vs start+tick full", round(fu["vs_full_start_then_tick"], 2), "x, light",
+              round(fu["vs_light_start_then_tick"], 2), "x; same", fu["state_equals_full"])
