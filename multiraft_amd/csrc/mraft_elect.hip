@@ -46,6 +46,11 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     last = s.last[sl];
     lterm = term_at(s, sl, s.dummy[sl], s.head[sl], last);             // lastEntry, raft_log.go:50-53
   }
+  // votedFor as a bit: 1 << votedFor, 0 for -1, kVJunk for a value outside
+  // [-1, P) (no candidate ever equals it, as in Go's compare at :69-74)
+  constexpr int kVJunk = 0x100;
+  const int pb = 1 << p;
+  int vb = voted == -1 ? 0 : ((unsigned)voted < (unsigned)P ? 1 << voted : kVJunk);
   // The logs do not change during an election storm, so isLogUpToDate of
   // every candidate's (lastTerm, lastIndex) against this voter's
   // (raft_log.go:99-104) is fixed for the launch: bit c of upm.
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     if (isc) {                                                         // StartElection :6-17
       role = kCandidate;
       term += 1;
-      voted = p;
+      vb = pb;
       votes = 1;
       pd = 1;
     }
@@ -105,35 +110,36 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
     // round 5's loop walked the candidate mask with a ds_bpermute per
     // candidate in its dependent chain, profiles/r6_e1)
     {
+      // every lane writes one rank slot: a candidate its rank (args.Term, its
+      // bit), the others the slots past the segment's candidates (INT_MIN, bit
+      // 0: a delivery that changes nothing), so the loop needs no validity test
       const int ncand = __builtin_popcount(cm);
-      if (isc) {
-        const int rk = __builtin_popcount(cm & ((1 << p) - 1));
-        lds_rt[(threadIdx.x & ~7u) + rk] = at;
-        lds_rc[(threadIdx.x & ~7u) + rk] = (uint8_t)p;
-      }
+      const int rk = __builtin_popcount(cm & (pb - 1));
+      const int pos = isc ? rk : ncand + p - rk;
+      lds_rt[(threadIdx.x & ~7u) + pos] = isc ? at : INT32_MIN;
+      lds_rc[(threadIdx.x & ~7u) + pos] = (uint8_t)(isc ? pb : 0);
       __builtin_amdgcn_wave_barrier();
       const int4 ra = *reinterpret_cast<const int4 *>(&lds_rt[threadIdx.x & ~7u]);
       const int4 rb = *reinterpret_cast<const int4 *>(&lds_rt[(threadIdx.x & ~7u) + 4]);
       const unsigned long long rcs = *reinterpret_cast<const unsigned long long *>(&lds_rc[threadIdx.x & ~7u]);
       __builtin_amdgcn_wave_barrier();
       const int rt[8] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+      // A candidate's delivery to itself (cb == pb) changes nothing: its term
+      // is at >= cat, and at term == at its vote is already its own; the grant
+      // bit it sets in gm is masked out of its tally (om). So no c != p test.
 #pragma unroll
       for (int k = 0; k < P; ++k) {
         if (!__ballot(k < ncand)) break;
-        const bool valid = k < ncand;
-        const int c = (int)((rcs >> (8 * k)) & 0xffull);
+        const int cb = (int)((rcs >> (8 * k)) & 0xffull);
         const int cat = rt[k];
-        // conditions as bitwise (non-short-circuit) ops: no exec-mask region per
-        // candidate (round 6: 126 -> 77 SALU per round body, storm -1.5 %)
-        pmx = (valid & (c <= p)) ? max(pmx, cat) : pmx;
-        const bool h = act & valid & (c != p);                         // this voter handles c's RV
-        const bool gt = h & (cat > term);                              // :63-66
-        const bool ge = h & (cat >= term);                             // :59-62 (stale: no change)
+        pmx = cb <= pb ? max(pmx, cat) : pmx;                          // c <= p
+        const bool gt = cat > term;                                    // :63-66
+        const bool ge = cat >= term;                                   // :59-62 (stale: no change)
         term = gt ? cat : term;
-        voted = gt ? -1 : voted;
-        const bool grant = ge & ((voted == -1) | (voted == c)) & (((upm >> c) & 1) != 0);  // :69-74
-        voted = grant ? c : voted;
-        gm |= grant ? (1 << c) : 0;
+        vb = gt ? 0 : vb;
+        const bool grant = ge & (((vb & ~cb) | (cb & ~upm)) == 0);     // :69-74
+        vb = grant ? cb : vb;
+        gm |= grant ? cb : 0;
       }
       role = term > at ? kFollower : role;                             // :63-66 (some RV carried a higher term)
     }
@@ -168,13 +174,14 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
       tv = lds_cx[(threadIdx.x & ~7u) + min(spos, 7)];  // used only when spos < P
       const bool lead = ok0 && lpos < spos;
       const bool sd = ok0 && spos < lpos;
-      const int upto = lead ? (int)((2u << lpos) - 1u) : sd ? (int)((1u << spos) - 1u) : -1;
+      const int upos = lead ? lpos + 1 : spos;                          // < 32 when lead | sd
+      const int upto = (lead | sd) ? (int)((1u << (upos & 31)) - 1u) : -1;
       votes += ok0 ? __builtin_popcount(mine & om & upto) : 0;                // :31
       role = lead ? kLeader : sd ? kFollower : role;
       became |= (int)lead;
       fl |= lead ? MRAFT_G_ELECTED : 0;
       term = sd ? max(tv, pmx) : term;
-      voted = sd ? -1 : voted;
+      vb = sd ? 0 : vb;
       fl |= sd ? MRAFT_G_STEPPED_DOWN : 0;
     }
   }
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(256) void k_election_rounds(Dev s, const uint8_t *_
   }
   if (!act) return;
   s.term[sl] = term;
-  s.voted[sl] = voted;
+  s.voted[sl] = (vb & kVJunk) ? voted : (vb ? __builtin_ctz(vb) : -1);
   s.role[sl] = role;
   s.votes[sl] = votes;
   if (pd) mark_persist(s, sl, MRAFT_PERSIST_STATE);
