@@ -131,7 +131,8 @@ for st in ${DO:-tests bench}; do
         --output-format csv -d "$OUT/valu" -o valu -- python3 bench_election.py --no-cpu-baseline --steps 5 \
         > "$OUT/valu_bench.json" 2> "$OUT/valu_bench.err" || { tail -5 "$OUT/valu_bench.err"; exit 1; }
       timeout -k 10 300 python3 bench_election.py --no-cpu-baseline > "$OUT/election_bench.json" 2> "$OUT/election_bench.err" || exit 1
-      python3 tools/pmc_valu.py "$TAG" "$OUT/valu" "$OUT/election_bench.json" | tee "$OUT/pmc_valu.log" | grep -E "frac|busy|SQ_INSTS_VALU" ;;
+      python3 tools/pmc_valu.py "$TAG" "$OUT/valu" "$OUT/election_bench.json" | tee "$OUT/pmc_valu.log" | grep -E "frac|busy|SQ_INSTS_VALU"
+      cp profiles/pmc_valu_config5.json "$OUT/" ;;
     elect)
       # where the election storm's issue slots go: stall and LDS counters of
       # k_election_rounds<7>, one pass per counter group
