@@ -72,7 +72,10 @@ void launch_claim_ae(const mraft_ae_args *args, int64_t n, int64_t n_log, int L,
 // one 128-B line each) and its stripes: stripe x lists its deferred items at
 // defer[x * n] (the list buffer holds kAeStripes * n) and stages at
 // stage[x * capacity / kAeStripes].
-constexpr int kAeStripes = 8;
+#ifndef MRAFT_AE_STRIPES
+#define MRAFT_AE_STRIPES 8
+#endif
+constexpr int kAeStripes = MRAFT_AE_STRIPES;
 constexpr int kAeTotalWords = 16 + 2 * kAeStripes * 16;
 // The deferred launch's buffers and grid (mraft_kernels.hip "deferred
 // launch's fallback"): per item a 16-B record (writer, arrivals, run flag,
