@@ -397,17 +397,21 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
   const bool mrg = isf && !fb && !bel && n > 0;
   // successful replies: with at least P/2 of them the last evaluation of a1's
   // order statistic is `last` (so top = min(M*, last) = last); with none, a1
-  // never runs; in between the full tick decides
-  const int nsucc = __popcll(__ballot(isf && !fb && !bel) >> gbase & 0xffull);
-  bool gfb = ((__ballot(fb) >> gbase) & 0xffull) != 0 || (nsucc > 0 && nsucc < P / 2);
+  // never runs; in between (few) a1 runs on an order statistic that still
+  // holds older matchIndex words, settled below when it cannot pass commitIndex
+  const bool succ = isf && !fb && !bel;
+  const int nsucc = __popcll(__ballot(succ) >> gbase & 0xffull);
+  const bool few = nsucc > 0 && nsucc < P / 2;
+  bool gfb = ((__ballot(fb) >> gbase) & 0xffull) != 0;
   // Round trip 2 (groups still settling here): prevLogTerm at leader and
   // follower, a1's probe log[last] and each merging follower's first four
   // entries to append (its own lane loads the leader's words).
   const bool t2 = go && !gfb;
-  int pt = 0, ft = 0, probe = 0;
+  int pt = 0, ft = 0, probe = 0, mj = 0;
   int e4[4] = {0, 0, 0, 0};
   // (START: Indexes above last0 are the entries Start appends, currentTerm)
   if (t2) {
+    if (few && isf) mj = s.match[((long long)g * P + lp) * P + j];     // the leader's matchIndex[j]
     if (isf && !bel) {
       pt = (START && prev > last0) ? T : s.log[lrow + ring(prev + lb, L)];  // :49
       ft = s.log[f * L + ring(prev - fdummy + fhead, L)];                // :128
@@ -435,9 +439,37 @@ __global__ __launch_bounds__(64 * kLiteWaves, 8) void k_tick_lite(Dev s, const i
     s.last[sl] = last;
     if (s.pdirty) s.pdirty[sl] = rpd | MRAFT_PERSIST_STATE;             // :101
   }
-  int commit = c0;
+  int commit = c0, ftop = 0, pq = 0;
   gfb = gfb || ((__ballot(fb) >> gbase) & 0xffull) != 0;
-  if (go && !gfb && nsucc > 0 && last > c0) {                             // top = last (above)
+  if (__ballot(t2 && few)) {
+    // few successes (fewer than P/2): a1 runs after each of them (:78) on
+    // quorum_rt's order statistic — the (P/2)-th largest follower matchIndex —
+    // over words each success raises to `last`, the others' older words kept.
+    // With no success lowering its word (old <= last) the evaluations' tops
+    // rise to the last one's, so a1's ranges cover (commitIndex, top] and its
+    // probe of log[top] settles it as for top = last below; otherwise, over
+    // each follower's larger word, a bound on every evaluation's top that at
+    // or below commitIndex means a1 changes nothing. Else the full tick.
+    const int mm = isf ? (succ ? max(mj, last) : mj) : INT32_MIN;
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) c += (bc((int)isf, q) && bc(mm, q) >= mm) ? 1 : 0;  // followers at or above mine
+    int qv = (isf && c >= P / 2) ? mm : INT32_MIN;
+#pragma unroll
+    for (int q = 0; q < P; ++q) qv = max(qv, bc(qv, q));
+    const bool mono = ((__ballot(succ && mj > last) >> gbase) & 0xffull) == 0;
+    ftop = min(qv, last);
+    if (go && few && ftop > c0) {
+      if (!mono) gfb = true;
+      else if (j == lp) pq = (START && ftop > last0) ? T : s.log[lrow + ring(ftop + lb, L)];  // :98
+    }
+    const int pqv = bc(pq, lp);
+    if (go && few && !gfb && ftop > c0) {
+      if (pqv == T) commit = ftop;                                       // :98-100
+      else if (!(lsrt && pqv < T)) gfb = true;                           // a scan: the full tick
+    }
+  }
+  if (go && !gfb && nsucc > 0 && !few && last > c0) {                    // top = last (above)
     if (t == T) commit = last;                                           // :98-100
     else if (!(lsrt && t < T)) gfb = true;                               // a Figure-8 scan: the full tick
   }

@@ -143,6 +143,71 @@ def test_light_span_and_grid_stride_gpu():
             _start_all(e, o, lp, G, P, rng, 1)
 
 
+@pytest.mark.parametrize("P", [5, 7, 8])
+def test_light_few_successes_gpu(P):
+    """Groups where fewer than P/2 followers reply success and the others sit
+    ahead of the leader's nextIndex (prev below their dummy: IC_BELOW, the
+    reply dropped by the leader's gate, raft_append_entry.go:123-127): a1 runs
+    on an order statistic that still holds the others' older matchIndex
+    (:78, :89-105). The light launch settles the group when that statistic
+    cannot pass commitIndex or its top's term settles a1 (currentTerm, or
+    below it under terms_sorted), and lists it otherwise; the leader's
+    matchIndex words for those followers are drawn around commitIndex so
+    each happens, and some successes lower their word (old matchIndex above
+    last), where only the bound applies."""
+    G, L = 1024, 256
+    rng = np.random.default_rng(7700 + P)
+    st, lp, _ = synth_tick_state(G, P, L, seed=7700 + P)
+    o = Oracle(G, P, L, st)
+    for _ in range(3):  # steady on the oracle: followers caught up
+        o.replicate_tick(lp)
+        g = np.flatnonzero(lp >= 0)
+        o.start((g * P + lp[g]).astype(np.int32), rng.integers(1, 4, size=len(g)).astype(np.int32))
+    o.replicate_tick(lp)
+    s = {k: v.copy() for k, v in o.state().items()}
+    nx = s["next_index"].reshape(G * P, P)
+    mt = s["match_index"].reshape(G * P, P)
+    dm, hd, la, cm = s["dummy_index"], s["log_head"], s["last_index"], s["commit_index"]
+    changed = 0
+    for g in np.flatnonzero(lp >= 0)[::2]:
+        ld = g * P + lp[g]
+        fol = [j for j in range(P) if j != lp[g]]
+        nsucc = int(rng.integers(1, P // 2))  # 1 .. P/2 - 1 successes
+        ahead = rng.permutation(fol)[: len(fol) - nsucc]
+        ok = True
+        for j in ahead:
+            f = g * P + j
+            # the follower compacted to its last entry (ring mapping kept), the
+            # leader's nextIndex one below that dummy
+            if la[f] - 1 < dm[ld] or la[f] <= dm[f]:
+                ok = False
+                break
+        if not ok:
+            continue
+        for j in ahead:
+            f = g * P + j
+            hd[f] = (hd[f] + (la[f] - dm[f])) % L
+            dm[f] = la[f]
+            cm[f] = max(cm[f], dm[f])
+            nx[ld, j] = dm[f]
+            mt[ld, j] = max(0, cm[ld] + int(rng.integers(-3, 4)))
+        if rng.random() < 0.3:  # a success that lowers its matchIndex word (a bad-state leader)
+            sj = [j for j in fol if j not in set(ahead)][0]
+            mt[ld, sj] = la[ld] + 2
+        changed += 1
+    assert changed > 50
+    o2 = Oracle(G, P, L, s)
+    with Engine(G, P, L) as e:
+        e.load_state(s)
+        e.set_tick_mode(TICK_LIGHT)
+        for k in range(3):
+            gf = _step(e, o2, lp, G, P, L, f"few P={P} step {k}", export=(k == 1))
+            if k == 0:
+                fb = e.tick_light_fallbacks()
+                assert 0 <= fb < changed, (fb, changed)  # some of them settled in the light launch
+            _start_all(e, o2, lp, G, P, rng, 3)
+
+
 @pytest.mark.parametrize("j", [0, 5])
 def test_light_top_of_index_domain_gpu(j):
     """Steady ticks whose Indexes end within j of 2^31 - 2 (include/mraft.h: the
