@@ -358,7 +358,7 @@ def message_path_deferred(master, copies, lp, G, P, L, dev, steps=5):
     return out
 
 
-def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
+def steady_state(master, copies, lp, G, P, L, dev, steps=40, ss0=24, seed=0x5EAD):
     """Config #3 ticked in place: one state copy, and per
     step a Start of 1-4 entries at every leader (mraft_start, raft.go:90-104)
     then one mraft_replicate_tick — a heartbeat / append round of a running
@@ -417,7 +417,7 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
             marks[k][2].record(st)
         e.synchronize()
         return ([m[0].elapsed_time(m[1]) for m in marks], [m[1].elapsed_time(m[2]) for m in marks],
-                marks[2][0].elapsed_time(marks[-1][2]) / (steps - 2), gf.cpu().numpy())
+                marks[ss0][0].elapsed_time(marks[-1][2]) / (steps - ss0), gf.cpu().numpy())
 
     start_ms, tick_ms, span_ss, flags = timed(TICK_FULL, copies[0])
     log_full = int((oe.cpu().numpy() == 3).sum())
@@ -466,8 +466,11 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
         e.synchronize()
         empty.append(a.elapsed_time(b))
     e.close()
-    # steady state: the steps after the first two (the synthetic state's backlog merges there)
-    ss = slice(2, steps)
+    # steady state: the last steps - ss0 steps. The synthetic state's backlog
+    # (followers with conflicting or missing tails) is repaired over the first
+    # ~15 ticks: the light tick's fallback count per step drains to its floor
+    # (fallback_groups_steps), and the steps before carry that work
+    ss = slice(ss0, steps)
     tick_ss = float(np.mean(tick_ms[ss]))
     ltick_ss = float(np.mean(ltick_ms[ss]))
     bytes_ss = float(np.mean(4 * (words[ss, 0] + words[ss, 1])))
@@ -475,8 +478,8 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
     empty_ms = float(np.median(empty))
     return {"workload": "config #3 ticked in place: per step mraft_start of 1-4 entries at each of the %d leaders, "
                         "then one mraft_replicate_tick (no shards), %d steps back to back on one engine stream; "
-                        "steady state = steps 3..%d; top-level fields: the full tick (MRAFT_TICK_FULL, one "
-                        "launch), `light`: the same sequence with MRAFT_TICK_LIGHT" % (nl, steps, steps),
+                        "steady state = steps %d..%d (the backlog drained: fallback_groups_steps); top-level fields: the full tick (MRAFT_TICK_FULL, one "
+                        "launch), `light`: the same sequence with MRAFT_TICK_LIGHT" % (nl, steps, ss0 + 1, steps),
             "steps": steps, "tick_ms_steps": [round(x, 4) for x in tick_ms],
             "start_ms_mean": float(np.mean(start_ms)),
             "tick_ms_steady": tick_ss, "device_ms_per_step_steady": span_ss,
@@ -493,7 +496,7 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
                                  "leader_peer and exits) over the steady-state tick: the part of a steady tick a "
                                  "launch with no work already costs",
             "gaps_share_steady": 1.0 - (float(np.sum(tick_ms[ss])) + float(np.sum(start_ms[ss]))) /
-                                 (span_ss * (steps - 2)),
+                                 (span_ss * (steps - ss0)),
             "start_log_full_last_step": log_full,
             "groups_committed_last_step": int(((flags & 2) != 0).sum()),
             "light": {"what": "MRAFT_TICK_LIGHT: k_tick_lite (eight groups per wave; the steady-state groups "
@@ -512,10 +515,10 @@ def steady_state(master, copies, lp, G, P, L, dev, steps=24, seed=0x5EAD):
                               "tick's first launch, one call and one event per step (the same Starts and ticks as "
                               "above, on a third copy)",
                       "step_ms_steps": [round(x, 4) for x in fstep_ms],
-                      "device_ms_per_step_steady": float(np.mean(fstep_ms[2:])),
-                      "decisions_per_s_steady": G / (float(np.mean(fstep_ms[2:])) / 1e3),
-                      "vs_full_start_then_tick": span_ss / float(np.mean(fstep_ms[2:])),
-                      "vs_light_start_then_tick": lspan_ss / float(np.mean(fstep_ms[2:])),
+                      "device_ms_per_step_steady": float(np.mean(fstep_ms[ss])),
+                      "decisions_per_s_steady": G / (float(np.mean(fstep_ms[ss])) / 1e3),
+                      "vs_full_start_then_tick": span_ss / float(np.mean(fstep_ms[ss])),
+                      "vs_light_start_then_tick": lspan_ss / float(np.mean(fstep_ms[ss])),
                       "state_equals_full": fsame}}
 
 
