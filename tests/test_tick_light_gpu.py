@@ -143,7 +143,7 @@ def test_light_span_and_grid_stride_gpu():
             _start_all(e, o, lp, G, P, rng, 1)
 
 
-@pytest.mark.parametrize("P", [5, 7, 8])
+@pytest.mark.parametrize("P", [4, 5, 6, 7, 8])
 def test_light_few_successes_gpu(P):
     """Groups where fewer than P/2 followers reply success and the others sit
     ahead of the leader's nextIndex (prev below their dummy: IC_BELOW, the
