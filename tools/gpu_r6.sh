@@ -73,7 +73,7 @@ for st in ${DO:-tests bench}; do
         timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pst$i" -o p -- python3 tools/bench_steady.py \
           > "$OUT/pst$i.json" 2> "$OUT/pst$i.err" || { tail -5 "$OUT/pst$i.err"; exit 1; }
       done
-      python3 tools/pmc_kernels.py "$OUT/steady_counters.json" "$OUT"/pst[0-9]* --kernels "k_tick_lite<5>;k_tick_list<5>;k_tick_group<5, false>" | head -60 ;;
+      python3 tools/pmc_kernels.py "$OUT/steady_counters.json" "$OUT"/pst[0-9]* --kernels "k_tick_lite<5, false>;k_tick_lite<5, true>;k_tick_list<5>;k_tick_group<5, false>;k_tick_group<5, true>" | head -60 ;;
     abdeferred)
       # the deferred-heavy handle measurement per library variant (ABDEF_LIBS tags + in-tree)
       echo "== abdeferred ${ABDEF_LIBS:-}"
